@@ -1,0 +1,155 @@
+/*
+ * sphrt.h — C ABI of the MI355X-native spherical-grid raytracer (libsphrt.so, gfx950).
+ *
+ * This is the drop-in boundary for the hot path of Evidlo/sph_raytracer: ray <-> spherical-voxel
+ * intersection (sphere / cone / half-plane crossings), per-ray merge + forward fill + segment
+ * lengths, and the line-integral forward / adjoint.  The reference has no native boundary; its
+ * interface is the Python `Operator` (raytracer.py:647-755).  Each entry point below names the
+ * reference code it replaces.  The Python package `sph_raytracer_amd` binds these with ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Plain C types only.  Every large buffer is allocated by the caller (PyTorch-ROCm tensors) and
+ *    passed as a raw device pointer; the library never frees caller memory.  A plan owns only its
+ *    small boundary tables.
+ *  - `stream` is a hipStream_t passed as void*.  All work is stream-ordered; the only host sync in
+ *    the whole trace is the caller's read of the total segment count between count and fill.
+ *  - Return value: 0 on success, non-zero on error; sphrt_last_error() gives a message
+ *    (thread-local).  Functions never abort the process.
+ *  - Geometry is float64 (reference FTYPE = float64, raytracer.py:14).  Densities / images may be
+ *    float32 or float64; accumulation is always float64.
+ */
+#ifndef SPHRT_H
+#define SPHRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPHRT_MAX_DIMS 6
+
+/* Boundary description of a SphericalGrid (geometry.py:107-183).  All pointers are HOST memory;
+ * the trigonometric tables are computed by the caller with the same host library the reference
+ * uses (torch CPU: raytracer.py:373-375, 505-506), so every table entry is bit-identical. */
+typedef struct sphrt_grid_desc {
+    int32_t nr, ne, na;       /* voxels per axis: grid.shape.r/e/a                              */
+    const double *r_b;        /* nr+1 sphere radii, ascending            (geometry.py:158-161)  */
+    const double *e_b;        /* ne+1 cone angles from +Z                (geometry.py:165)      */
+    const double *a_b;        /* na+1 half-plane azimuths                (geometry.py:166)      */
+    const double *cos_e;      /* torch.cos(e_b)                          (raytracer.py:452)     */
+    const double *cos2_e;     /* torch.cos(e_b)**2                       (raytracer.py:373-375) */
+    const double *cos_a;      /* torch.cos(a_b)                          (raytracer.py:505)     */
+    const double *sin_a;      /* torch.sin(a_b)                          (raytracer.py:506)     */
+    int32_t a_wrap;           /* -a_b[0] == a_b[-1] == pi                (raytracer.py:528)     */
+    double close_tol;         /* finfo(ftype).resolution ** (1/3)        (raytracer.py:233-246) */
+    double plane_par_tol;     /* finfo(ftype).resolution                 (raytracer.py:521)     */
+} sphrt_grid_desc;
+
+typedef struct sphrt_plan sphrt_plan;
+
+/* Ray batch: `ndim`-dimensional broadcast shape; xs (...,3) f64 ray starts and rays (...,3) f64
+ * directions addressed with per-dim element strides (0 = broadcast dim), last dim contiguous.
+ * `start` holds the start voxel of every *unique* start as int32 (r, e, a, pad), addressed as
+ * start[4 * (xs_offset / 3)] — i.e. laid out like an un-broadcast, contiguous xs.  It replaces
+ * find_starts (raytracer.py:605-644), which the caller evaluates on the host once per unique
+ * start. */
+typedef struct sphrt_rays {
+    int32_t ndim;
+    int64_t shape[SPHRT_MAX_DIMS];
+    int64_t xs_stride[SPHRT_MAX_DIMS];
+    int64_t rays_stride[SPHRT_MAX_DIMS];
+    const double *xs;
+    const double *rays;
+    const int32_t *start;
+} sphrt_rays;
+
+/* ---- plan --------------------------------------------------------------------------------- */
+/* Replaces the per-call conversion of grid.r_b/e_b/a_b inside r_torch/e_torch/a_torch
+ * (raytracer.py:271-277, 353-361, 493-501).  `device` is the HIP device ordinal. */
+int sphrt_plan_create(const sphrt_grid_desc *grid, int device, sphrt_plan **out);
+int sphrt_plan_destroy(sphrt_plan *plan);
+/* Candidates per ray in the reference's concatenation (raytracer.py:92, 117-122):
+ * K = 2(nr+1) + 2(ne+1) + (na+1) + 1. */
+int64_t sphrt_plan_candidates(const sphrt_plan *plan);
+const char *sphrt_last_error(void);
+const char *sphrt_version(void);
+
+/* ---- per-family crossing solves (API-parity with r_torch / e_torch / a_torch) -------------- */
+/* family 0 = spheres  (r_torch, raytracer.py:248-325): t, region  (n, 2*(nr+1))
+ * family 1 = cones    (e_torch, raytracer.py:328-468): t, region  (n, 2*(ne+1))
+ * family 2 = planes   (a_torch, raytracer.py:471-552): t, region  (n, na+1)
+ * `neg` receives negative_crossing (int8, same shape).  Rays are normalised on private copies
+ * (the reference normalises the caller's tensor in place, raytracer.py:281/365). */
+int sphrt_solve(const sphrt_plan *plan, const sphrt_rays *rays, int family,
+                double *t, int32_t *region, int8_t *neg, void *stream);
+
+/* ---- trace to compact CSR (replaces trace_indices, raytracer.py:48-230) -------------------- */
+/* Every trace call takes a caller-allocated device workspace of
+ * sphrt_trace_workspace_bytes(plan, n) bytes: it holds the list of rays whose crossings tie
+ * exactly in a way that makes the result depend on the reference's (unstable, libstdc++
+ * introsort) tie order, and the scratch of the exact kernel that replays that order. */
+size_t sphrt_trace_workspace_bytes(const sphrt_plan *plan, int64_t n);
+/* Pass 1: number of non-zero-length, in-grid segments of every ray (int32, n = prod(shape)). */
+int sphrt_trace_count(const sphrt_plan *plan, const sphrt_rays *rays, int32_t *counts,
+                      void *workspace, size_t workspace_size, void *stream);
+/* Exclusive scan counts -> row_ptr (n+1, int64).  `workspace` must hold
+ * sphrt_scan_workspace_bytes(n) bytes.  row_ptr[n] is the total segment count. */
+size_t sphrt_scan_workspace_bytes(int64_t n);
+int sphrt_scan_counts(const int32_t *counts, int64_t n, int64_t *row_ptr, void *workspace,
+                      void *stream);
+/* Pass 2: per-segment linear voxel index ((r*ne + e)*na + a) and length, in ray order and, per
+ * ray, in order of increasing distance.  Equivalent to the reference's (regs, lens) with
+ * zero-length and invalid entries dropped (raytracer.py:131-173). */
+int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64_t *row_ptr,
+                     int32_t *vox, double *len, void *workspace, size_t workspace_size,
+                     void *stream);
+
+/* ---- static work partition of a CSR for the apply kernels -------------------------------- */
+/* block_lo[b] = first ray whose row starts at or after b*seg_per_block, b = 0..nblocks
+ * (nblocks = row_ptr[n] / seg_per_block + 1; block_lo has nblocks+1 entries). */
+int sphrt_partition(const int64_t *row_ptr, int64_t n, int64_t seg_per_block, int64_t *block_lo,
+                    int64_t nblocks, void *stream);
+
+/* ---- forward line integral on the CSR (replaces Operator.__call__, raytracer.py:692-713) -- */
+/* out[c*out_chan_stride + i] = sum_s density[c*chan_stride + vox[s]] * len[s] over ray i's row.
+ * If ray_chan_div > 0, ray i only sees channel c = i / ray_chan_div (dynamic grid paired with a
+ * ViewGeomCollection, raytracer.py:705-706) and n_chan must be 1 in the call (the channel is
+ * derived); otherwise every ray is integrated for all n_chan channels (static multichannel). */
+int sphrt_forward_f32(const int64_t *row_ptr, const int32_t *vox, const double *len, int64_t n,
+                      const int64_t *block_lo, int64_t nblocks, int64_t seg_per_block,
+                      const float *density, int64_t n_chan, int64_t chan_stride,
+                      int64_t ray_chan_div, float *out, int64_t out_chan_stride, void *stream);
+int sphrt_forward_f64(const int64_t *row_ptr, const int32_t *vox, const double *len, int64_t n,
+                      const int64_t *block_lo, int64_t nblocks, int64_t seg_per_block,
+                      const double *density, int64_t n_chan, int64_t chan_stride,
+                      int64_t ray_chan_div, double *out, int64_t out_chan_stride, void *stream);
+
+/* ---- adjoint / back-projection (replaces Operator.T, raytracer.py:715-748, and the autograd
+ * backward of raytracer.py:710) ------------------------------------------------------------ */
+/* acc[c*chan_stride + vox[s]] += y[c*y_chan_stride + i] * len[s], float64 atomics into a zeroed
+ * float64 accumulator `acc` (caller-allocated).  Same channel rules as forward. */
+int sphrt_adjoint_accumulate(const int64_t *row_ptr, const int32_t *vox, const double *len,
+                             int64_t n, const int64_t *block_lo, int64_t nblocks,
+                             int64_t seg_per_block, const void *y, int y_is_f64, int64_t n_chan,
+                             int64_t y_chan_stride, int64_t ray_chan_div, double *acc,
+                             int64_t chan_stride, void *stream);
+/* dst[i] = (float)src[i] — rounding the float64 accumulator to a float32 result. */
+int sphrt_f64_to_f32(const double *src, float *dst, int64_t n, void *stream);
+
+/* ---- fused no-store mode: trace + integrate in one pass (nothing persisted) --------------- */
+int sphrt_trace_integrate_f32(const sphrt_plan *plan, const sphrt_rays *rays,
+                              const float *density, int64_t n_chan, int64_t chan_stride,
+                              int64_t ray_chan_div, float *out, int64_t out_chan_stride,
+                              void *workspace, size_t workspace_size, void *stream);
+int sphrt_trace_integrate_f64(const sphrt_plan *plan, const sphrt_rays *rays,
+                              const double *density, int64_t n_chan, int64_t chan_stride,
+                              int64_t ray_chan_div, double *out, int64_t out_chan_stride,
+                              void *workspace, size_t workspace_size, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPHRT_H */

@@ -1,0 +1,108 @@
+"""ctypes binding of libsphrt.so (the C ABI declared in include/sphrt.h).
+
+The library is built in-tree by ``sph_raytracer_amd.build`` (hipcc, gfx950) and loaded *after*
+torch, so it binds to the HIP runtime torch already loaded (same soname ``libamdhip64.so.7``) and
+can run on torch's streams and allocations.  There is no fallback: if the library or a GPU is
+missing, every compute entry point raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'lib', 'libsphrt.so')
+MAX_DIMS = 6
+
+c_i32, c_i64, c_dbl, c_vp, c_int = (ctypes.c_int32, ctypes.c_int64, ctypes.c_double,
+                                    ctypes.c_void_p, ctypes.c_int)
+
+
+class GridDesc(ctypes.Structure):
+    _fields_ = [('nr', c_i32), ('ne', c_i32), ('na', c_i32),
+                ('r_b', c_vp), ('e_b', c_vp), ('a_b', c_vp),
+                ('cos_e', c_vp), ('cos2_e', c_vp), ('cos_a', c_vp), ('sin_a', c_vp),
+                ('a_wrap', c_i32), ('close_tol', c_dbl), ('plane_par_tol', c_dbl)]
+
+
+class RayBatch(ctypes.Structure):
+    _fields_ = [('ndim', c_i32),
+                ('shape', c_i64 * MAX_DIMS),
+                ('xs_stride', c_i64 * MAX_DIMS),
+                ('rays_stride', c_i64 * MAX_DIMS),
+                ('xs', c_vp), ('rays', c_vp), ('start', c_vp)]
+
+
+# (name, restype, argtypes) — mirrors include/sphrt.h one to one
+_SIGNATURES = [
+    ('sphrt_plan_create', c_int, [ctypes.POINTER(GridDesc), c_int, ctypes.POINTER(c_vp)]),
+    ('sphrt_plan_destroy', c_int, [c_vp]),
+    ('sphrt_plan_candidates', c_i64, [c_vp]),
+    ('sphrt_last_error', ctypes.c_char_p, []),
+    ('sphrt_version', ctypes.c_char_p, []),
+    ('sphrt_solve', c_int, [c_vp, ctypes.POINTER(RayBatch), c_int, c_vp, c_vp, c_vp, c_vp]),
+    ('sphrt_trace_workspace_bytes', ctypes.c_size_t, [c_vp, c_i64]),
+    ('sphrt_trace_count', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_vp, ctypes.c_size_t,
+                                  c_vp]),
+    ('sphrt_scan_workspace_bytes', ctypes.c_size_t, [c_i64]),
+    ('sphrt_scan_counts', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
+    ('sphrt_trace_fill', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_vp, c_vp, c_vp,
+                                 ctypes.c_size_t, c_vp]),
+    ('sphrt_partition', c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    ('sphrt_forward_f32', c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                  c_i64, c_i64, c_vp, c_i64, c_vp]),
+    ('sphrt_forward_f64', c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
+                                  c_i64, c_i64, c_vp, c_i64, c_vp]),
+    ('sphrt_adjoint_accumulate', c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp,
+                                         c_int, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    ('sphrt_f64_to_f32', c_int, [c_vp, c_vp, c_i64, c_vp]),
+    ('sphrt_trace_integrate_f32', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_i64, c_i64,
+                                          c_i64, c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
+    ('sphrt_trace_integrate_f64', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_i64, c_i64,
+                                          c_i64, c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
+]
+EXPORTED = [s[0] for s in _SIGNATURES]
+
+_lib = None
+
+
+def load():
+    """Load libsphrt.so (once).  Raises RuntimeError if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f'sph_raytracer_amd: HIP library not found at {LIB_PATH}; build it with '
+            '`python -m sph_raytracer_amd.build` (hipcc --offload-arch=gfx950). '
+            'There is no CPU fallback.')
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, res, args in _SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = load().sphrt_last_error().decode(errors='replace')
+        raise RuntimeError(f'{what} failed: {msg}')
+
+
+def require_gpu():
+    """The device every kernel runs on.  No GPU -> loud failure (no CPU fallback)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError('sph_raytracer_amd requires a ROCm GPU (MI355X / gfx950); '
+                           'torch.cuda.is_available() is False and there is no CPU fallback.')
+    load()
+    return torch.device('cuda', torch.cuda.current_device())
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)

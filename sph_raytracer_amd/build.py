@@ -1,0 +1,63 @@
+"""Build libsphrt.so in-tree for gfx950 with hipcc (no torch extension, no JIT cache).
+
+    python -m sph_raytracer_amd.build [--verbose]
+
+The library goes to sph_raytracer_amd/lib/libsphrt.so, which travels with the repo snapshot to
+the GPU box (it is git-ignored, not gpurun-ignored).  Device code is compiled with
+-ffp-contract=off: the solver's fused multiply-adds are explicit (csrc/solve.hpp).
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, 'csrc')
+OUT = os.path.join(HERE, 'lib', 'libsphrt.so')
+SOURCES = ['api.hip', 'trace.hip']
+HEADERS = ['common.hpp', 'solve.hpp']
+ARCH = os.environ.get('SPHRT_ARCH', 'gfx950')
+
+
+def hipcc():
+    for cand in (os.environ.get('HIPCC'), '/opt/rocm/bin/hipcc', shutil.which('hipcc')):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError('hipcc not found (ROCm 7.x expected under /opt/rocm)')
+
+
+def command(out=OUT, extra=()):
+    return [hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared',
+            '-ffp-contract=off', '-munsafe-fp-atomics',
+            '-I', os.path.join(ROOT, 'include'), '-I', CSRC,
+            *extra, '-o', out] + [os.path.join(CSRC, s) for s in SOURCES]
+
+
+def _stale(out):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', 'sphrt.h'),
+                                                                   os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    if not force and not _stale(OUT):
+        return OUT
+    cmd = command()
+    if verbose:
+        print(' '.join(cmd))
+    tmp = OUT + '.tmp'
+    cmd[cmd.index(OUT)] = tmp
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f'hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}')
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == '__main__':
+    print(build(force='--force' in sys.argv, verbose='--verbose' in sys.argv))

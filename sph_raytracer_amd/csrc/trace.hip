@@ -1,0 +1,711 @@
+// trace.hip — fused per-ray trace on gfx950 (replaces trace_indices, raytracer.py:48-230).
+//
+// The reference materialises every ray's K = 2(nr+1)+2(ne+1)+(na+1)+1 candidate crossings,
+// sorts them, forward-fills three (K,)-long region rows and differences the distances.  Here a
+// tile of 64 rays is screened one ray per lane; every ray that can produce a segment is then
+// traced by the whole wave:
+//   1. lanes solve disjoint boundaries of each family (solve.hpp) and append the finite,
+//      non-negative crossings to a per-wave LDS list (ballot + mbcnt compaction); the most
+//      negative finite distance is reduced across the wave (it bounds the behind-start segment);
+//   2. the list is sorted by (distance, candidate index) — a total order equal to a stable sort
+//      of the reference's concatenation — in registers (<= 512 entries) or in LDS;
+//   3. 64-entry chunks are scanned (forward fill of the r/e/a rows), differenced and the
+//      non-zero in-grid segments compacted, in order, back into LDS;
+//   4. depending on MODE the segments are counted, copied to the CSR, or integrated against
+//      the density right away (no-store mode).
+// Nothing of size K ever reaches HBM.
+//
+// Exact ties.  The reference orders equal distances the way libstdc++'s introsort happens to
+// (torch.sort is unstable, raytracer.py:131).  That order only matters when two crossings that
+// update the same region row coincide exactly — in practice a ray that starts exactly on a
+// boundary (e.g. an orbit view at azimuth 0 with a boundary at 0).  The wave path detects such
+// tie groups and defers the ray to exact_kernel, which rebuilds all K candidates in the
+// reference's concatenation order, runs the emulated introsort (introsort.hpp) and walks the
+// sorted list exactly like trace_indices.  Deferred rays are rare; the list lives in workspace.
+#include "common.hpp"
+#include "introsort.hpp"
+#include "solve.hpp"
+
+namespace sphrt {
+
+enum { MODE_COUNT = 0, MODE_FILL = 1, MODE_INTEGRATE = 2 };
+constexpr int kNone = 0x7fffffff;  // "no update" in the forward-fill scans
+constexpr int kWavesPerBlock = 4;
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
+
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+    return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+// inclusive scan with op(a, b) = (b != none) ? b : a  — "last update wins" forward fill
+__device__ __forceinline__ int scan_last(int v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int u = __shfl_up(v, off);
+        if (lane >= off && v == kNone) v = u;
+    }
+    return v;
+}
+
+// ---- sorting of (key = distance bits, pay = candidate<<16 | region+2) pairs ---------------
+__device__ __forceinline__ bool pair_less(uint64_t ka, uint32_t pa, uint64_t kb, uint32_t pb) {
+    return ka < kb || (ka == kb && pa < pb);
+}
+
+// One compare-exchange layer of the ascending-only ("flip") bitonic network over 64*M elements,
+// element e = i*64 + lane; partner = e ^ mask.  `mask` is a compile-time constant after unroll.
+template <int M>
+__device__ __forceinline__ void cas_layer(uint64_t (&k)[M], uint32_t (&p)[M], int mask,
+                                          int lane) {
+    uint64_t nk[M];
+    uint32_t np[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int pi = i ^ (mask >> 6);
+        const int pl = lane ^ (mask & 63);
+        uint64_t ok;
+        uint32_t op;
+        if ((mask & 63) == 0) {
+            ok = k[pi];
+            op = p[pi];
+        } else {
+            ok = __shfl(k[pi], pl);
+            op = __shfl(p[pi], pl);
+        }
+        const int e = i * 64 + lane;
+        const int pe = pi * 64 + pl;
+        bool take = (e < pe) ? pair_less(ok, op, k[i], p[i]) : pair_less(k[i], p[i], ok, op);
+        nk[i] = take ? ok : k[i];
+        np[i] = take ? op : p[i];
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        k[i] = nk[i];
+        p[i] = np[i];
+    }
+}
+
+template <int M>
+__device__ void sort_regs(uint64_t* keys, uint32_t* pays, int F, int lane) {
+    uint64_t k[M];
+    uint32_t p[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int e = i * 64 + lane;
+        const bool r = e < F;
+        k[i] = r ? keys[e] : ~0ull;
+        p[i] = r ? pays[e] : ~0u;
+    }
+    constexpr int P = 64 * M;
+#pragma unroll
+    for (int kk = 2; kk <= P; kk <<= 1) {
+        cas_layer<M>(k, p, kk - 1, lane);  // flip: mirror partner inside the 2-block
+#pragma unroll
+        for (int j = kk >> 2; j > 0; j >>= 1) cas_layer<M>(k, p, j, lane);
+    }
+    wave_sync();
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int e = i * 64 + lane;
+        if (e < F) {
+            keys[e] = k[i];
+            pays[e] = p[i];
+        }
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ void cas_lds(uint64_t* keys, uint32_t* pays, int i, int l) {
+    uint64_t ki = keys[i], kl = keys[l];
+    uint32_t pi = pays[i], pl = pays[l];
+    if (pair_less(kl, pl, ki, pi)) {
+        keys[i] = kl; pays[i] = pl;
+        keys[l] = ki; pays[l] = pi;
+    }
+}
+// Same network in LDS for long lists; virtual +inf padding beyond F never moves (ascending-only
+// comparators), so storage is exactly F entries.
+__device__ void sort_lds(uint64_t* keys, uint32_t* pays, int F, int lane) {
+    int P = 1;
+    while (P < F) P <<= 1;
+    for (int kk = 2; kk <= P; kk <<= 1) {
+        const int half = kk >> 1;
+        for (int q = lane; q < (P >> 1); q += 64) {
+            const int blk = q / half, off = q - blk * half;
+            const int i = blk * kk + off, l = blk * kk + kk - 1 - off;
+            if (l < F) cas_lds(keys, pays, i, l);
+        }
+        wave_sync();
+        for (int j = kk >> 2; j > 0; j >>= 1) {
+            for (int q = lane; q < (P >> 1); q += 64) {
+                const int i = (q / j) * 2 * j + (q % j), l = i + j;
+                if (l < F) cas_lds(keys, pays, i, l);
+            }
+            wave_sync();
+        }
+    }
+}
+
+template <typename T>
+struct TraceOut {
+    int32_t* counts;          // COUNT
+    const int64_t* row_ptr;   // FILL
+    int32_t* vox;
+    double* len;
+    const T* density;         // INTEGRATE
+    int64_t n_chan, chan_stride, ray_chan_div;
+    T* out;
+    int64_t out_chan_stride;
+    unsigned long long* n_deferred;  // workspace: deferred-ray counter
+    int64_t* deferred;               // workspace: deferred ray ids
+};
+
+// region rows a candidate updates: bit0 r, bit1 e, bit2 a (start entry: all)
+__device__ __forceinline__ int update_mask(uint32_t pay, int r_lim, int e_lim, int start_c) {
+    const int cand = (int)(pay >> 16);
+    const int reg = (int)(pay & 0xffffu) - 2;
+    if (cand == start_c) return 7;
+    if (cand < r_lim) return 1;
+    if (reg == -2) return 0;
+    return cand < e_lim ? 2 : 4;
+}
+
+__device__ __forceinline__ int scan_max(int v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int u = __shfl_up(v, off);
+        if (lane >= off) v = max(v, u);
+    }
+    return v;
+}
+
+// Does any group of exactly equal distances hold two crossings that update a region row?  Then
+// the result depends on the reference's tie order (only updater/updater ties can change a row's
+// final value within the group; the segments inside a group have zero length).
+__device__ bool ambiguous_ties(const uint64_t* keys, const uint32_t* pays, int F, int lane,
+                               int r_lim, int e_lim, int start_c) {
+    bool any = false;
+    for (int c0 = 1; c0 < F; c0 += 64) {
+        const int e = c0 + lane;
+        any |= __ballot(e < F && keys[e] == keys[e - 1]) != 0;
+    }
+    if (!any) return false;
+    int grp = 0, last_upd = -1;   // carried across chunks
+    bool amb = false;
+    for (int c0 = 0; c0 < F; c0 += 64) {
+        const int e = c0 + lane;
+        const bool real = e < F;
+        const bool gs = real && (e == 0 || keys[e] != keys[e - 1]);
+        const bool upd = real && update_mask(pays[e], r_lim, e_lim, start_c) != 0;
+        int g = scan_max(gs ? e : -1, lane);
+        g = max(g, grp);
+        const int u_inc = max(scan_max(upd ? e : -1, lane), last_upd);
+        int u_exc = __shfl_up(u_inc, 1);
+        if (lane == 0) u_exc = last_upd;
+        amb |= upd && u_exc >= g;
+        grp = __shfl(g, 63);
+        last_upd = __shfl(u_inc, 63);
+    }
+    return __ballot(amb) != 0;
+}
+
+__device__ __forceinline__ void load_ray(const RaysDev& R, int64_t i, double* x, double* d,
+                                         int* s) {
+    int64_t xo = 0, ro = 0, rem = i;
+#pragma unroll
+    for (int dd = kMaxDims - 1; dd >= 0; --dd) {
+        if (dd < R.ndim) {
+            const int64_t sz = R.shape[dd];
+            const int64_t c = rem % sz;
+            rem /= sz;
+            xo += c * R.xs_stride[dd];
+            ro += c * R.rays_stride[dd];
+        }
+    }
+    x[0] = R.xs[xo]; x[1] = R.xs[xo + 1]; x[2] = R.xs[xo + 2];
+    d[0] = R.rays[ro]; d[1] = R.rays[ro + 1]; d[2] = R.rays[ro + 2];
+    const int32_t* sp = R.start + 4 * (xo / 3);
+    s[0] = sp[0]; s[1] = sp[1]; s[2] = sp[2];
+}
+
+// Trace ray `ray` (wave-uniform) with the whole wave.  keys/pays: this wave's LDS list.
+template <int MODE, typename T>
+__device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const int se,
+                          const int sa, const int64_t ray, uint64_t* keys, uint32_t* pays,
+                          const int lane, const TraceOut<T>& o) {
+    // ---- 1. crossings -> LDS list (finite, t >= 0), min finite negative distance ----------
+    int base = 0;
+    double tneg = kInf;
+    auto note = [&](double t) {
+        if (t < 0.0 && __builtin_isfinite(t)) tneg = fmin(tneg, t);
+    };
+    auto push = [&](bool has, double t, int cand, int reg) {
+        const uint64_t m = __ballot(has);
+        if (has) {
+            const int pos = base + __popcll(m & lanemask_lt(lane));
+            keys[pos] = (uint64_t)__double_as_longlong(t + 0.0);  // -0 -> +0
+            pays[pos] = ((uint32_t)cand << 16) | (uint32_t)(reg + 2);
+        }
+        base += __popcll(m);
+    };
+    auto keep = [](double t) { return __builtin_isfinite(t) && !(t < 0.0); };
+
+    const int nbr = G.nbr, nbe = G.nbe, nba = G.nba;
+    for (int j0 = 0; j0 < nbr; j0 += 64) {
+        const int j = j0 + lane;
+        const bool v = j < nbr;
+        double ti = kInf, to = kInf;
+        int ri = 0, ro = 0, ni, no;
+        if (v) sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
+        note(ti);
+        note(to);
+        push(v && keep(ti), ti, j, ri);
+        push(v && keep(to), to, nbr + j, ro);
+    }
+    const int ce0 = 2 * nbr;
+    for (int j0 = 0; j0 < nbe; j0 += 64) {
+        const int j = j0 + lane;
+        const bool v = j < nbe;
+        double ta = kInf, tb = kInf;
+        int ra = 0, rb = 0, na_, nb_;
+        if (v) cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
+        note(ta);
+        note(tb);
+        push(v && keep(ta), ta, ce0 + j, ra);
+        push(v && keep(tb), tb, ce0 + nbe + j, rb);
+    }
+    const int ca0 = 2 * nbr + 2 * nbe;
+    for (int j0 = 0; j0 < nba; j0 += 64) {
+        const int j = j0 + lane;
+        const bool v = j < nba;
+        double t = kInf;
+        int r = 0, ng;
+        if (v) plane_solve(G, g, j, t, r, ng);
+        note(t);
+        push(v && keep(t), t, ca0 + j, r);
+    }
+    push(lane == 0, 0.0, G.K - 1, 0);  // the start entry (raytracer.py:111-122)
+    const int F = base;
+    tneg = wave_min(tneg);
+    wave_sync();
+
+    // ---- 2. sort by (distance, candidate) ------------------------------------------------
+    if (F <= 64) sort_regs<1>(keys, pays, F, lane);
+    else if (F <= 128) sort_regs<2>(keys, pays, F, lane);
+    else if (F <= 256) sort_regs<4>(keys, pays, F, lane);
+    else if (F <= 512) sort_regs<8>(keys, pays, F, lane);
+    else sort_lds(keys, pays, F, lane);
+
+    const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe, start_c = G.K - 1;
+    if (ambiguous_ties(keys, pays, F, lane, r_lim, e_lim, start_c)) {
+        if (lane == 0) {
+            const unsigned long long q = atomicAdd(o.n_deferred, 1ull);
+            o.deferred[q] = ray;
+        }
+        wave_sync();
+        return;
+    }
+
+    // ---- 3. forward fill, lengths, compaction ----------------------------------------------
+    const bool start_ok = sr >= 0 && sr < G.nr && se >= 0 && se < G.ne && sa >= 0 && sa < G.na;
+    // every distance behind the start is integrated in the start voxel (raytracer.py:126,140)
+    const int head = (start_ok && tneg < 0.0) ? 1 : 0;
+    double* seg_len = reinterpret_cast<double*>(keys);
+    int32_t* seg_vox = reinterpret_cast<int32_t*>(pays);
+    int cr = sr, cE = se, cA = sa;  // state before the first sorted entry
+    int nseg = 0;
+    for (int c0 = 0; c0 < F; c0 += 64) {
+        const int e = c0 + lane;
+        const bool real = e < F;
+        uint64_t k = 0;
+        uint32_t p = 0;
+        double tn = kInf;
+        if (real) {
+            k = keys[e];
+            p = pays[e];
+            if (e + 1 < F) tn = __longlong_as_double((long long)keys[e + 1]);
+        }
+        wave_sync();
+        int ur = kNone, ue = kNone, ua = kNone;
+        if (real) {
+            const int cand = (int)(p >> 16);
+            const int reg = (int)(p & 0xffffu) - 2;
+            if (cand == start_c) {
+                ur = sr; ue = se; ua = sa;
+            } else if (cand < r_lim) {
+                ur = reg;
+            } else if (cand < e_lim) {
+                if (reg != -2) ue = reg;
+            } else {
+                if (reg != -2) ua = reg;
+            }
+        }
+        ur = scan_last(ur, lane);
+        ue = scan_last(ue, lane);
+        ua = scan_last(ua, lane);
+        if (ur == kNone) ur = cr;
+        if (ue == kNone) ue = cE;
+        if (ua == kNone) ua = cA;
+        cr = __shfl(ur, 63);
+        cE = __shfl(ue, 63);
+        cA = __shfl(ua, 63);
+        const double t = __longlong_as_double((long long)k);
+        const double len = tn - t;
+        const bool ok = real && len > 0.0 && __builtin_isfinite(len) && ur >= 0 && ur < G.nr &&
+                        ue >= 0 && ue < G.ne && ua >= 0 && ua < G.na;
+        const uint64_t m = __ballot(ok);
+        if (MODE != MODE_COUNT && ok) {
+            const int pos = nseg + __popcll(m & lanemask_lt(lane));
+            seg_len[pos] = len;
+            seg_vox[pos] = (ur * G.ne + ue) * G.na + ua;
+        }
+        nseg += __popcll(m);
+        wave_sync();
+    }
+
+    // ---- 4. emit ---------------------------------------------------------------------------
+    if (MODE == MODE_COUNT) {
+        if (lane == 0) o.counts[ray] = head + nseg;
+    } else if (MODE == MODE_FILL) {
+        const int64_t r0 = o.row_ptr[ray];
+        if (head && lane == 0) {
+            o.vox[r0] = (sr * G.ne + se) * G.na + sa;
+            o.len[r0] = -tneg;
+        }
+        for (int q = lane; q < nseg; q += 64) {
+            o.vox[r0 + head + q] = seg_vox[q];
+            o.len[r0 + head + q] = seg_len[q];
+        }
+    } else {
+        const int svox = (sr * G.ne + se) * G.na + sa;
+        int64_t c_lo = 0, c_hi = o.n_chan;
+        if (o.ray_chan_div > 0) {
+            c_lo = ray / o.ray_chan_div;
+            c_hi = c_lo + 1;
+        }
+        for (int64_t c = c_lo; c < c_hi; ++c) {
+            const T* rho = o.density + c * o.chan_stride;
+            double acc = 0.0;
+            if (head && lane == 0) acc = (double)rho[svox] * (-tneg);
+            for (int q = lane; q < nseg; q += 64) acc += (double)rho[seg_vox[q]] * seg_len[q];
+            acc = wave_sum(acc);
+            const int64_t oc = (o.ray_chan_div > 0) ? 0 : c;
+            if (lane == 0) o.out[oc * o.out_chan_stride + ray] = (T)acc;
+        }
+    }
+    wave_sync();
+}
+
+template <int MODE, typename T>
+__global__ __launch_bounds__(256) void trace_kernel(GridDev G, RaysDev R, TraceOut<T> o,
+                                                    int cap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    uint64_t* keys = reinterpret_cast<uint64_t*>(smem) + (size_t)wid * cap;
+    uint32_t* pays =
+        reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(smem) + (size_t)kWavesPerBlock * cap) +
+        (size_t)wid * cap;
+    const int64_t ntiles = (R.n + 63) / 64;
+    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid; tile < ntiles;
+         tile += (int64_t)gridDim.x * kWavesPerBlock) {
+        const int64_t ray = tile * 64 + lane;
+        const bool active = ray < R.n;
+        double x[3] = {0, 0, 0}, d[3] = {0, 0, 1};
+        int s[3] = {-1, -1, -1};
+        if (active) load_ray(R, ray, x, d, s);
+        const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
+        // A ray produces a non-zero segment only if it reaches the outer sphere or starts in a
+        // voxel: otherwise every r-row value stays the (invalid) start region.  t1c is NaN for
+        // every shell when it is NaN for the outermost (monotone in R), tangents excluded.
+        const double t1c_outer = __builtin_sqrt(G.r_outer * G.r_outer - g.dd * g.dd);
+        const bool start_r_ok = s[0] >= 0 && s[0] < G.nr;
+        const bool hit = active && !(!start_r_ok && __builtin_isnan(t1c_outer));
+        if (active && !hit) {
+            if (MODE == MODE_COUNT) o.counts[ray] = 0;
+            if (MODE == MODE_INTEGRATE) {
+                int64_t c_lo = 0, c_hi = o.n_chan;
+                if (o.ray_chan_div > 0) { c_lo = 0; c_hi = 1; }
+                for (int64_t c = c_lo; c < c_hi; ++c) o.out[c * o.out_chan_stride + ray] = (T)0;
+            }
+        }
+        uint64_t todo = __ballot(hit);
+        while (todo) {
+            const int src = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            RayGeo gw;
+            gw.x0 = __shfl(g.x0, src); gw.x1 = __shfl(g.x1, src); gw.x2 = __shfl(g.x2, src);
+            gw.u0 = __shfl(g.u0, src); gw.u1 = __shfl(g.u1, src); gw.u2 = __shfl(g.u2, src);
+            gw.w0 = __shfl(g.w0, src); gw.w1 = __shfl(g.w1, src); gw.w2 = __shfl(g.w2, src);
+            gw.tc = __shfl(g.tc, src); gw.dd = __shfl(g.dd, src);
+            gw.nx2 = __shfl(g.nx2, src); gw.wx = __shfl(g.wx, src);
+            const int sr = __shfl(s[0], src), se = __shfl(s[1], src), sa = __shfl(s[2], src);
+            trace_one<MODE, T>(G, gw, sr, se, sa, tile * 64 + src, keys, pays, lane, o);
+        }
+    }
+}
+
+// ---- per-family solves for the r_torch / e_torch / a_torch API ------------------------------
+__global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int family, double* t,
+                                                    int32_t* region, int8_t* neg) {
+    const int64_t ray = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (ray >= R.n) return;
+    double x[3], d[3];
+    int s[3];
+    load_ray(R, ray, x, d, s);
+    const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
+    if (family == 0) {
+        const int w = 2 * G.nbr;
+        for (int j = 0; j < G.nbr; ++j) {
+            double ti, to;
+            int ri, ro, ni, no;
+            sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
+            t[ray * w + j] = ti; region[ray * w + j] = ri; neg[ray * w + j] = (int8_t)ni;
+            t[ray * w + G.nbr + j] = to; region[ray * w + G.nbr + j] = ro;
+            neg[ray * w + G.nbr + j] = (int8_t)no;
+        }
+    } else if (family == 1) {
+        const int w = 2 * G.nbe;
+        for (int j = 0; j < G.nbe; ++j) {
+            double ta, tb;
+            int ra, rb, na_, nb_;
+            cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
+            t[ray * w + j] = ta; region[ray * w + j] = ra; neg[ray * w + j] = (int8_t)na_;
+            t[ray * w + G.nbe + j] = tb; region[ray * w + G.nbe + j] = rb;
+            neg[ray * w + G.nbe + j] = (int8_t)nb_;
+        }
+    } else {
+        const int w = G.nba;
+        for (int j = 0; j < G.nba; ++j) {
+            double tt;
+            int r, ng;
+            plane_solve(G, g, j, tt, r, ng);
+            t[ray * w + j] = tt; region[ray * w + j] = r; neg[ray * w + j] = (int8_t)ng;
+        }
+    }
+}
+
+// ---- exact path for deferred rays: one lane per ray, the reference algorithm verbatim --------
+template <int MODE, typename T>
+__global__ __launch_bounds__(64) void exact_kernel(GridDev G, RaysDev R, TraceOut<T> o,
+                                                   Cand* scratch) {
+    const int64_t lanes = (int64_t)gridDim.x * blockDim.x;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    Cand* v = scratch + gid * G.K;
+    const int64_t count = (int64_t)*o.n_deferred;
+    const int nbr = G.nbr, nbe = G.nbe, nba = G.nba, K = G.K;
+    const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe;
+    for (int64_t q = gid; q < count; q += lanes) {
+        const int64_t ray = o.deferred[q];
+        double x[3], d[3];
+        int s[3];
+        load_ray(R, ray, x, d, s);
+        const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
+        auto put = [&](int c, double t, int reg) {
+            v[c].t = t;
+            v[c].pay = ((uint32_t)c << 16) | (uint32_t)(reg + 2);
+        };
+        // candidates in the reference's concatenation order (raytracer.py:92, 117-122)
+        for (int j = 0; j < nbr; ++j) {
+            double ti, to;
+            int ri, ro, ni, no;
+            sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
+            put(j, ti, ri);
+            put(nbr + j, to, ro);
+        }
+        for (int j = 0; j < nbe; ++j) {
+            double ta, tb;
+            int ra, rb, na_, nb_;
+            cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
+            put(r_lim + j, ta, ra);
+            put(r_lim + nbe + j, tb, rb);
+        }
+        for (int j = 0; j < nba; ++j) {
+            double t;
+            int r, ng;
+            plane_solve(G, g, j, t, r, ng);
+            put(e_lim + j, t, r);
+        }
+        put(K - 1, 0.0, 0);
+        introsort(v, K);
+        // forward fill + diff + masking (raytracer.py:126, 140-173)
+        int64_t c_lo = 0, c_hi = o.n_chan;
+        if (MODE == MODE_INTEGRATE && o.ray_chan_div > 0) {
+            c_lo = ray / o.ray_chan_div;
+            c_hi = c_lo + 1;
+        }
+        if (MODE != MODE_INTEGRATE) c_hi = c_lo + 1;
+        for (int64_t c = c_lo; c < c_hi; ++c) {
+            int cr = s[0], ce = s[1], ca = s[2];
+            int64_t nseg = 0;
+            double acc = 0.0;
+            const int64_t base = MODE == MODE_FILL ? o.row_ptr[ray] : 0;
+            for (int k = 0; k < K; ++k) {
+                const double t = v[k].t;
+                const uint32_t p = v[k].pay;
+                if (!(t < 0.0)) {
+                    const int cand = (int)(p >> 16);
+                    const int reg = (int)(p & 0xffffu) - 2;
+                    if (cand == K - 1) { cr = s[0]; ce = s[1]; ca = s[2]; }
+                    else if (cand < r_lim) cr = reg;
+                    else if (cand < e_lim) { if (reg != -2) ce = reg; }
+                    else if (reg != -2) ca = reg;
+                }
+                const double tn = k + 1 < K ? v[k + 1].t : kInf;
+                const double len = tn - t;
+                if (!(len > 0.0) || !__builtin_isfinite(len)) continue;
+                if (cr < 0 || cr >= G.nr || ce < 0 || ce >= G.ne || ca < 0 || ca >= G.na) continue;
+                const int vx = (cr * G.ne + ce) * G.na + ca;
+                if (MODE == MODE_FILL) {
+                    o.vox[base + nseg] = vx;
+                    o.len[base + nseg] = len;
+                } else if (MODE == MODE_INTEGRATE) {
+                    acc += (double)o.density[c * o.chan_stride + vx] * len;
+                }
+                ++nseg;
+            }
+            if (MODE == MODE_COUNT) o.counts[ray] = (int32_t)nseg;
+            if (MODE == MODE_INTEGRATE) {
+                const int64_t oc = o.ray_chan_div > 0 ? 0 : c;
+                o.out[oc * o.out_chan_stride + ray] = (T)acc;
+            }
+        }
+    }
+}
+
+// ---- host launchers ----------------------------------------------------------------------
+static int trace_cap(const GridDev& G) { return ((G.K + 63) / 64) * 64; }
+constexpr int kExactBlocks = 64;     // 4096 lanes for the (rare) deferred rays
+constexpr size_t kWsHead = 256;      // deferred counter, padded
+
+static size_t exact_scratch_bytes(const GridDev& G) {
+    return (size_t)kExactBlocks * 64 * G.K * sizeof(Cand);
+}
+static size_t workspace_bytes(const GridDev& G, int64_t n) {
+    return kWsHead + (((size_t)n * sizeof(int64_t) + 255) / 256) * 256 + exact_scratch_bytes(G);
+}
+
+template <int MODE, typename T>
+static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void* workspace,
+                        size_t workspace_size, hipStream_t st) {
+    if (G.nr < 1 || G.ne < 1 || G.na < 1) return fail("tracing needs at least one voxel per axis");
+    if (R.n == 0) return 0;
+    if (!workspace || workspace_size < workspace_bytes(G, R.n))
+        return fail("trace workspace too small: %zu < %zu bytes", workspace_size,
+                    workspace_bytes(G, R.n));
+    const int cap = trace_cap(G);
+    const size_t lds = (size_t)kWavesPerBlock * cap * (sizeof(uint64_t) + sizeof(uint32_t));
+    if (lds > 160 * 1024) return fail("grid too large for the per-wave LDS list (K=%d)", G.K);
+    unsigned char* ws = (unsigned char*)workspace;
+    o.n_deferred = (unsigned long long*)ws;
+    o.deferred = (int64_t*)(ws + kWsHead);
+    Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
+    if (hipMemsetAsync(o.n_deferred, 0, kWsHead, st) != hipSuccess) return fail("memset failed");
+    const int64_t ntiles = (R.n + 63) / 64;
+    int64_t grid = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(256), lds, st, G, R, o,
+                       cap);
+    if (int e = check_launch("trace_kernel")) return e;
+    hipLaunchKernelGGL((exact_kernel<MODE, T>), dim3(kExactBlocks), dim3(64), 0, st, G, R, o,
+                       scratch);
+    return check_launch("exact_kernel");
+}
+
+}  // namespace sphrt
+
+using namespace sphrt;
+
+extern "C" size_t sphrt_trace_workspace_bytes(const sphrt_plan* plan, int64_t n) {
+    if (!plan || n < 0) return 0;
+    return workspace_bytes(plan->dev, n);
+}
+
+extern "C" int sphrt_trace_count(const sphrt_plan* plan, const sphrt_rays* rays, int32_t* counts,
+                                 void* workspace, size_t workspace_size, void* stream) {
+    GridDev G;
+    RaysDev R;
+    if (int e = resolve(plan, rays, G, R)) return e;
+    TraceOut<double> o{};
+    o.counts = counts;
+    return launch_trace<MODE_COUNT, double>(G, R, o, workspace, workspace_size,
+                                            (hipStream_t)stream);
+}
+
+extern "C" int sphrt_trace_fill(const sphrt_plan* plan, const sphrt_rays* rays,
+                                const int64_t* row_ptr, int32_t* vox, double* len,
+                                void* workspace, size_t workspace_size, void* stream) {
+    GridDev G;
+    RaysDev R;
+    if (int e = resolve(plan, rays, G, R)) return e;
+    TraceOut<double> o{};
+    o.row_ptr = row_ptr;
+    o.vox = vox;
+    o.len = len;
+    return launch_trace<MODE_FILL, double>(G, R, o, workspace, workspace_size,
+                                           (hipStream_t)stream);
+}
+
+template <typename T>
+static int trace_integrate(const sphrt_plan* plan, const sphrt_rays* rays, const T* density,
+                           int64_t n_chan, int64_t chan_stride, int64_t ray_chan_div, T* out,
+                           int64_t out_chan_stride, void* workspace, size_t workspace_size,
+                           void* stream) {
+    GridDev G;
+    RaysDev R;
+    if (int e = resolve(plan, rays, G, R)) return e;
+    if (n_chan < 1) return fail("n_chan must be >= 1");
+    if (ray_chan_div > 0 && n_chan != 1) return fail("ray_chan_div requires n_chan == 1");
+    TraceOut<T> o{};
+    o.density = density;
+    o.n_chan = n_chan;
+    o.chan_stride = chan_stride;
+    o.ray_chan_div = ray_chan_div;
+    o.out = out;
+    o.out_chan_stride = out_chan_stride;
+    return launch_trace<MODE_INTEGRATE, T>(G, R, o, workspace, workspace_size,
+                                           (hipStream_t)stream);
+}
+
+extern "C" int sphrt_trace_integrate_f32(const sphrt_plan* plan, const sphrt_rays* rays,
+                                         const float* density, int64_t n_chan,
+                                         int64_t chan_stride, int64_t ray_chan_div, float* out,
+                                         int64_t out_chan_stride, void* workspace,
+                                         size_t workspace_size, void* stream) {
+    return trace_integrate<float>(plan, rays, density, n_chan, chan_stride, ray_chan_div, out,
+                                  out_chan_stride, workspace, workspace_size, stream);
+}
+extern "C" int sphrt_trace_integrate_f64(const sphrt_plan* plan, const sphrt_rays* rays,
+                                         const double* density, int64_t n_chan,
+                                         int64_t chan_stride, int64_t ray_chan_div, double* out,
+                                         int64_t out_chan_stride, void* workspace,
+                                         size_t workspace_size, void* stream) {
+    return trace_integrate<double>(plan, rays, density, n_chan, chan_stride, ray_chan_div, out,
+                                   out_chan_stride, workspace, workspace_size, stream);
+}
+
+extern "C" int sphrt_solve(const sphrt_plan* plan, const sphrt_rays* rays, int family, double* t,
+                           int32_t* region, int8_t* neg, void* stream) {
+    GridDev G;
+    RaysDev R;
+    if (int e = resolve(plan, rays, G, R)) return e;
+    if (family < 0 || family > 2) return fail("family must be 0 (r), 1 (e) or 2 (a)");
+    if (R.n == 0) return 0;
+    const int64_t grid = (R.n + 255) / 256;
+    hipLaunchKernelGGL(solve_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, G, R,
+                       family, t, region, neg);
+    return check_launch("solve_kernel");
+}

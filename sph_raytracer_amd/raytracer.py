@@ -1,0 +1,460 @@
+"""Raytracing operator on MI355X: drop-in for the reference's ``sph_raytracer.raytracer``.
+
+``Operator(grid, geom)`` traces every detector ray through the spherical grid once, on the GPU,
+into a compact CSR of (linear voxel index, length) segments; ``op(density)`` is the line
+integral (forward), ``op.T(y)`` the back-projection (adjoint), and autograd's backward of
+``op(density)`` runs the adjoint kernel.  Constructor arguments, attributes and call shapes follow
+raytracer.py:647-755.  All compute goes through libsphrt.so (include/sphrt.h); there is no CPU
+fallback — without a ROCm GPU every compute entry point raises.
+
+Differences from the reference, by design:
+- the trace is stored as a CSR of non-zero segments, not as (3, *rays, K) / (*rays, K) tensors;
+  ``op.regs`` / ``op.lens`` rebuild a padded compatibility view on demand;
+- crossings at exactly equal distances are ordered as the reference's libstdc++ introsort orders
+  them whenever that order can change a voxel (rare rays, replayed by an exact kernel);
+- forward sums accumulate in float64 and round once to the density dtype;
+- the caller's ``geom.rays`` tensor is never normalised in place.
+"""
+import math
+
+import torch as tr
+
+from . import _lib
+from .geometry import ViewGeomCollection
+
+DEVICE = 'cpu'
+PDEVICE = 'cpu'
+FTYPE = tr.float64
+ITYPE = tr.int64
+
+SEG_PER_BLOCK = 2048   # forward/adjoint partition granularity (segments per workgroup)
+
+
+def isclose(a, b, factor=3):
+    """|a - b| < finfo(dtype).resolution ** (1/factor)   (raytracer.py:233-246)."""
+    return abs(a - b) < tr.finfo(a.dtype).resolution ** (1 / factor)
+
+
+# ----- host helpers: start voxels (raytracer.py:555-644) --------------------------------------
+
+def cart2sph(xyz):
+    """(x, y, z) -> (radius, elevation from +Z in [0, pi], azimuth from +X in [-pi, pi])."""
+    x, y, z = xyz.moveaxis(-1, 0)
+    out = tr.empty_like(xyz, dtype=float)
+    rho2 = x ** 2 + y ** 2
+    out[..., 0] = tr.sqrt(rho2 + z ** 2)
+    out[..., 1] = tr.arctan2(tr.sqrt(rho2), z)
+    out[..., 2] = tr.arctan2(y, x)
+    return out
+
+
+def sph2cart(rea):
+    """(radius, elevation, azimuth) -> (x, y, z)."""
+    r, e, a = rea.moveaxis(-1, 0)
+    out = tr.empty_like(rea)
+    out[..., 0] = r * tr.sin(e) * tr.cos(a)
+    out[..., 1] = r * tr.sin(e) * tr.sin(a)
+    out[..., 2] = r * tr.cos(e)
+    return out
+
+
+def _region_of(bounds, v, n):
+    """Bin of v in `bounds` (searchsorted right - 1); the last boundary belongs to the last bin;
+    outside -> -1."""
+    idx = tr.searchsorted(bounds, v.contiguous(), right=True) - 1
+    idx = tr.where(v == bounds[-1], n - 1, idx)
+    idx[idx == n] = -1
+    return idx
+
+
+def find_starts(grid, xs, ftype=FTYPE, device=DEVICE):
+    """Voxel (r, e, a) containing each ray start, shape (3, ...).  Evaluated on the host with
+    torch — once per *unique* start — so angles and bins are bit-identical to the reference."""
+    spec = dict(dtype=ftype, device=device)
+    xs = tr.asarray(xs, **spec)
+    rb, eb, ab = (tr.asarray(b, **spec) for b in (grid.r_b, grid.e_b, grid.a_b))
+    sph = cart2sph(xs)
+    shp = grid.shape
+    return tr.stack((_region_of(rb, sph[..., 0], shp.r),
+                     _region_of(eb, sph[..., 1], shp.e),
+                     _region_of(ab, sph[..., 2], shp.a)), axis=0)
+
+
+# ----- device plumbing ------------------------------------------------------------------------
+
+class _Plan:
+    """Owner of a libsphrt plan: the grid's boundary tables resident on one GPU."""
+
+    def __init__(self, grid, device, boundaries=None):
+        lib = _lib.load()
+        rb, eb, ab = boundaries if boundaries is not None else (grid.r_b, grid.e_b, grid.a_b)
+        rb, eb, ab = (tr.asarray(b, dtype=tr.float64).contiguous() for b in (rb, eb, ab))
+        # trigonometric tables with torch CPU — the values the reference solvers use
+        cos_e = tr.cos(eb)
+        cos2_e = tr.cos(eb) ** 2
+        cos_a, sin_a = tr.cos(ab), tr.sin(ab)
+        self._keep = [t.contiguous() for t in (rb, eb, ab, cos_e, cos2_e, cos_a, sin_a)]
+        rb, eb, ab, cos_e, cos2_e, cos_a, sin_a = self._keep
+        desc = _lib.GridDesc()
+        desc.nr, desc.ne, desc.na = len(rb) - 1, len(eb) - 1, len(ab) - 1
+        desc.r_b, desc.e_b, desc.a_b = rb.data_ptr(), eb.data_ptr(), ab.data_ptr()
+        desc.cos_e, desc.cos2_e = cos_e.data_ptr(), cos2_e.data_ptr()
+        desc.cos_a, desc.sin_a = cos_a.data_ptr(), sin_a.data_ptr()
+        desc.a_wrap = int(bool(-ab[0] == ab[-1] == tr.pi))
+        res = tr.finfo(tr.float64).resolution
+        desc.close_tol = res ** (1 / 3)
+        desc.plane_par_tol = res
+        self.shape = (desc.nr, desc.ne, desc.na)
+        self.device = device
+        h = _lib.c_vp()
+        _lib.check(lib.sphrt_plan_create(desc, device.index, h), 'sphrt_plan_create')
+        self.handle = h
+        self.K = lib.sphrt_plan_candidates(h)
+
+    def __del__(self):
+        h = getattr(self, 'handle', None)
+        if h is not None and h.value:
+            try:
+                _lib.load().sphrt_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+def _broadcast_pair(xs, rays):
+    """Reference broadcasting rule (raytracer.py:76-80) -> (ray shape, xs, rays) un-expanded."""
+    xs = tr.asarray(xs, dtype=tr.float64)
+    rays = tr.asarray(rays, dtype=tr.float64)
+    if xs.numel() > rays.numel():
+        shape = tuple(tr.broadcast_shapes(rays.shape, xs.shape))
+    else:
+        shape = tuple(tr.broadcast_shapes(xs.shape, rays.shape))
+    return shape[:-1], xs, rays
+
+
+class _RayBatch:
+    """Device copies of the unique starts / directions + the broadcast descriptor."""
+
+    def __init__(self, grid, xs, rays, device):
+        """grid=None: no start voxels (per-family solves only)."""
+        rshape, xs, rays = _broadcast_pair(xs, rays)
+        if len(rshape) > _lib.MAX_DIMS:
+            raise ValueError(f'ray batch rank {len(rshape)} > {_lib.MAX_DIMS}')
+        self.shape = rshape
+        self.n = math.prod(rshape)
+        xs_u = xs.detach().to('cpu').contiguous()
+        st = tr.zeros(xs_u.shape[:-1] + (4,), dtype=tr.int32)
+        if grid is not None:
+            starts = find_starts(grid, xs_u)                   # (3, ...) on the host
+            st[..., :3] = starts.moveaxis(0, -1).to(tr.int32)
+        self.xs = xs_u.to(device)
+        self.rays = rays.detach().contiguous().to(device)
+        self.start = st.to(device)
+        full = rshape + (3,)
+        xs_str = self.xs.expand(full).stride()
+        ry_str = self.rays.expand(full).stride()
+        d = _lib.RayBatch()
+        d.ndim = len(rshape)
+        for i, s in enumerate(rshape):
+            d.shape[i] = s
+            d.xs_stride[i] = xs_str[i]
+            d.rays_stride[i] = ry_str[i]
+        d.xs, d.rays, d.start = self.xs.data_ptr(), self.rays.data_ptr(), self.start.data_ptr()
+        self.desc = d
+
+
+# ----- API-parity solvers (raytracer.py:248-552) ----------------------------------------------
+
+def _solve(family, bounds, xs, rays, ftype, itype, device):
+    if ftype != tr.float64:
+        raise NotImplementedError('sph_raytracer_amd traces in float64 only')
+    dev = _lib.require_gpu()
+    bounds = tr.asarray(bounds, dtype=tr.float64)
+    unit = tr.tensor([0.0, 1.0], dtype=tr.float64)
+    grid_b = tuple(bounds if i == family else unit for i in range(3))
+    plan = _Plan(None, dev, boundaries=grid_b)
+    batch = _RayBatch(None, xs, rays, dev)
+    nb = len(bounds)
+    width = nb if family == 2 else 2 * nb
+    t = tr.empty(batch.shape + (width,), dtype=tr.float64, device=dev)
+    reg = tr.empty(batch.shape + (width,), dtype=tr.int32, device=dev)
+    neg = tr.empty(batch.shape + (width,), dtype=tr.int8, device=dev)
+    _lib.check(_lib.load().sphrt_solve(plan.handle, batch.desc, family, _lib.ptr(t),
+                                       _lib.ptr(reg), _lib.ptr(neg), _lib.stream_of(dev)),
+               'sphrt_solve')
+    inds = tr.arange(nb, dtype=itype)
+    inds = (inds if family == 2 else tr.cat((inds, inds))).repeat(*batch.shape, 1)
+    return t.to(device), reg.to(itype).to(device), inds.to(device), neg.to(device)
+
+
+def r_torch(r, xs, rays, ftype=FTYPE, itype=ITYPE, device=DEVICE):
+    """Crossings of every ray with spheres of radii ``r`` (raytracer.py:248-325).
+    Returns (t, regions, inds, negative_crossing), each (*rays, 2*len(r))."""
+    return _solve(0, r, xs, rays, ftype, itype, device)
+
+
+def e_torch(e, xs, rays, ftype=FTYPE, itype=ITYPE, device=DEVICE):
+    """Crossings with elevation cones at angles ``e`` (raytracer.py:328-468), (*rays, 2*len(e))."""
+    return _solve(1, e, xs, rays, ftype, itype, device)
+
+
+def a_torch(a_b, xs, rays, ftype=FTYPE, itype=ITYPE, device=DEVICE):
+    """Crossings with azimuth half-planes ``a_b`` (raytracer.py:471-552), (*rays, len(a_b))."""
+    return _solve(2, a_b, xs, rays, ftype, itype, device)
+
+
+def _layout_for(grid, ray_shape, shape):
+    """-> (n_chan, ray_chan_div, out_shape): the indexing rules of raytracer.py:703-712.
+
+    Static grid: density (C..., nr, ne, na) -> (C..., *rays).  Dynamic grid: density
+    (T, nr, ne, na) indexed with t = arange(T)[:, None, None, None], i.e. view i of a (T, H, W)
+    collection sees time slice i, while a single detector is integrated for every time step."""
+    R = tuple(ray_shape)
+    g = tuple(grid.shape)
+    if grid.dynamic:
+        if len(shape) != 4 or tuple(shape[1:]) != g[1:]:
+            raise ValueError(f'dynamic grid expects density (T, {g[1]}, {g[2]}, {g[3]}), '
+                             f'got {tuple(shape)}')
+        T = shape[0]
+        if len(R) > 3:
+            raise NotImplementedError('dynamic grids need a detector of rank <= 3')
+        out_shape = tuple(tr.broadcast_shapes((T, 1, 1, 1), R + (1,))[:-1])
+        if len(R) == 3 and R[0] == T and T > 1:
+            return 1, R[1] * R[2], out_shape        # view i sees time slice i
+        if len(R) == 3 and R[0] != 1 and T != 1:
+            raise ValueError(f'cannot pair {T} time steps with {R[0]} views')
+        return T, 0, out_shape                        # every time step sees every ray
+    if tuple(shape[-3:]) != g:
+        raise ValueError(f'density shape {tuple(shape)} does not end with grid shape {g}')
+    lead = tuple(shape[:-3])
+    return math.prod(lead), 0, lead + R
+
+
+def _workspace(lib, plan, n, dev):
+    return tr.empty(lib.sphrt_trace_workspace_bytes(plan.handle, n), dtype=tr.uint8, device=dev)
+
+
+def line_integrals(grid, geom, density):
+    """No-store forward: trace and integrate in one fused pass, nothing persisted.
+
+    Same result as ``Operator(grid, geom)(density)`` (not differentiable), without building the
+    segment CSR — the memory-capped / cold path (one kernel, O(output) memory)."""
+    dev = _lib.require_gpu()
+    plan = _Plan(grid, dev)
+    batch = _RayBatch(grid, geom.ray_starts, geom.rays, dev)
+    density = tr.as_tensor(density)
+    n_chan, div, out_shape = _layout_for(grid, batch.shape, density.shape)
+    cdt = density.dtype if density.dtype in (tr.float32, tr.float64) else tr.float32
+    d = density.detach().to(device=dev, dtype=cdt).contiguous()
+    n = batch.n
+    out = tr.empty((n_chan, n) if div == 0 else (n,), dtype=cdt, device=dev)
+    lib = _lib.load()
+    ws = _workspace(lib, plan, n, dev)
+    fn = lib.sphrt_trace_integrate_f32 if cdt == tr.float32 else lib.sphrt_trace_integrate_f64
+    _lib.check(fn(plan.handle, batch.desc, _lib.ptr(d), n_chan, math.prod(grid.shape[-3:]), div,
+                  _lib.ptr(out), n, _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)),
+               'sphrt_trace_integrate')
+    return out.reshape(out_shape).to(device=density.device, dtype=density.dtype)
+
+
+# ----- the operator ---------------------------------------------------------------------------
+
+class _LineIntegral(tr.autograd.Function):
+    """y = A x with dA/dx = A^T on the cached CSR; nothing large is saved for backward."""
+
+    @staticmethod
+    def forward(ctx, density, op):
+        ctx.op = op
+        ctx.meta = (density.shape, density.dtype, density.device)
+        return op._apply_forward(density)
+
+    @staticmethod
+    def backward(ctx, grad):
+        shape, dtype, device = ctx.meta
+        return ctx.op._apply_adjoint(grad, shape, dtype, device), None
+
+
+class Operator:
+    """Raytracing operator (raytracer.py:647-755).
+
+    Args:
+        grid (SphericalGrid), geom (ViewGeom or collection), dynamic (bool or None: infer from
+        geom), ftype (float64 only), itype (index dtype of the ``regs`` view), device (where
+        results live; compute always runs on the current ROCm GPU), pdevice (accepted for
+        compatibility), debug / debug_los (print one ray's segments), invalid (unsupported),
+        _compute (False: skip the trace, for plotting-only operators).
+    """
+
+    def __init__(self, grid, geom, dynamic=False, ftype=FTYPE, itype=ITYPE, device=DEVICE,
+                 pdevice=PDEVICE, debug=False, debug_los=None, invalid=False, _compute=True):
+        self.grid = grid
+        self.geom = geom
+        if dynamic is None:
+            dynamic = isinstance(geom, ViewGeomCollection)
+        self.dynamic = dynamic
+        self.ftype = ftype
+        self.itype = itype
+        self.device = device
+        if ftype != tr.float64:
+            raise NotImplementedError('sph_raytracer_amd traces in float64 (the reference default); '
+                                      'ftype=float32 is not supported')
+        if invalid:
+            raise NotImplementedError('invalid=True (keep invalid segments) is not supported')
+        self._csr = None
+        if _compute:
+            self._trace()
+            if debug:
+                self._debug_print(debug_los)
+
+    # -- trace ---------------------------------------------------------------------------------
+    def _trace(self):
+        dev = _lib.require_gpu()
+        self._cdev = dev
+        lib = _lib.load()
+        self._plan = _Plan(self.grid, dev)
+        batch = _RayBatch(self.grid, self.geom.ray_starts, self.geom.rays, dev)
+        self._ray_shape = batch.shape
+        n = batch.n
+        stream = _lib.stream_of(dev)
+        counts = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
+        row_ptr = tr.empty(n + 1, dtype=tr.int64, device=dev)
+        ws = tr.empty(lib.sphrt_scan_workspace_bytes(n), dtype=tr.uint8, device=dev)
+        tws = _workspace(lib, self._plan, n, dev)
+        _lib.check(lib.sphrt_trace_count(self._plan.handle, batch.desc, _lib.ptr(counts),
+                                         _lib.ptr(tws), tws.numel(), stream), 'sphrt_trace_count')
+        _lib.check(lib.sphrt_scan_counts(_lib.ptr(counts), n, _lib.ptr(row_ptr), _lib.ptr(ws),
+                                         stream), 'sphrt_scan_counts')
+        total = int(row_ptr[n].item())          # the one host sync of the trace
+        vox = tr.empty(max(total, 1), dtype=tr.int32, device=dev)
+        seg_len = tr.empty(max(total, 1), dtype=tr.float64, device=dev)
+        _lib.check(lib.sphrt_trace_fill(self._plan.handle, batch.desc, _lib.ptr(row_ptr),
+                                        _lib.ptr(vox), _lib.ptr(seg_len), _lib.ptr(tws),
+                                        tws.numel(), stream), 'sphrt_trace_fill')
+        del tws
+        nblocks = total // SEG_PER_BLOCK + 1
+        block_lo = tr.empty(nblocks + 1, dtype=tr.int64, device=dev)
+        _lib.check(lib.sphrt_partition(_lib.ptr(row_ptr), n, SEG_PER_BLOCK, _lib.ptr(block_lo),
+                                       nblocks, stream), 'sphrt_partition')
+        self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, block_lo=block_lo,
+                         nblocks=nblocks, n=n, total=total)
+        self._batch = batch
+
+    # -- shape logic of raytracer.py:703-712 -----------------------------------------------------
+    def _layout(self, shape):
+        """-> (n_chan, ray_chan_div, out_shape) for a density of `shape`."""
+        return _layout_for(self.grid, self._ray_shape, shape)
+
+    def __call__(self, density):
+        """Line integrals of ``density`` along every ray: (C..., *geom.shape) for a static grid,
+        (T, H, W) for a dynamic one (raytracer.py:692-713).  Differentiable in ``density``."""
+        if self._csr is None:
+            raise RuntimeError('Operator was built with _compute=False')
+        density = tr.as_tensor(density)
+        return _LineIntegral.apply(density, self)
+
+    def _apply_forward(self, density):
+        dev = self._cdev
+        n_chan, div, out_shape = self._layout(density.shape)
+        in_dtype = density.dtype
+        cdt = in_dtype if in_dtype in (tr.float32, tr.float64) else tr.float32
+        d = density.detach().to(device=dev, dtype=cdt).contiguous()
+        csr = self._csr
+        n = csr['n']
+        vol = math.prod(self.grid.shape[-3:])
+        out = tr.empty((n_chan, n) if div == 0 else (n,), dtype=cdt, device=dev)
+        fn = _lib.load().sphrt_forward_f32 if cdt == tr.float32 else _lib.load().sphrt_forward_f64
+        _lib.check(fn(_lib.ptr(csr['row_ptr']), _lib.ptr(csr['vox']), _lib.ptr(csr['len']), n,
+                      _lib.ptr(csr['block_lo']), csr['nblocks'], SEG_PER_BLOCK, _lib.ptr(d),
+                      n_chan, vol, div, _lib.ptr(out), n, _lib.stream_of(dev)), 'sphrt_forward')
+        out = out.reshape(out_shape)
+        return out.to(device=density.device, dtype=in_dtype)
+
+    def _apply_adjoint(self, y, dshape, ddtype, ddevice):
+        dev = self._cdev
+        n_chan, div, out_shape = self._layout(dshape)
+        csr = self._csr
+        n = csr['n']
+        vol = math.prod(self.grid.shape[-3:])
+        ydt = y.dtype if y.dtype in (tr.float32, tr.float64) else tr.float32
+        yv = y.detach().to(device=dev, dtype=ydt).reshape(-1).contiguous()
+        if yv.numel() != n_chan * n:
+            raise ValueError(f'adjoint input has {yv.numel()} values, expected {n_chan * n}')
+        acc = tr.zeros(math.prod(dshape), dtype=tr.float64, device=dev)
+        _lib.check(_lib.load().sphrt_adjoint_accumulate(
+            _lib.ptr(csr['row_ptr']), _lib.ptr(csr['vox']), _lib.ptr(csr['len']), n,
+            _lib.ptr(csr['block_lo']), csr['nblocks'], SEG_PER_BLOCK, _lib.ptr(yv),
+            int(ydt == tr.float64), n_chan, n, div, _lib.ptr(acc), vol, _lib.stream_of(dev)),
+            'sphrt_adjoint_accumulate')
+        if ddtype == tr.float64:
+            res = acc
+        elif ddtype == tr.float32:
+            res = tr.empty(acc.shape, dtype=tr.float32, device=dev)
+            _lib.check(_lib.load().sphrt_f64_to_f32(_lib.ptr(acc), _lib.ptr(res), acc.numel(),
+                                                     _lib.stream_of(dev)), 'sphrt_f64_to_f32')
+        else:
+            res = acc.to(ddtype)
+        return res.reshape(dshape).to(ddevice)
+
+    def T(self, line_integrations):
+        """Back-projection of ``line_integrations`` (geom.shape) into a grid.shape volume
+        (raytracer.py:715-748).  Static grids only, like the reference."""
+        if self.grid.dynamic:
+            raise NotImplementedError
+        y = tr.as_tensor(line_integrations)
+        return self._apply_adjoint(y, tuple(self.grid.shape), y.dtype, tr.device(self.device))
+
+    # -- compatibility views -----------------------------------------------------------------------
+    def _padded(self):
+        csr = self._csr
+        row_ptr = csr['row_ptr']
+        counts = (row_ptr[1:] - row_ptr[:-1])
+        smax = max(int(counts.max().item()) if csr['n'] else 0, 1)
+        n, total = csr['n'], csr['total']
+        ray = tr.repeat_interleave(tr.arange(n, device=row_ptr.device), counts)
+        pos = tr.arange(total, device=row_ptr.device) - row_ptr[:-1][ray]
+        vox = tr.zeros((n, smax), dtype=tr.int64, device=row_ptr.device)
+        lens = tr.zeros((n, smax), dtype=tr.float64, device=row_ptr.device)
+        vox[ray, pos] = csr['vox'][:total].to(tr.int64)
+        lens[ray, pos] = csr['len'][:total]
+        _, ne, na = self.grid.shape[-3:]
+        regs = tr.stack((vox // (ne * na), (vox // na) % ne, vox % na))
+        R = tuple(self._ray_shape)
+        return regs.reshape((3,) + R + (smax,)), lens.reshape(R + (smax,))
+
+    @property
+    def regs(self):
+        """(3, *rays, S_max) voxel indices (padded; compatibility view of the CSR)."""
+        return self._padded()[0].to(device=self.device, dtype=self.itype)
+
+    @property
+    def lens(self):
+        """(*rays, S_max) segment lengths matching ``regs`` (zero padding)."""
+        return self._padded()[1].to(device=self.device)
+
+    def segments(self):
+        """The trace itself: (row_ptr int64 (n+1,), vox int32, len float64) on the GPU."""
+        c = self._csr
+        return c['row_ptr'], c['vox'][:c['total']], c['len'][:c['total']]
+
+    def _debug_print(self, debug_los):
+        R = tuple(self._ray_shape)
+        if debug_los is None:
+            debug_los = (0,) * len(R)
+        i = 0
+        for k, s in zip(debug_los, R):
+            i = i * s + k
+        row_ptr, vox, seg = self.segments()
+        a, b = int(row_ptr[i]), int(row_ptr[i + 1])
+        _, ne, na = self.grid.shape[-3:]
+        print('ray_start:', self._batch.xs.reshape(-1, 3)[0].tolist())
+        print('  r   e   a      len')
+        for v, l in zip(vox[a:b].tolist(), seg[a:b].tolist()):
+            print(f'{v // (ne * na):3d} {(v // na) % ne:3d} {v % na:3d}  {l:.6g}')
+
+    def __repr__(self):
+        if self.dynamic:
+            return f"Operator({(self.geom.shape[0], *self.grid.shape)} → {self.geom.shape})"
+        return f"Operator({self.grid.shape} → {self.geom.shape})"
+
+    def plot(self, *args, **kwargs):
+        raise NotImplementedError('plotting is out of scope for sph_raytracer_amd')

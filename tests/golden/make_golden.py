@@ -1,0 +1,182 @@
+"""Generate golden vectors from the real reference (this container only; needs /root/reference).
+
+    python tests/golden/make_golden.py
+
+Every case stores its INPUTS (grid boundaries, ray starts, ray directions as the reference
+geometry produced them, densities, adjoint inputs) and the reference's OUTPUTS (non-zero trace
+segments in ray order, forward line integrals in float64 and float32, the adjoint T(y)), so the
+GPU tests never regenerate rays and never need the reference.  Files: tests/golden/<case>.npz.
+"""
+import os
+import sys
+
+import numpy as np
+import torch as tr
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import refshim  # noqa: E402
+
+R = refshim.load()
+G, RT = R.geometry, R.raytracer
+
+
+def segments_from_dense(regs, lens, grid_shape):
+    """Reference (3, *rays, K) regs + (*rays, K) lens -> non-zero segments per ray (in order)."""
+    nr, ne, na = grid_shape
+    K = lens.shape[-1]
+    regs = regs.reshape(3, -1, K).numpy()
+    lens = lens.reshape(-1, K).numpy()
+    keep = lens > 0
+    ray_ptr = np.zeros(lens.shape[0] + 1, np.int64)
+    ray_ptr[1:] = np.cumsum(keep.sum(1))
+    r, e, a = (regs[i][keep] for i in range(3))
+    vox = ((r * ne + e) * na + a).astype(np.int32)
+    return ray_ptr, vox, lens[keep]
+
+
+def orbit(n_obs, maker):
+    geoms = []
+    for th in tr.linspace(0, 2 * tr.pi, n_obs):
+        geoms.append(maker((5 * tr.cos(th), 5 * tr.sin(th), 1)))
+    return sum(geoms)
+
+
+def grid_arrays(grid):
+    return dict(r_b=grid.r_b.numpy(), e_b=grid.e_b.numpy(), a_b=grid.a_b.numpy(),
+                shape=np.array(tuple(grid.shape)), dynamic=np.array(grid.dynamic))
+
+
+def save_case(name, grid, geom, densities=(), ys=(), note='', keep_dense=False):
+    tr.manual_seed(1234)
+    xs = geom.ray_starts.clone()
+    rays = geom.rays.clone()     # as the reference geometry produced them (before tracing)
+    op = RT.Operator(grid, geom)
+    gshape = tuple(grid.shape)[-3:]
+    ray_ptr, vox, seglen = segments_from_dense(op.regs, op.lens, gshape)
+    out = dict(grid_arrays(grid), xs=xs.numpy(), rays=rays.numpy(), ray_shape=np.array(op.lens.shape[:-1]),
+               seg_ptr=ray_ptr, seg_vox=vox, seg_len=seglen, note=np.array(note))
+    starts = RT.find_starts(grid, xs)
+    out['starts'] = starts.numpy()
+    for i, d in enumerate(densities):
+        d64 = d.to(tr.float64)
+        out[f'density{i}'] = d64.numpy()
+        out[f'fwd64_{i}'] = op(d64).numpy()
+        out[f'fwd32_{i}'] = op(d64.to(tr.float32)).numpy()
+    for i, y in enumerate(ys):
+        y64 = y.to(tr.float64)
+        out[f'y{i}'] = y64.numpy()
+        out[f'adj64_{i}'] = op.T(y64).numpy()
+    if keep_dense:
+        out['dense_regs'] = op.regs.numpy().astype(np.int32)
+        out['dense_lens'] = op.lens.numpy()
+    path = os.path.join(HERE, f'{name}.npz')
+    np.savez_compressed(path, **out)
+    print(f'{name}: rays={int(np.prod(op.lens.shape[:-1]))} K={op.lens.shape[-1]} '
+          f'segments={len(vox)} -> {os.path.getsize(path) / 1e3:.0f} kB')
+
+
+def solver_case():
+    """Raw per-family solver outputs on random rays (bit-level check of the crossing solves)."""
+    g = tr.Generator().manual_seed(7)
+    n = 4000
+    xs = (tr.rand(n, 3, generator=g, dtype=tr.float64) - 0.5) * 6
+    xs[: n // 4] = (tr.rand(n // 4, 3, generator=g, dtype=tr.float64) - 0.5) * 1.2   # inside
+    rays = tr.randn(n, 3, generator=g, dtype=tr.float64)
+    rays /= tr.linalg.norm(rays, axis=-1)[..., None]
+    r_b = tr.linspace(0, 1, 11, dtype=tr.float64)
+    e_b = tr.linspace(0, tr.pi, 11, dtype=tr.float64)
+    a_b = tr.linspace(-tr.pi, tr.pi, 11, dtype=tr.float64)
+    out = dict(xs=xs.numpy(), rays=rays.numpy(), r_b=r_b.numpy(), e_b=e_b.numpy(),
+               a_b=a_b.numpy())
+    for key, fn, b in (('r', RT.r_torch, r_b), ('e', RT.e_torch, e_b), ('a', RT.a_torch, a_b)):
+        t, reg, _, neg = fn(b, xs.clone(), rays.clone())
+        out[f'{key}_t'] = t.numpy()
+        out[f'{key}_reg'] = reg.numpy().astype(np.int32)
+        out[f'{key}_neg'] = neg.numpy().astype(np.int8)
+    path = os.path.join(HERE, 'solvers.npz')
+    np.savez_compressed(path, **out)
+    print(f'solvers: {n} rays -> {os.path.getsize(path) / 1e3:.0f} kB')
+
+
+def main():
+    tr.manual_seed(0)
+    # C1: examples/single_vantage.py geometry at the BASELINE (50, 100) detector
+    grid = G.SphericalGrid(shape=(50, 50, 50))
+    geom = G.ConeRectGeom((50, 100), pos=(5, 0, 0), fov=(45, 45))
+    shells = tr.zeros(grid.shape)
+    shells[-1] += 1
+    shells[-10] += 1
+    save_case('c1_single_vantage', grid, geom,
+              densities=[shells, tr.rand(grid.shape)], ys=[tr.rand(geom.shape, dtype=tr.float64)],
+              note='C1 50^3, ConeRect (50,100) at (5,0,0)')
+
+    # C2 subset: 3 orbit observations of the BASELINE config
+    grid = G.SphericalGrid(shape=(50, 50, 50))
+    geoms = [G.ConeRectGeom((50, 100), pos=(5 * tr.cos(th), 5 * tr.sin(th), 1), fov=(45, 45))
+             for th in tr.linspace(0, 2 * tr.pi, 50)[[0, 17, 33]]]
+    geom = sum(geoms)
+    save_case('c2_orbit3', grid, geom, densities=[tr.rand(grid.shape)],
+              ys=[tr.rand(geom.shape, dtype=tr.float64)], note='3 of the 50 C2 orbit views')
+
+    # ConeCirc orbit (static_retrieval.py geometry, smaller detector); ring 0 passes the origin
+    grid = G.SphericalGrid(shape=(24, 20, 28))
+    geom = orbit(5, lambda p: G.ConeCircGeom(shape=(30, 24), pos=p, fov=(0, 45)))
+    x = tr.zeros(grid.shape)
+    x[:, 10:, :14] = 1
+    x[:, :10, 14:] = 1
+    save_case('circ_orbit', grid, geom, densities=[x, tr.rand(grid.shape)],
+              ys=[tr.rand(geom.shape, dtype=tr.float64)], note='ConeCirc orbit, 24x20x28 grid')
+
+    # starts inside the grid: behind-start integration in the start voxel
+    g = tr.Generator().manual_seed(3)
+    grid = G.SphericalGrid(shape=(12, 10, 14))
+    n = 3000
+    xs = (tr.rand(n, 3, generator=g, dtype=tr.float64) - 0.5) * 1.6
+    rays = tr.randn(n, 3, generator=g, dtype=tr.float64)
+    save_case('inside_starts', grid, G.ViewGeom(xs, rays), densities=[tr.rand(grid.shape)],
+              ys=[tr.rand((n,), dtype=tr.float64)], note='random starts in/around the unit grid')
+
+    # hollow / log-spaced / partial-angle grids with ConeRect views
+    grid = G.SphericalGrid(shape=(10, 12, 16), size_r=(0.3, 1), size_e=(0, tr.pi / 2),
+                           size_a=(-tr.pi / 2, tr.pi / 2))
+    geom = orbit(3, lambda p: G.ConeRectGeom((24, 20), pos=p, fov=(40, 40)))
+    save_case('partial_grid', grid, geom, densities=[tr.rand(grid.shape)],
+              ys=[tr.rand(geom.shape, dtype=tr.float64)], note='hollow, hemisphere, half azimuth')
+
+    grid = G.SphericalGrid(shape=(9, 11, 13), size_r=(0.1, 1), spacing='log',
+                           size_a=(0, 2 * tr.pi))
+    geom = orbit(3, lambda p: G.ConeRectGeom((20, 22), pos=p, fov=(45, 45)))
+    save_case('log_grid', grid, geom, densities=[tr.rand(grid.shape)],
+              ys=[tr.rand(geom.shape, dtype=tr.float64)], note='log radial, a in [0, 2pi] (no wrap)')
+
+    # dynamic grid: T views paired with T time slices (dynamic_measurements.py shape, small)
+    grid = G.SphericalGrid(shape=(6, 12, 10, 14))
+    geom = orbit(6, lambda p: G.ConeCircGeom(shape=(16, 12), pos=p, fov=(0, 45)))
+    x = tr.zeros(grid.shape)
+    x[:, :, 5:, :7] = 1
+    x[:, :, :5, 7:] = 1
+    for t in range(6):
+        x[t, :, (2 * t) % 10, :] += 1
+    save_case('dynamic_obs', grid, geom, densities=[x, tr.rand(grid.shape)],
+              note='dynamic (6,12,10,14), 6 ConeCirc views')
+
+    # the reference's own operator tests (test_raytracer.py:8-60), dense outputs kept
+    u = 0.001
+    starts = [[-100, u, u], [u, -100, u], [u, u, -100], [-100, 0, u], [0, -100, u],
+              [0, u, -100], [-100, u, 0], [u, -100, 0], [u, 0, -100], [5, 0, 0]]
+    dirs = [[1, 0, 0], [0, 1, 0], [0, 0, 1], [1, 0, 0], [0, 1, 0], [0, 0, 1], [1, 0, 0],
+            [0, 1, 0], [0, 0, 1],
+            [-0.99998629093170166016, 0.00413372274488210678, 0.00321511807851493359]]
+    grids = [G.SphericalGrid(shape=(50, 50, 50), size_r=(3, 25)), G.SphericalGrid(shape=(4, 4, 4)),
+             G.SphericalGrid(shape=(1, 4, 4)), G.SphericalGrid(shape=(4, 1, 4)),
+             G.SphericalGrid(shape=(4, 4, 1))]
+    for i, grid in enumerate(grids):
+        save_case(f'optest_{i}', grid, G.ViewGeom(starts, dirs),
+                  densities=[tr.ones(grid.shape), tr.rand(grid.shape)], keep_dense=True,
+                  note='test_raytracer.py:8-60 rays')
+    solver_case()
+
+
+if __name__ == '__main__':
+    main()

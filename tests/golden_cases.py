@@ -1,0 +1,101 @@
+"""Golden-fixture access and the canonical segment comparison used by the parity tests.
+
+Parity contract: per ray, drop segments shorter than TINY * scale, run-length
+merge consecutive equal voxels; voxel sequences must then be identical, lengths within
+LEN_RTOL (+ LEN_ATOL * scale absolute, for ulp-level distance differences from IEEE vs MKL sqrt).
+"""
+import os
+
+import numpy as np
+import torch as tr
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+CASES = ['c1_single_vantage', 'c2_orbit3', 'circ_orbit', 'inside_starts', 'partial_grid',
+         'log_grid', 'dynamic_obs'] + [f'optest_{i}' for i in range(5)]
+
+TINY = 1e-12           # segments shorter than TINY*scale are tie/ulp artefacts
+LEN_RTOL = 1e-12       # lengths, float64
+LEN_ATOL = 1e-12       # x scale
+F64_RTOL = 1e-10       # line integrals, float64
+F32_RTOL = 1e-5        # line integrals, float32
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+class FixtureGeom:
+    """Duck-typed geometry that hands the stored rays to Operator unchanged (no re-normalising)."""
+
+    def __init__(self, case):
+        self.ray_starts = tr.from_numpy(case['xs'])
+        self.rays = tr.from_numpy(case['rays'])
+        self.shape = tuple(int(s) for s in case['ray_shape'])
+
+
+def make_grid(case):
+    from sph_raytracer_amd import SphericalGrid
+    kw = dict(r_b=tr.from_numpy(case['r_b']), e_b=tr.from_numpy(case['e_b']),
+              a_b=tr.from_numpy(case['a_b']))
+    if bool(case['dynamic']):
+        kw['t'] = tr.arange(int(case['shape'][0]), dtype=tr.float64)
+    return SphericalGrid(**kw)
+
+
+def scale_of(case):
+    return max(float(np.abs(case['r_b']).max()), float(np.abs(case['xs']).max()))
+
+
+def canonical(ptr, vox, seg, tiny):
+    ptr = np.asarray(ptr, np.int64)
+    vox = np.asarray(vox, np.int64)
+    seg = np.asarray(seg, np.float64)
+    n = len(ptr) - 1
+    ray = np.repeat(np.arange(n), np.diff(ptr))
+    keep = seg >= tiny
+    ray, vox, seg = ray[keep], vox[keep], seg[keep]
+    if len(vox) == 0:
+        return np.zeros(n + 1, np.int64), vox, seg
+    new = np.ones(len(vox), bool)
+    new[1:] = (ray[1:] != ray[:-1]) | (vox[1:] != vox[:-1])
+    idx = np.flatnonzero(new)
+    seg_m = np.add.reduceat(seg, idx)
+    cnt = np.bincount(ray[idx], minlength=n)
+    ptr_m = np.zeros(n + 1, np.int64)
+    ptr_m[1:] = np.cumsum(cnt)
+    return ptr_m, vox[idx], seg_m
+
+
+def compare_segments(ref, got, scale, what=''):
+    """ref/got: (ptr, vox, len).  Returns None if equal under the contract, else a message."""
+    tiny = TINY * scale
+    pr, vr, lr = canonical(*ref, tiny)
+    pg, vg, lg = canonical(*got, tiny)
+    if len(pr) != len(pg):
+        return f'{what}: ray count {len(pr) - 1} != {len(pg) - 1}'
+    bad = np.flatnonzero(np.diff(pr) != np.diff(pg))
+    if len(bad) == 0 and not np.array_equal(vr, vg):
+        ray = np.repeat(np.arange(len(pr) - 1), np.diff(pr))
+        bad = np.unique(ray[vr != vg])
+    if len(bad):
+        i = int(bad[0])
+        return (f'{what}: {len(bad)} rays differ in voxel sequence; first ray {i}: '
+                f'ref {list(zip(vr[pr[i]:pr[i+1]].tolist(), lr[pr[i]:pr[i+1]].round(12).tolist()))} '
+                f'got {list(zip(vg[pg[i]:pg[i+1]].tolist(), lg[pg[i]:pg[i+1]].round(12).tolist()))}')
+    err = np.abs(lr - lg)
+    tol = LEN_RTOL * np.abs(lr) + LEN_ATOL * scale
+    if np.any(err > tol):
+        k = int(np.argmax(err - tol))
+        return f'{what}: length mismatch {lr[k]!r} vs {lg[k]!r} (|d|={err[k]:.3g})'
+    return None
+
+
+def rel_close(got, ref, rtol, floor=1e-30):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    den = np.maximum(np.abs(ref), floor)
+    err = np.abs(got - ref) / den
+    # near-zero integrals: compare absolutely against the row scale
+    err = np.where(np.abs(ref) < 1e-12, np.abs(got - ref), err)
+    return float(err.max()) if err.size else 0.0
