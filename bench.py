@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""Benchmark: steady-state forward Operator throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c5] [--no-cpu-baseline]
+
+Workload (default, BASELINE configs[1] = SURVEY §8(d) C2): a (50,50,50) SphericalGrid seen by a
+circular orbit of 50 ConeRectGeom((50,100), fov=(45,45)) views, 250,000 rays, float32 density.
+A step is one ``op(x)`` forward call on the cached trace (the reference's Operator.__call__,
+raytracer.py:692-713) — the drop-in call including its host overhead.  With N GPUs (one process
+each, torchrun) every rank traces its own 50-view slice of a 50*N-view orbit (weak scaling) and
+the image stack is all-gathered over RCCL every step (the only exchange of the path).
+
+One JSON line on rank 0: value = rays/s over all ranks; roofline of the forward kernel
+(algorithmic bytes per launch / its mean duration from HIP events over graph-replayed
+launches); cpu_baseline = the reference's forward (torch CPU on the reference's padded trace,
+oracle/ref_forward.py) on a bounded sample, timed on this host.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+METRIC = ('rays/sec (forward Operator) + peak GB resident, 50³ grid, 50×(50,100) sensor')
+
+CONFIGS = {
+    # name: (grid shape, views per GPU, detector, geometry kind, dtype, description)
+    'c2': ((50, 50, 50), 50, (50, 100), 'rect', torch.float32,
+           'C2: (50,50,50) grid, 50-view orbit x ConeRect (50,100), fp32 forward, trace cached'),
+    'c1': ((50, 50, 50), 1, (50, 100), 'rect1', torch.float32,
+           'C1: (50,50,50) grid, single ConeRect (50,100) view at (5,0,0), fp32 forward'),
+    'c3': ((128, 128, 128), 128, (128, 256), 'rect', torch.float32,
+           'C3: (128,128,128) grid, 128-view orbit x ConeRect (128,256), fp32 forward'),
+    'c5': ((64, 64, 64), 64, (100, 50), 'circ', torch.float64,
+           'C5: (64,64,64) grid, 64-view orbit x ConeCirc (100,50), fp64 forward'),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_geometry(cfg, rank, world):
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom, SphericalGrid
+    shape, n_views, det, kind, _, _ = cfg
+    grid = SphericalGrid(shape=shape)
+    if kind == 'rect1':
+        return grid, ConeRectGeom(det, pos=(5, 0, 0), fov=(45, 45))
+    thetas = torch.linspace(0, 2 * torch.pi, n_views * world)[rank * n_views:(rank + 1) * n_views]
+    geoms = []
+    for th in thetas:
+        pos = (5 * torch.cos(th), 5 * torch.sin(th), 1)
+        if kind == 'rect':
+            geoms.append(ConeRectGeom(det, pos=pos, fov=(45, 45)))
+        else:
+            geoms.append(ConeCircGeom(shape=det, pos=pos, fov=(0, 45)))
+    return grid, sum(geoms)
+
+
+def kernel_time_ms(op, x, reps=50):
+    """Mean duration of the forward kernel: `reps` launches captured in one HIP graph, replayed
+    between two HIP events on the launch stream (no host gaps)."""
+    n_chan, div, _ = op._layout(x.shape)
+    out = torch.empty(op._csr['n'], dtype=x.dtype, device=x.device)
+    op._lengths(x.dtype)
+    side = torch.cuda.Stream(device=x.device)
+    side.wait_stream(torch.cuda.current_stream(x.device))
+    try:
+        with torch.cuda.stream(side):
+            op._launch_forward(x, out, n_chan, div)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=side):
+                for _ in range(reps):
+                    op._launch_forward(x, out, n_chan, div)
+            g.replay()
+            torch.cuda.synchronize(x.device)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(side)
+            for _ in range(3):
+                g.replay()
+            e1.record(side)
+        torch.cuda.synchronize(x.device)
+        return e0.elapsed_time(e1) / (3 * reps), 'hip-graph replay, HIP events'
+    except Exception as exc:   # capture unsupported: back-to-back launches, events around them
+        log(f'graph capture failed ({exc}); timing back-to-back launches')
+        torch.cuda.synchronize(x.device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            op._launch_forward(x, out, n_chan, div)
+        e1.record()
+        torch.cuda.synchronize(x.device)
+        return e0.elapsed_time(e1) / reps, 'back-to-back launches, HIP events'
+
+
+def cpu_baseline(cfg, sample_views, reps):
+    """Reference forward (torch CPU on the reference's padded trace) on a bounded sample."""
+    from oracle import ref_forward
+    from sph_raytracer_amd import ConeRectGeom, ConeCircGeom, SphericalGrid
+    from sph_raytracer_amd.raytracer import find_starts
+    shape, n_views, det, kind, dtype, _ = cfg
+    grid = SphericalGrid(shape=shape)
+    views = min(sample_views, n_views)
+    thetas = torch.linspace(0, 2 * torch.pi, n_views)[:views]
+    mk = (lambda p: ConeRectGeom(det, pos=p, fov=(45, 45))) if kind.startswith('rect') else \
+        (lambda p: ConeCircGeom(shape=det, pos=p, fov=(0, 45)))
+    geom = sum(mk((5 * torch.cos(t), 5 * torch.sin(t), 1)) for t in thetas)
+    xs, rays = geom.ray_starts, geom.rays
+    starts = find_starts(grid, xs)
+    t0 = time.perf_counter()
+    regs, lens = ref_forward.dense_trace((grid.r_b, grid.e_b, grid.a_b), xs.numpy(), rays.numpy(),
+                                         starts.numpy())
+    t_trace = time.perf_counter() - t0
+    x = torch.rand(shape, dtype=dtype)
+    ref_forward.forward(regs, lens, x)           # warm-up
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ref_forward.forward(regs, lens, x)
+        times.append(time.perf_counter() - t0)
+    n = lens.numel() // lens.shape[-1]
+    med = sorted(times)[len(times) // 2]
+    return {'value': n / med, 'unit': 'rays/s', 'cores': torch.get_num_threads(),
+            'kind': 'port',
+            'sample': f'{views} of {n_views} views ({n} rays, K={lens.shape[-1]}), reference '
+                      f'forward (raytracer.py:703-713) in torch CPU on the padded trace, median '
+                      f'of {reps}; padded trace built by the C oracle in {t_trace:.2f} s',
+            'host_cpus': os.cpu_count()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=20)
+    ap.add_argument('--config', default='c2', choices=sorted(CONFIGS))
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-sample-views', type=int, default=10)
+    ap.add_argument('--cpu-reps', type=int, default=10)
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.gpus != world:
+        log(f'note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE')
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=dev)
+
+    from sph_raytracer_amd import Operator, build
+    build.build()
+    cfg = CONFIGS[args.config]
+    shape, n_views, det, kind, dtype, desc = cfg
+    torch.manual_seed(0)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    # ---- cold: geometry + trace + first forward ----------------------------------------------
+    torch.cuda.reset_peak_memory_stats(dev)
+    barrier()
+    t0 = time.perf_counter()
+    grid, geom = build_geometry(cfg, rank, world)
+    op = Operator(grid, geom, device=dev)
+    x = torch.rand(shape, dtype=dtype, device=dev)
+    y = op(x)
+    torch.cuda.synchronize(dev)
+    t_cold = time.perf_counter() - t0
+    n_rays = op._csr['n']
+    total_seg = op._csr['total']
+
+    stack = None
+    if dist is not None:
+        stack = torch.empty((world,) + tuple(y.shape), dtype=y.dtype, device=dev)
+
+    def step():
+        out = op(x)
+        if dist is not None:
+            dist.all_gather_into_tensor(stack, out)
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt, t_cold], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt, t_cold = tt.tolist()
+    peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9
+
+    k_ms, k_method = kernel_time_ms(op, x)
+    # bytes/ray = s_y + 4 + S*(4 + s_len + s_rho); f32 path s_len = s_rho = 4
+    es = x.element_size()
+    alg_bytes = n_rays * (es + 4) + total_seg * (4 + es + es)
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+
+    rec = {
+        'metric': METRIC,
+        'value': n_rays * world * args.steps / dt,
+        'unit': 'rays/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': dt / args.steps * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f32' if dtype == torch.float32 else 'f64',
+        'data': 'synthetic (torch.rand density, reference geometry)',
+        'config': {'workload': desc, 'grid': list(shape), 'views_per_gpu': n_views,
+                   'detector': list(det), 'rays_per_gpu': n_rays, 'segments_per_gpu': total_seg,
+                   'parallelism': f'obs-sharded x{world}' + (' + RCCL all-gather' if world > 1 else '')},
+        'peak_gb_resident': peak_gb,
+        'cold': {'rays_per_s': n_rays * world / t_cold, 'seconds': t_cold,
+                 'what': 'geometry + Operator trace + first forward'},
+        'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                     'kernel': 'forward_kernel<float,float>' if dtype == torch.float32
+                               else 'forward_kernel<double,double>',
+                     'kernel_ms': k_ms, 'bytes_per_launch': alg_bytes, 'timing': k_method},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            rec['cpu_baseline'] = cpu_baseline(cfg, args.cpu_sample_views, args.cpu_reps)
+        except Exception as exc:   # the baseline is informative; never fail the GPU bench on it
+            rec['cpu_baseline'] = {'value': None, 'error': repr(exc)}
+    else:
+        rec['cpu_baseline'] = None
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -118,7 +118,9 @@ int sphrt_partition(const int64_t *row_ptr, int64_t n, int64_t seg_per_block, in
  * If ray_chan_div > 0, ray i only sees channel c = i / ray_chan_div (dynamic grid paired with a
  * ViewGeomCollection, raytracer.py:705-706) and n_chan must be 1 in the call (the channel is
  * derived); otherwise every ray is integrated for all n_chan channels (static multichannel). */
-int sphrt_forward_f32(const int64_t *row_ptr, const int32_t *vox, const double *len, int64_t n,
+/* The float32 path streams a float32 copy of the segment lengths (sphrt_f64_to_f32 of `len`);
+ * every product and sum is float64 and rounded once. */
+int sphrt_forward_f32(const int64_t *row_ptr, const int32_t *vox, const float *len, int64_t n,
                       const int64_t *block_lo, int64_t nblocks, int64_t seg_per_block,
                       const float *density, int64_t n_chan, int64_t chan_stride,
                       int64_t ray_chan_div, float *out, int64_t out_chan_stride, void *stream);

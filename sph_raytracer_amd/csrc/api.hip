@@ -148,10 +148,12 @@ __device__ __forceinline__ int64_t seg_channel(const int64_t* row_ptr, int64_t s
     return o;
 }
 
-template <typename T>
+// T: density / image type; L: stored segment length type (float32 copy on the float32 path,
+// the float64 trace itself otherwise).  Products and sums are float64 either way.
+template <typename T, typename L>
 __global__ __launch_bounds__(256) void forward_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ vox,
-    const double* __restrict__ len, const int64_t* __restrict__ block_lo,
+    const L* __restrict__ len, const int64_t* __restrict__ block_lo,
     const T* __restrict__ density, int64_t n_chan, int64_t chan_stride, int64_t div,
     T* __restrict__ out, int64_t ocs) {
     __shared__ double prod[kApplyCap];
@@ -237,8 +239,8 @@ static unsigned grid_for(int64_t n, int64_t per_block, int64_t cap) {
     return (unsigned)g;
 }
 
-template <typename T>
-static int forward_impl(const int64_t* row_ptr, const int32_t* vox, const double* len, int64_t n,
+template <typename T, typename L>
+static int forward_impl(const int64_t* row_ptr, const int32_t* vox, const L* len, int64_t n,
                         const int64_t* block_lo, int64_t nblocks, int64_t spb, const T* density,
                         int64_t n_chan, int64_t chan_stride, int64_t div, T* out, int64_t ocs,
                         void* stream) {
@@ -247,7 +249,7 @@ static int forward_impl(const int64_t* row_ptr, const int32_t* vox, const double
     if (spb > kApplyCap) return fail("seg_per_block %lld exceeds the LDS stage %d", (long long)spb, kApplyCap);
     if (n_chan < 1) return fail("n_chan must be >= 1");
     if (div > 0 && n_chan != 1) return fail("ray_chan_div requires n_chan == 1");
-    hipLaunchKernelGGL((forward_kernel<T>), dim3((unsigned)nblocks), dim3(256), 0,
+    hipLaunchKernelGGL((forward_kernel<T, L>), dim3((unsigned)nblocks), dim3(256), 0,
                        (hipStream_t)stream, row_ptr, vox, len, block_lo, density, n_chan,
                        chan_stride, div, out, ocs);
     return check_launch("forward_kernel");
@@ -375,21 +377,21 @@ extern "C" int sphrt_partition(const int64_t* row_ptr, int64_t n, int64_t spb, i
     return check_launch("partition_kernel");
 }
 
-extern "C" int sphrt_forward_f32(const int64_t* row_ptr, const int32_t* vox, const double* len,
+extern "C" int sphrt_forward_f32(const int64_t* row_ptr, const int32_t* vox, const float* len,
                                  int64_t n, const int64_t* block_lo, int64_t nblocks,
                                  int64_t spb, const float* density, int64_t n_chan,
                                  int64_t chan_stride, int64_t div, float* out, int64_t ocs,
                                  void* stream) {
-    return forward_impl<float>(row_ptr, vox, len, n, block_lo, nblocks, spb, density, n_chan,
-                               chan_stride, div, out, ocs, stream);
+    return forward_impl<float, float>(row_ptr, vox, len, n, block_lo, nblocks, spb, density,
+                                      n_chan, chan_stride, div, out, ocs, stream);
 }
 extern "C" int sphrt_forward_f64(const int64_t* row_ptr, const int32_t* vox, const double* len,
                                  int64_t n, const int64_t* block_lo, int64_t nblocks,
                                  int64_t spb, const double* density, int64_t n_chan,
                                  int64_t chan_stride, int64_t div, double* out, int64_t ocs,
                                  void* stream) {
-    return forward_impl<double>(row_ptr, vox, len, n, block_lo, nblocks, spb, density, n_chan,
-                                chan_stride, div, out, ocs, stream);
+    return forward_impl<double, double>(row_ptr, vox, len, n, block_lo, nblocks, spb, density,
+                                        n_chan, chan_stride, div, out, ocs, stream);
 }
 
 extern "C" int sphrt_adjoint_accumulate(const int64_t* row_ptr, const int32_t* vox,

@@ -70,6 +70,21 @@ __device__ __forceinline__ RayGeo make_ray(double x0, double x1, double x2,
     return g;
 }
 
+// The per-family API: called on their own, e_torch normalises its input once
+// (raytracer.py:365) and a_torch not at all (raytracer.py:471-552), so the cone/plane direction
+// is u resp. the raw input, not the twice-normalised w that trace_indices hands them.
+__device__ __forceinline__ RayGeo make_ray_family(double x0, double x1, double x2, double d0,
+                                                  double d1, double d2, int family) {
+    RayGeo g = make_ray(x0, x1, x2, d0, d1, d2);
+    if (family == 1) {
+        g.w0 = g.u0; g.w1 = g.u1; g.w2 = g.u2;
+    } else if (family == 2) {
+        g.w0 = d0; g.w1 = d1; g.w2 = d2;
+    }
+    g.wx = dot_seq(g.w0, g.w1, g.w2, x0, x1, x2);
+    return g;
+}
+
 // ---- spheres (r_torch, raytracer.py:288-323) ------------------------------------------------
 // Region entered at distance t on sphere j: j - [u . p(t) < 0], j == nr -> -1 (outside).
 __device__ __forceinline__ int sphere_region(const RayGeo& g, double t, int j, int nr,

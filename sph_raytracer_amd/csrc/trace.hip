@@ -466,7 +466,7 @@ __global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int fa
     double x[3], d[3];
     int s[3];
     load_ray(R, ray, x, d, s);
-    const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
+    const RayGeo g = make_ray_family(x[0], x[1], x[2], d[0], d[1], d[2], family);
     if (family == 0) {
         const int w = 2 * G.nbr;
         for (int j = 0; j < G.nbr; ++j) {

@@ -1,0 +1,225 @@
+"""CPU-side checks: geometry API + bit-identity with the reference geometry, host logic, and the
+C ABI library (loads and exports every symbol include/sphrt.h declares; no compute without GPU)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch as tr
+
+import golden_cases as gc
+from known_answers import START_CASES
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def check(a, b):
+    return tr.allclose(tr.asarray(a).type(tr.float32).flatten().squeeze(),
+                       tr.asarray(b).type(tr.float32).flatten().squeeze(), atol=1e-2)
+
+
+# ---- test_all.py:176-302 geometry tests, on this package ---------------------------------------
+
+def test_sphericalgrid_static():
+    from sph_raytracer_amd import SphericalGrid
+    grid = SphericalGrid(shape=(10, 11, 12))
+    assert not grid.dynamic
+    assert (len(grid.r_b), len(grid.e_b), len(grid.a_b)) == (11, 12, 13)
+    grid = SphericalGrid(r_b=[1, 2], e_b=[1, 2, 3], a_b=[1, 2, 3, 4])
+    assert grid.shape == (1, 2, 3) and not grid.dynamic
+
+    def check_bounds(g):
+        for c, b in ((g.r, g.r_b), (g.e, g.e_b), (g.a, g.a_b)):
+            assert len(c) == len(b) - 1
+            assert all(c > b[:-1]) and all(c < b[1:])
+    check_bounds(grid)
+    check_bounds(SphericalGrid(shape=(10, 11, 12), size_r=(1, 10), size_e=(0, tr.pi),
+                               size_a=(0, 2 * tr.pi), spacing='log'))
+    for x in (grid.r, grid.e, grid.a):
+        assert type(x) is tr.Tensor
+    assert grid.mesh.ndim == 4
+
+
+def test_sphericalgrid_dynamic():
+    from sph_raytracer_amd import SphericalGrid
+    grid = SphericalGrid(shape=(9, 10, 11, 12))
+    assert grid.dynamic
+    assert (len(grid.t), len(grid.r_b), len(grid.e_b), len(grid.a_b)) == (9, 11, 12, 13)
+    grid = SphericalGrid(t=[1], r_b=[1, 2], e_b=[1, 2, 3], a_b=[1, 2, 3, 4])
+    assert grid.shape == (1, 1, 2, 3) and grid.dynamic
+    assert len(grid.nptime) == grid.shape.t
+    for x in (grid.t, grid.r, grid.e, grid.a):
+        assert type(x) is tr.Tensor
+    assert grid.mesh.ndim == 5
+
+
+def test_find_starts():
+    from sph_raytracer_amd import SphericalGrid
+    from sph_raytracer_amd.raytracer import find_starts
+    for shape, x, exp in START_CASES:
+        assert check(find_starts(SphericalGrid(shape=shape), x), exp)
+
+
+def test_conerectgeom():
+    from sph_raytracer_amd import ConeRectGeom
+    g = ConeRectGeom((11, 11), (4, 0, 1), fov=(23, 45))
+    assert check(tr.dot(g.rays[5, 0], g.rays[5, -1]), tr.cos(tr.deg2rad(g.fov[1])))
+    assert check(tr.dot(g.rays[0, 5], g.rays[-1, 5]), tr.cos(tr.deg2rad(g.fov[0])))
+    assert check(g.rays[5, 5], g.lookdir)
+    g = ConeRectGeom((1, 1), (1, 0, 0), (-1, 0, 0), (0, 1, 0), fov=(23, 45))
+    assert check(g.rays[0, 0], g.lookdir)
+    g._wireframe
+
+
+def test_conecircgeom():
+    from sph_raytracer_amd import ConeCircGeom
+    g = ConeCircGeom((11, 11), (1, 0, 0), (-1, 0, 0), (0, 1, 0), fov=(0, 45))
+    assert check(tr.dot(g.rays[-1, 0], g.rays[-1, 5]), tr.cos(tr.deg2rad(g.fov[1])))
+    assert check(g.rays[0, 0], g.lookdir)
+    g = ConeCircGeom((1, 1), (1, 0, 0), (-1, 0, 0), (0, 1, 0), fov=(0, 45))
+    assert check(g.rays[0, 0], g.lookdir)
+    g._wireframe
+
+
+def test_parallelgeom():
+    from sph_raytracer_amd import ParallelGeom
+    g = ParallelGeom((11, 11), (4, 0, 1), size=(2, 3))
+    assert check(tr.linalg.norm(g.ray_starts[5, 0] - g.ray_starts[5, -1]), g.size[1])
+    assert check(tr.linalg.norm(g.ray_starts[0, 5] - g.ray_starts[-1, 5]), g.size[0])
+    assert all((g.rays == g.lookdir).flatten())
+    g = ParallelGeom((1, 1), (1, 0, 0), (-1, 0, 0), (0, 1, 0))
+    assert check(g.rays[0, 0], g.lookdir)
+    g._wireframe
+
+
+def test_viewgeom():
+    from sph_raytracer_amd import ViewGeom
+    rays = tr.rand((4, 4, 3))
+    g = ViewGeom(rays=rays, ray_starts=tr.tensor((10, 0, 0)).broadcast_to(rays.shape))
+    g._wireframe
+    assert g.shape == (4, 4)
+
+
+def test_model_instantiation():
+    """test_model.py:7-15."""
+    from sph_raytracer_amd import SphericalGrid
+    from sph_raytracer_amd.model import AxisAlignmentModel, CubesModel, FullyDenseModel
+    g = SphericalGrid()
+    for model in (FullyDenseModel, CubesModel, AxisAlignmentModel):
+        m = model(g)
+        assert m(tr.rand(m.coeffs_shape)).shape == g.shape
+
+
+# ---- geometry is bit-identical to the reference's (rays are Operator inputs) ----------------
+
+def test_conerect_rays_bit_identical():
+    from sph_raytracer_amd import ConeRectGeom
+    case = gc.load('c1_single_vantage')
+    g = ConeRectGeom((50, 100), pos=(5, 0, 0), fov=(45, 45))
+    assert np.array_equal(g.rays.numpy(), case['rays'])
+    assert np.array_equal(g.ray_starts.numpy(), case['xs'])
+
+
+def test_orbit_collections_bit_identical():
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom
+    case = gc.load('circ_orbit')
+    geoms = [ConeCircGeom(shape=(30, 24), pos=(5 * tr.cos(th), 5 * tr.sin(th), 1), fov=(0, 45))
+             for th in tr.linspace(0, 2 * tr.pi, 5)]
+    coll = sum(geoms)
+    assert coll.shape == (5, 30, 24)
+    assert np.array_equal(coll.rays.numpy(), case['rays'])
+    assert np.array_equal(coll.ray_starts.numpy(), case['xs'])
+    case = gc.load('c2_orbit3')
+    th = tr.linspace(0, 2 * tr.pi, 50)[[0, 17, 33]]
+    coll = sum(ConeRectGeom((50, 100), pos=(5 * tr.cos(a), 5 * tr.sin(a), 1), fov=(45, 45))
+               for a in th)
+    assert np.array_equal(coll.rays.numpy(), case['rays'])
+
+
+def test_grid_boundaries_bit_identical():
+    from sph_raytracer_amd import SphericalGrid
+    case = gc.load('log_grid')
+    g = SphericalGrid(shape=(9, 11, 13), size_r=(0.1, 1), spacing='log', size_a=(0, 2 * tr.pi))
+    for k in ('r_b', 'e_b', 'a_b'):
+        assert np.array_equal(getattr(g, k).numpy(), case[k])
+
+
+# ---- host logic ------------------------------------------------------------------------------
+
+def test_density_layouts():
+    """Output shapes / channel rules of raytracer.py:703-712 (no GPU needed)."""
+    from sph_raytracer_amd import SphericalGrid
+    from sph_raytracer_amd.raytracer import _layout_for
+    static, dyn = SphericalGrid((2, 3, 4)), SphericalGrid((10, 2, 3, 4))
+    assert _layout_for(static, (64, 64), (2, 3, 4)) == (1, 0, (64, 64))
+    assert _layout_for(static, (64, 64), (10, 2, 3, 4)) == (10, 0, (10, 64, 64))
+    assert _layout_for(static, (), (5, 2, 3, 4)) == (5, 0, (5,))
+    assert _layout_for(dyn, (64, 64), (10, 2, 3, 4)) == (10, 0, (10, 64, 64))
+    assert _layout_for(dyn, (10, 8, 6), (10, 2, 3, 4)) == (1, 48, (10, 8, 6))
+    assert _layout_for(dyn, (4,), (10, 2, 3, 4)) == (10, 0, (10, 1, 4))   # App. C.5 quirk
+    with pytest.raises(ValueError):
+        _layout_for(static, (64, 64), (2, 3, 5))
+
+
+def test_no_cpu_fallback():
+    """Without a GPU the product path fails loudly instead of computing on the CPU."""
+    if tr.cuda.is_available():
+        pytest.skip('GPU present')
+    from sph_raytracer_amd import ConeRectGeom, Operator, SphericalGrid
+    from sph_raytracer_amd.raytracer import line_integrals, r_torch
+    grid, geom = SphericalGrid((4, 4, 4)), ConeRectGeom((4, 4), (5, 0, 0))
+    with pytest.raises(RuntimeError, match='GPU'):
+        Operator(grid, geom)
+    with pytest.raises(RuntimeError, match='GPU'):
+        line_integrals(grid, geom, tr.ones(grid.shape))
+    with pytest.raises(RuntimeError, match='GPU'):
+        r_torch([1.0], [(0, 0, 0)], [(1, 0, 0)])
+
+
+def test_gd_with_linear_stand_in():
+    """gd() contract (retrieval.py:24-127) with a dense linear stand-in for f."""
+    from sph_raytracer_amd import SphericalGrid
+    from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
+    from sph_raytracer_amd.model import FullyDenseModel
+    from sph_raytracer_amd.retrieval import gd
+    grid = SphericalGrid((3, 4, 5))
+    A = tr.rand(30, 60, dtype=tr.float64)
+
+    class F:
+        device = 'cpu'
+
+        def __init__(self):
+            self.grid = grid
+
+        def __call__(self, d):
+            return (A @ d.reshape(-1)).reshape(5, 6)
+    f = F()
+    truth = tr.rand(grid.shape, dtype=tr.float64)
+    y = f(truth).detach()
+    coeffs, y_res, losses = gd(f, y, FullyDenseModel(grid), num_iterations=20, lr=1e-2,
+                               loss_fns=[SquareLoss(), 0.5 * NegRegularizer()], progress_bar=False)
+    hist = list(losses.values())[0]
+    assert len(hist) == 20 and hist[-1] < hist[0]
+    assert y_res.shape == (5, 6)
+
+
+# ---- the C ABI library -------------------------------------------------------------------------
+
+def _declared_symbols():
+    hdr = open(os.path.join(ROOT, 'include', 'sphrt.h')).read()
+    return sorted(set(re.findall(r'\b(sphrt_[a-z0-9_]+)\s*\(', hdr)))
+
+
+def test_library_builds_and_exports_header():
+    from sph_raytracer_amd import _lib, build
+    build.build()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    declared = _declared_symbols()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(lib, name), f'{name} declared in include/sphrt.h but not exported'
+    assert sorted(_lib.EXPORTED) == declared, 'ctypes bindings out of sync with the header'
+    lib = _lib.load()
+    assert lib.sphrt_version().startswith(b'sph_raytracer_amd')
+    assert lib.sphrt_scan_workspace_bytes(10_000) > 0
