@@ -107,35 +107,50 @@ int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64
                      int32_t *vox, double *len, void *workspace, size_t workspace_size,
                      void *stream);
 
-/* ---- static work partition of a CSR for the apply kernels -------------------------------- */
-/* block_lo[b] = first ray whose row starts at or after b*seg_per_block, b = 0..nblocks
- * (nblocks = row_ptr[n] / seg_per_block + 1; block_lo has nblocks+1 entries). */
-int sphrt_partition(const int64_t *row_ptr, int64_t n, int64_t seg_per_block, int64_t *block_lo,
-                    int64_t nblocks, void *stream);
+/* ---- row index of the trace, built once (the apply kernels' work partition) ---------------- */
+/* A traced operator: the CSR above plus
+ *   vox     — bit 31 (SPHRT_ROW_HEAD) set on the first segment of every non-empty ray,
+ *   row_ray — ray id of every non-empty row, in order,
+ *   blocks  — n_blocks x 5 int64 {ray_lo, ray_hi, seg_lo, seg_hi, row_lo}: one workgroup per
+ *             block owns the whole rows starting in its slice of segments.
+ * sphrt_csr_index() fills them from row_ptr; n_blocks = sphrt_csr_blocks(n_segments).  `len32`
+ * is the float32 copy of `len` used by the float32 forward (sphrt_f64_to_f32). */
+#define SPHRT_ROW_HEAD 0x80000000u
+typedef struct sphrt_csr {
+    int64_t n_rays;
+    int64_t n_segments;
+    const int64_t *row_ptr;
+    const int32_t *vox;
+    const double *len;
+    const float *len32;
+    const int32_t *row_ray;
+    const int64_t *blocks;
+    int64_t n_blocks;
+} sphrt_csr;
+
+int64_t sphrt_csr_blocks(int64_t n_segments);
+size_t sphrt_csr_index_workspace_bytes(int64_t n_rays);
+int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_t *row_ray,
+                    int64_t *blocks, int64_t n_blocks, void *workspace, void *stream);
 
 /* ---- forward line integral on the CSR (replaces Operator.__call__, raytracer.py:692-713) -- */
 /* out[c*out_chan_stride + i] = sum_s density[c*chan_stride + vox[s]] * len[s] over ray i's row.
  * If ray_chan_div > 0, ray i only sees channel c = i / ray_chan_div (dynamic grid paired with a
  * ViewGeomCollection, raytracer.py:705-706) and n_chan must be 1 in the call (the channel is
- * derived); otherwise every ray is integrated for all n_chan channels (static multichannel). */
-/* The float32 path streams a float32 copy of the segment lengths (sphrt_f64_to_f32 of `len`);
- * every product and sum is float64 and rounded once. */
-int sphrt_forward_f32(const int64_t *row_ptr, const int32_t *vox, const float *len, int64_t n,
-                      const int64_t *block_lo, int64_t nblocks, int64_t seg_per_block,
-                      const float *density, int64_t n_chan, int64_t chan_stride,
-                      int64_t ray_chan_div, float *out, int64_t out_chan_stride, void *stream);
-int sphrt_forward_f64(const int64_t *row_ptr, const int32_t *vox, const double *len, int64_t n,
-                      const int64_t *block_lo, int64_t nblocks, int64_t seg_per_block,
-                      const double *density, int64_t n_chan, int64_t chan_stride,
-                      int64_t ray_chan_div, double *out, int64_t out_chan_stride, void *stream);
+ * derived); otherwise every ray is integrated for all n_chan channels (static multichannel).
+ * Products and sums are float64, rounded once; the float32 path streams `len32`. */
+int sphrt_forward_f32(const sphrt_csr *csr, const float *density, int64_t n_chan,
+                      int64_t chan_stride, int64_t ray_chan_div, float *out,
+                      int64_t out_chan_stride, void *stream);
+int sphrt_forward_f64(const sphrt_csr *csr, const double *density, int64_t n_chan,
+                      int64_t chan_stride, int64_t ray_chan_div, double *out,
+                      int64_t out_chan_stride, void *stream);
 
 /* ---- adjoint / back-projection (replaces Operator.T, raytracer.py:715-748, and the autograd
  * backward of raytracer.py:710) ------------------------------------------------------------ */
 /* acc[c*chan_stride + vox[s]] += y[c*y_chan_stride + i] * len[s], float64 atomics into a zeroed
  * float64 accumulator `acc` (caller-allocated).  Same channel rules as forward. */
-int sphrt_adjoint_accumulate(const int64_t *row_ptr, const int32_t *vox, const double *len,
-                             int64_t n, const int64_t *block_lo, int64_t nblocks,
-                             int64_t seg_per_block, const void *y, int y_is_f64, int64_t n_chan,
+int sphrt_adjoint_accumulate(const sphrt_csr *csr, const void *y, int y_is_f64, int64_t n_chan,
                              int64_t y_chan_stride, int64_t ray_chan_div, double *acc,
                              int64_t chan_stride, void *stream);
 /* dst[i] = (float)src[i] — rounding the float64 accumulator to a float32 result. */

@@ -33,6 +33,14 @@ class RayBatch(ctypes.Structure):
                 ('xs', c_vp), ('rays', c_vp), ('start', c_vp)]
 
 
+class CSR(ctypes.Structure):
+    _fields_ = [('n_rays', c_i64), ('n_segments', c_i64), ('row_ptr', c_vp), ('vox', c_vp),
+                ('len', c_vp), ('len32', c_vp), ('row_ray', c_vp), ('blocks', c_vp),
+                ('n_blocks', c_i64)]
+
+
+ROW_HEAD = 0x80000000
+
 # (name, restype, argtypes) — mirrors include/sphrt.h one to one
 _SIGNATURES = [
     ('sphrt_plan_create', c_int, [ctypes.POINTER(GridDesc), c_int, ctypes.POINTER(c_vp)]),
@@ -48,13 +56,15 @@ _SIGNATURES = [
     ('sphrt_scan_counts', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     ('sphrt_trace_fill', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_vp, c_vp, c_vp,
                                  ctypes.c_size_t, c_vp]),
-    ('sphrt_partition', c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
-    ('sphrt_forward_f32', c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
-                                  c_i64, c_i64, c_vp, c_i64, c_vp]),
-    ('sphrt_forward_f64', c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64,
-                                  c_i64, c_i64, c_vp, c_i64, c_vp]),
-    ('sphrt_adjoint_accumulate', c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_vp,
-                                         c_int, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp]),
+    ('sphrt_csr_blocks', c_i64, [c_i64]),
+    ('sphrt_csr_index_workspace_bytes', ctypes.c_size_t, [c_i64]),
+    ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    ('sphrt_forward_f32', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,
+                                  c_vp]),
+    ('sphrt_forward_f64', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,
+                                  c_vp]),
+    ('sphrt_adjoint_accumulate', c_int, [ctypes.POINTER(CSR), c_vp, c_int, c_i64, c_i64, c_i64,
+                                         c_vp, c_i64, c_vp]),
     ('sphrt_f64_to_f32', c_int, [c_vp, c_vp, c_i64, c_vp]),
     ('sphrt_trace_integrate_f32', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_i64, c_i64,
                                           c_i64, c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),

@@ -1,4 +1,4 @@
-// api.hip — plan management, CSR scan/partition, forward and adjoint kernels, error plumbing.
+// api.hip — plan management, the count -> row-pointer scan, conversions, error plumbing.
 #include <math.h>
 #include <string.h>
 
@@ -117,116 +117,6 @@ __global__ __launch_bounds__(256) void scan_apply_kernel(const int32_t* counts, 
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// static partition: block b owns the rays whose row starts in [b*spb, (b+1)*spb)
-__global__ __launch_bounds__(256) void partition_kernel(const int64_t* row_ptr, int64_t n,
-                                                        int64_t spb, int64_t* block_lo,
-                                                        int64_t nblocks) {
-    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b > nblocks) return;
-    const int64_t target = b * spb;
-    int64_t lo = 0, hi = n;  // first i in [0, n) with row_ptr[i] >= target, else n
-    while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if (row_ptr[mid] < target) lo = mid + 1;
-        else hi = mid;
-    }
-    block_lo[b] = lo;
-}
-
-// ---------------------------------------------------------------------------------------------
-// forward line integral over the CSR.  Per partition block: segment-parallel products staged
-// in LDS (balanced gathers, coalesced vox/len streams), then one thread per ray sums its row.
-constexpr int kApplyCap = 4096;
-
-// channel of segment s when every observation has its own time slice (ray_chan_div mode)
-__device__ __forceinline__ int64_t seg_channel(const int64_t* row_ptr, int64_t s, int64_t lo,
-                                               int64_t hi, int64_t div) {
-    int64_t o = lo / div;
-    const int64_t olast = (hi - 1) / div;
-    while (o < olast && row_ptr[(o + 1) * div] <= s) ++o;
-    return o;
-}
-
-// T: density / image type; L: stored segment length type (float32 copy on the float32 path,
-// the float64 trace itself otherwise).  Products and sums are float64 either way.
-template <typename T, typename L>
-__global__ __launch_bounds__(256) void forward_kernel(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ vox,
-    const L* __restrict__ len, const int64_t* __restrict__ block_lo,
-    const T* __restrict__ density, int64_t n_chan, int64_t chan_stride, int64_t div,
-    T* __restrict__ out, int64_t ocs) {
-    __shared__ double prod[kApplyCap];
-    const int64_t lo = block_lo[blockIdx.x], hi = block_lo[blockIdx.x + 1];
-    if (lo >= hi) return;
-    const int64_t s0 = row_ptr[lo], s1 = row_ptr[hi];
-    const int64_t nsg = s1 - s0;
-    const int tid = threadIdx.x;
-    for (int64_t c = 0; c < n_chan; ++c) {
-        const T* rho = density + c * chan_stride;
-        if (nsg <= kApplyCap) {
-            for (int64_t s = s0 + tid; s < s1; s += 256) {
-                const T* rc = div > 0 ? density + seg_channel(row_ptr, s, lo, hi, div) * chan_stride
-                                      : rho;
-                prod[s - s0] = (double)rc[vox[s]] * len[s];
-            }
-            __syncthreads();
-            for (int64_t r = lo + tid; r < hi; r += 256) {
-                const int64_t a = row_ptr[r] - s0, b = row_ptr[r + 1] - s0;
-                double acc = 0.0;
-                for (int64_t q = a; q < b; ++q) acc += prod[q];
-                out[c * ocs + r] = (T)acc;
-            }
-            __syncthreads();
-        } else {  // a row longer than the LDS stage: direct (rare)
-            for (int64_t r = lo + tid; r < hi; r += 256) {
-                const T* rc = div > 0 ? density + (r / div) * chan_stride : rho;
-                double acc = 0.0;
-                for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) acc += (double)rc[vox[q]] * len[q];
-                out[c * ocs + r] = (T)acc;
-            }
-        }
-    }
-}
-
-// adjoint: acc[chan][vox] += y[chan][ray] * len, float64 atomics.  Per block the ray values are
-// spread over their segments in LDS, then segments are streamed in order (coalesced).
-template <typename TY>
-__global__ __launch_bounds__(256) void adjoint_kernel(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ vox,
-    const double* __restrict__ len, const int64_t* __restrict__ block_lo,
-    const TY* __restrict__ y, int64_t n_chan, int64_t ycs, int64_t div, double* acc,
-    int64_t chan_stride) {
-    __shared__ double yb[kApplyCap];
-    const int64_t lo = block_lo[blockIdx.x], hi = block_lo[blockIdx.x + 1];
-    if (lo >= hi) return;
-    const int64_t s0 = row_ptr[lo], s1 = row_ptr[hi];
-    const int64_t nsg = s1 - s0;
-    const int tid = threadIdx.x;
-    for (int64_t c = 0; c < n_chan; ++c) {
-        const TY* yc = y + c * ycs;
-        if (nsg <= kApplyCap) {
-            for (int64_t r = lo + tid; r < hi; r += 256) {
-                const double v = (double)yc[r];
-                for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) yb[q - s0] = v;
-            }
-            __syncthreads();
-            for (int64_t s = s0 + tid; s < s1; s += 256) {
-                double* ac = div > 0 ? acc + seg_channel(row_ptr, s, lo, hi, div) * chan_stride
-                                     : acc + c * chan_stride;
-                atomicAdd(ac + vox[s], yb[s - s0] * len[s]);
-            }
-            __syncthreads();
-        } else {
-            for (int64_t r = lo + tid; r < hi; r += 256) {
-                double* ac = div > 0 ? acc + (r / div) * chan_stride : acc + c * chan_stride;
-                const double v = (double)yc[r];
-                for (int64_t q = row_ptr[r]; q < row_ptr[r + 1]; ++q) atomicAdd(ac + vox[q], v * len[q]);
-            }
-        }
-    }
-}
-
 __global__ __launch_bounds__(256) void f64_to_f32_kernel(const double* src, float* dst, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
         dst[i] = (float)src[i];
@@ -237,22 +127,6 @@ static unsigned grid_for(int64_t n, int64_t per_block, int64_t cap) {
     if (g < 1) g = 1;
     if (g > cap) g = cap;
     return (unsigned)g;
-}
-
-template <typename T, typename L>
-static int forward_impl(const int64_t* row_ptr, const int32_t* vox, const L* len, int64_t n,
-                        const int64_t* block_lo, int64_t nblocks, int64_t spb, const T* density,
-                        int64_t n_chan, int64_t chan_stride, int64_t div, T* out, int64_t ocs,
-                        void* stream) {
-    if (n == 0) return 0;
-    if (nblocks < 1 || nblocks > 0x7fffffff) return fail("bad partition block count %lld", (long long)nblocks);
-    if (spb > kApplyCap) return fail("seg_per_block %lld exceeds the LDS stage %d", (long long)spb, kApplyCap);
-    if (n_chan < 1) return fail("n_chan must be >= 1");
-    if (div > 0 && n_chan != 1) return fail("ray_chan_div requires n_chan == 1");
-    hipLaunchKernelGGL((forward_kernel<T, L>), dim3((unsigned)nblocks), dim3(256), 0,
-                       (hipStream_t)stream, row_ptr, vox, len, block_lo, density, n_chan,
-                       chan_stride, div, out, ocs);
-    return check_launch("forward_kernel");
 }
 
 }  // namespace sphrt
@@ -365,55 +239,6 @@ extern "C" int sphrt_scan_counts(const int32_t* counts, int64_t n, int64_t* row_
     hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nb), dim3(256), 0, st, counts, n, bs,
                        row_ptr);
     return check_launch("scan_apply");
-}
-
-extern "C" int sphrt_partition(const int64_t* row_ptr, int64_t n, int64_t spb, int64_t* block_lo,
-                               int64_t nblocks, void* stream) {
-    if (spb < 1) return fail("seg_per_block must be >= 1");
-    if (nblocks < 1) return fail("nblocks must be >= 1");
-    const int64_t m = nblocks + 1;
-    hipLaunchKernelGGL(partition_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, row_ptr, n, spb, block_lo, nblocks);
-    return check_launch("partition_kernel");
-}
-
-extern "C" int sphrt_forward_f32(const int64_t* row_ptr, const int32_t* vox, const float* len,
-                                 int64_t n, const int64_t* block_lo, int64_t nblocks,
-                                 int64_t spb, const float* density, int64_t n_chan,
-                                 int64_t chan_stride, int64_t div, float* out, int64_t ocs,
-                                 void* stream) {
-    return forward_impl<float, float>(row_ptr, vox, len, n, block_lo, nblocks, spb, density,
-                                      n_chan, chan_stride, div, out, ocs, stream);
-}
-extern "C" int sphrt_forward_f64(const int64_t* row_ptr, const int32_t* vox, const double* len,
-                                 int64_t n, const int64_t* block_lo, int64_t nblocks,
-                                 int64_t spb, const double* density, int64_t n_chan,
-                                 int64_t chan_stride, int64_t div, double* out, int64_t ocs,
-                                 void* stream) {
-    return forward_impl<double, double>(row_ptr, vox, len, n, block_lo, nblocks, spb, density,
-                                        n_chan, chan_stride, div, out, ocs, stream);
-}
-
-extern "C" int sphrt_adjoint_accumulate(const int64_t* row_ptr, const int32_t* vox,
-                                        const double* len, int64_t n, const int64_t* block_lo,
-                                        int64_t nblocks, int64_t spb, const void* y, int y_is_f64,
-                                        int64_t n_chan, int64_t ycs, int64_t div, double* acc,
-                                        int64_t chan_stride, void* stream) {
-    if (n == 0) return 0;
-    if (nblocks < 1 || nblocks > 0x7fffffff) return fail("bad partition block count");
-    if (spb > kApplyCap) return fail("seg_per_block exceeds the LDS stage");
-    if (n_chan < 1) return fail("n_chan must be >= 1");
-    if (div > 0 && n_chan != 1) return fail("ray_chan_div requires n_chan == 1");
-    hipStream_t st = (hipStream_t)stream;
-    if (y_is_f64)
-        hipLaunchKernelGGL((adjoint_kernel<double>), dim3((unsigned)nblocks), dim3(256), 0, st,
-                           row_ptr, vox, len, block_lo, (const double*)y, n_chan, ycs, div, acc,
-                           chan_stride);
-    else
-        hipLaunchKernelGGL((adjoint_kernel<float>), dim3((unsigned)nblocks), dim3(256), 0, st,
-                           row_ptr, vox, len, block_lo, (const float*)y, n_chan, ycs, div, acc,
-                           chan_stride);
-    return check_launch("adjoint_kernel");
 }
 
 extern "C" int sphrt_f64_to_f32(const double* src, float* dst, int64_t n, void* stream) {

@@ -192,32 +192,46 @@ __device__ __forceinline__ int scan_max(int v, int lane) {
     return v;
 }
 
-// Does any group of exactly equal distances hold two crossings that update a region row?  Then
-// the result depends on the reference's tie order (only updater/updater ties can change a row's
-// final value within the group; the segments inside a group have zero length).
+// value a candidate writes into region row `row` (0 r, 1 e, 2 a); start entry: the start voxel
+__device__ __forceinline__ int row_value(uint32_t pay, int row, int start_c, const int* sv) {
+    return (int)(pay >> 16) == start_c ? sv[row] : (int)(pay & 0xffffu) - 2;
+}
+
+// Does any group of exactly equal distances hold two crossings that write DIFFERENT values into
+// the same region row?  Only then does the reference's tie order change a row's value after the
+// group (the segments inside a group have zero length).  Equal-valued ties — a double root of
+// the e = pi/2 "cone", a tangent sphere, a boundary crossing that re-enters the start voxel —
+// are order-independent and stay on the fast path.
 __device__ bool ambiguous_ties(const uint64_t* keys, const uint32_t* pays, int F, int lane,
-                               int r_lim, int e_lim, int start_c) {
+                               int r_lim, int e_lim, int start_c, const int* sv) {
     bool any = false;
     for (int c0 = 1; c0 < F; c0 += 64) {
         const int e = c0 + lane;
         any |= __ballot(e < F && keys[e] == keys[e - 1]) != 0;
     }
     if (!any) return false;
-    int grp = 0, last_upd = -1;   // carried across chunks
+    int grp = 0;                          // start of the current tie group (carried)
+    int last[3] = {-1, -1, -1};           // last updater of each row so far (carried)
     bool amb = false;
     for (int c0 = 0; c0 < F; c0 += 64) {
         const int e = c0 + lane;
         const bool real = e < F;
+        const uint32_t p = real ? pays[e] : 0u;
         const bool gs = real && (e == 0 || keys[e] != keys[e - 1]);
-        const bool upd = real && update_mask(pays[e], r_lim, e_lim, start_c) != 0;
-        int g = scan_max(gs ? e : -1, lane);
-        g = max(g, grp);
-        const int u_inc = max(scan_max(upd ? e : -1, lane), last_upd);
-        int u_exc = __shfl_up(u_inc, 1);
-        if (lane == 0) u_exc = last_upd;
-        amb |= upd && u_exc >= g;
+        const int mask = real ? update_mask(p, r_lim, e_lim, start_c) : 0;
+        const int g = max(scan_max(gs ? e : -1, lane), grp);
+#pragma unroll
+        for (int row = 0; row < 3; ++row) {
+            const bool upd = (mask >> row) & 1;
+            const int u_inc = max(scan_max(upd ? e : -1, lane), last[row]);
+            int u_exc = __shfl_up(u_inc, 1);
+            if (lane == 0) u_exc = last[row];
+            if (upd && u_exc >= g &&
+                row_value(pays[u_exc], row, start_c, sv) != row_value(p, row, start_c, sv))
+                amb = true;
+            last[row] = __shfl(u_inc, 63);
+        }
         grp = __shfl(g, 63);
-        last_upd = __shfl(u_inc, 63);
     }
     return __ballot(amb) != 0;
 }
@@ -310,7 +324,8 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     else sort_lds(keys, pays, F, lane);
 
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe, start_c = G.K - 1;
-    if (ambiguous_ties(keys, pays, F, lane, r_lim, e_lim, start_c)) {
+    const int start_vals[3] = {sr, se, sa};
+    if (ambiguous_ties(keys, pays, F, lane, r_lim, e_lim, start_c, start_vals)) {
         if (lane == 0) {
             const unsigned long long q = atomicAdd(o.n_deferred, 1ull);
             o.deferred[q] = ray;

@@ -27,7 +27,6 @@ PDEVICE = 'cpu'
 FTYPE = tr.float64
 ITYPE = tr.int64
 
-SEG_PER_BLOCK = 2048   # forward/adjoint partition granularity (segments per workgroup)
 
 
 def isclose(a, b, factor=3):
@@ -331,12 +330,21 @@ class Operator:
                                         _lib.ptr(vox), _lib.ptr(seg_len), _lib.ptr(tws),
                                         tws.numel(), stream), 'sphrt_trace_fill')
         del tws
-        nblocks = total // SEG_PER_BLOCK + 1
-        block_lo = tr.empty(nblocks + 1, dtype=tr.int64, device=dev)
-        _lib.check(lib.sphrt_partition(_lib.ptr(row_ptr), n, SEG_PER_BLOCK, _lib.ptr(block_lo),
-                                       nblocks, stream), 'sphrt_partition')
-        self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, block_lo=block_lo,
-                         nblocks=nblocks, n=n, total=total)
+        # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
+        nblocks = lib.sphrt_csr_blocks(total)
+        row_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
+        blocks = tr.empty(5 * nblocks, dtype=tr.int64, device=dev)
+        iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n), dtype=tr.uint8, device=dev)
+        _lib.check(lib.sphrt_csr_index(_lib.ptr(row_ptr), n, _lib.ptr(vox), _lib.ptr(row_ray),
+                                       _lib.ptr(blocks), nblocks, _lib.ptr(iws), stream),
+                   'sphrt_csr_index')
+        del iws
+        c = _lib.CSR()
+        c.n_rays, c.n_segments, c.n_blocks = n, total, nblocks
+        c.row_ptr, c.vox, c.len = row_ptr.data_ptr(), vox.data_ptr(), seg_len.data_ptr()
+        c.row_ray, c.blocks, c.len32 = row_ray.data_ptr(), blocks.data_ptr(), None
+        self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, row_ray=row_ray, blocks=blocks,
+                         nblocks=nblocks, n=n, total=total, desc=c)
         self._batch = batch
 
     # -- shape logic of raytracer.py:703-712 -----------------------------------------------------
@@ -366,6 +374,7 @@ class Operator:
                                                      csr['len'].numel(), _lib.stream_of(self._cdev)),
                        'sphrt_f64_to_f32')
             csr['len32'] = l32
+            csr['desc'].len32 = l32.data_ptr()
         return csr['len32']
 
     def _launch_forward(self, d, out, n_chan, div):
@@ -373,12 +382,10 @@ class Operator:
         float32/float64) -> out (preallocated, same dtype).  No allocation, no host sync."""
         csr = self._csr
         lib = _lib.load()
+        self._lengths(d.dtype)
         fn = lib.sphrt_forward_f32 if d.dtype == tr.float32 else lib.sphrt_forward_f64
-        _lib.check(fn(_lib.ptr(csr['row_ptr']), _lib.ptr(csr['vox']),
-                      _lib.ptr(self._lengths(d.dtype)), csr['n'], _lib.ptr(csr['block_lo']),
-                      csr['nblocks'], SEG_PER_BLOCK, _lib.ptr(d), n_chan,
-                      math.prod(self.grid.shape[-3:]), div, _lib.ptr(out), csr['n'],
-                      _lib.stream_of(self._cdev)), 'sphrt_forward')
+        _lib.check(fn(csr['desc'], _lib.ptr(d), n_chan, math.prod(self.grid.shape[-3:]), div,
+                      _lib.ptr(out), csr['n'], _lib.stream_of(self._cdev)), 'sphrt_forward')
 
     def _apply_forward(self, density):
         dev = self._cdev
@@ -408,10 +415,8 @@ class Operator:
             raise ValueError(f'adjoint input has {yv.numel()} values, expected {n_chan * n}')
         acc = tr.zeros(math.prod(dshape), dtype=tr.float64, device=dev)
         _lib.check(_lib.load().sphrt_adjoint_accumulate(
-            _lib.ptr(csr['row_ptr']), _lib.ptr(csr['vox']), _lib.ptr(csr['len']), n,
-            _lib.ptr(csr['block_lo']), csr['nblocks'], SEG_PER_BLOCK, _lib.ptr(yv),
-            int(ydt == tr.float64), n_chan, n, div, _lib.ptr(acc), vol, _lib.stream_of(dev)),
-            'sphrt_adjoint_accumulate')
+            csr['desc'], _lib.ptr(yv), int(ydt == tr.float64), n_chan, n, div, _lib.ptr(acc), vol,
+            _lib.stream_of(dev)), 'sphrt_adjoint_accumulate')
         if ddtype == tr.float64:
             res = acc
         elif ddtype == tr.float32:
@@ -441,7 +446,7 @@ class Operator:
         pos = tr.arange(total, device=row_ptr.device) - row_ptr[:-1][ray]
         vox = tr.zeros((n, smax), dtype=tr.int64, device=row_ptr.device)
         lens = tr.zeros((n, smax), dtype=tr.float64, device=row_ptr.device)
-        vox[ray, pos] = csr['vox'][:total].to(tr.int64)
+        vox[ray, pos] = csr['vox'][:total].to(tr.int64) & 0x7FFFFFFF
         lens[ray, pos] = csr['len'][:total]
         _, ne, na = self.grid.shape[-3:]
         regs = tr.stack((vox // (ne * na), (vox // na) % ne, vox % na))
@@ -459,9 +464,10 @@ class Operator:
         return self._padded()[1].to(device=self.device)
 
     def segments(self):
-        """The trace itself: (row_ptr int64 (n+1,), vox int32, len float64) on the GPU."""
+        """The trace itself: (row_ptr int64 (n+1,), linear voxel int32, len float64) on the GPU;
+        segment s of ray i is row_ptr[i] <= s < row_ptr[i+1], voxel (r*ne + e)*na + a."""
         c = self._csr
-        return c['row_ptr'], c['vox'][:c['total']], c['len'][:c['total']]
+        return c['row_ptr'], c['vox'][:c['total']] & 0x7FFFFFFF, c['len'][:c['total']]
 
     def _debug_print(self, debug_los):
         R = tuple(self._ray_shape)

@@ -106,3 +106,40 @@ def test_solvers_bitlevel(gpu):
         # regions are only meaningful for finite distances (inf entries never update a row)
         assert np.array_equal(reg[fin], z[f'{key}_reg'][fin]), f'{key}: regions differ'
         assert np.array_equal(neg[fin], z[f'{key}_neg'][fin]), f'{key}: negative_crossing differs'
+
+
+def test_solvers_match_ieee_oracle(gpu):
+    """GPU crossing solves vs the oracle with IEEE sqrt: same arithmetic, same rounding, so every
+    distance, region and negative_crossing must be identical (all entries, inf/NaN included)."""
+    import os, sys
+    sys.path.insert(0, os.path.dirname(gc.GOLDEN) + '/..')
+    from oracle import oracle
+    from sph_raytracer_amd.raytracer import a_torch, e_torch, r_torch
+    z = gc.load('solvers')
+    xs, rays = tr.from_numpy(z['xs']), tr.from_numpy(z['rays'])
+    oracle.use_mkl_sqrt(False)
+    g = oracle.Grid.from_boundaries(z['r_b'], z['e_b'], z['a_b'])
+    for fam, (key, fn) in enumerate((('r', r_torch), ('e', e_torch), ('a', a_torch))):
+        t, reg, _, neg = fn(tr.from_numpy(z[f'{key}_b']), xs, rays)
+        ot, oreg, oneg = oracle.solve(g, fam, z['xs'], z['rays'])
+        t = t.numpy()
+        same = (t == ot) | (np.isnan(t) & np.isnan(ot))
+        assert same.all(), f'{key}: {int((~same).sum())} distances differ from the IEEE oracle, ' \
+                           f'first {t[~same][:3]} vs {ot[~same][:3]}'
+        assert np.array_equal(reg.numpy(), oreg), f'{key}: regions differ'
+        assert np.array_equal(neg.numpy(), oneg), f'{key}: negative_crossing differs'
+
+
+def test_gpu_sqrt_div_correctly_rounded(gpu):
+    """FP64 sqrt and division on gfx950 as compiled here must be IEEE correctly rounded (the
+    solver's bit-exactness against the IEEE oracle rests on it)."""
+    from sph_raytracer_amd.raytracer import r_torch
+    rng = np.random.default_rng(5)
+    # r_torch with start on the z axis and direction +x: tc = 0, d = |x| ... t = +-sqrt(R^2 - d^2)
+    R = np.sort(rng.uniform(1.0, 3.0, 2000))
+    x = np.zeros((2000, 3))
+    x[:, 2] = rng.uniform(0.0, 0.999, 2000)
+    t, _, _, _ = r_torch(tr.from_numpy(R), tr.from_numpy(x[:1]), tr.tensor([[1.0, 0.0, 0.0]]))
+    d = x[0, 2]
+    ref = np.sqrt(R * R - d * d)
+    assert np.array_equal(t.numpy()[0, len(R):], ref)

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch as tr
 
-from known_answers import A_CASES, E_CASES, R_CASES
+from known_answers import A_CASES, E_CASES, R_CASES, e_boundaries
 
 pytestmark = pytest.mark.gpu
 
@@ -31,8 +31,9 @@ def test_r(gpu):
 
 def test_e(gpu):
     from sph_raytracer_amd.raytracer import e_torch
-    for bounds, xs, rays, t_exp, reg_exp in E_CASES:
-        t, reg = e_torch(tr.tensor(bounds), xs, rays)[:2]
+    for spec, xs, rays, t_exp, reg_exp in E_CASES:
+        bounds = e_boundaries(spec)
+        t, reg = e_torch(tr.from_numpy(bounds), xs, rays)[:2]
         assert check(t, t_exp), (bounds, xs, rays, t)
         if reg_exp is not None:
             assert check(reg, reg_exp)

@@ -150,8 +150,9 @@ def test_known_answers_r():
 
 
 def test_known_answers_e():
-    from known_answers import E_CASES
-    for bounds, xs, rays, t_exp, reg_exp in E_CASES:
+    from known_answers import E_CASES, e_boundaries
+    for spec, xs, rays, t_exp, reg_exp in E_CASES:
+        bounds = e_boundaries(spec)
         t, reg = _fam(1, bounds, xs, rays)
         assert check(t, t_exp), (bounds, xs, rays, t)
         if reg_exp is not None:
