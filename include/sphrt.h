@@ -153,6 +153,15 @@ int sphrt_forward_f64(const sphrt_csr *csr, const double *density, int64_t n_cha
 int sphrt_adjoint_accumulate(const sphrt_csr *csr, const void *y, int y_is_f64, int64_t n_chan,
                              int64_t y_chan_stride, int64_t ray_chan_div, double *acc,
                              int64_t chan_stride, void *stream);
+
+/* Deterministic adjoint: the voxel-major transpose of the trace (built once).  col_ptr
+ * (n_vox+1), t_ray / t_len (n_segments): for voxel v, the segments col_ptr[v] .. col_ptr[v+1]
+ * in ray order (stable radix sort).  Index it with sphrt_csr_index(col_ptr, n_vox, t_ray, ...)
+ * and the adjoint is sphrt_forward_f32/f64 on that CSR with y as the "density": no atomics,
+ * bitwise reproducible. */
+size_t sphrt_transpose_workspace_bytes(int64_t n_segments, int64_t n_vox);
+int sphrt_csr_transpose(const sphrt_csr *csr, int64_t n_vox, int64_t *col_ptr, int32_t *t_ray,
+                        double *t_len, void *workspace, size_t workspace_size, void *stream);
 /* dst[i] = (float)src[i] — rounding the float64 accumulator to a float32 result. */
 int sphrt_f64_to_f32(const double *src, float *dst, int64_t n, void *stream);
 

@@ -65,6 +65,9 @@ _SIGNATURES = [
                                   c_vp]),
     ('sphrt_adjoint_accumulate', c_int, [ctypes.POINTER(CSR), c_vp, c_int, c_i64, c_i64, c_i64,
                                          c_vp, c_i64, c_vp]),
+    ('sphrt_transpose_workspace_bytes', ctypes.c_size_t, [c_i64, c_i64]),
+    ('sphrt_csr_transpose', c_int, [ctypes.POINTER(CSR), c_i64, c_vp, c_vp, c_vp, c_vp,
+                                    ctypes.c_size_t, c_vp]),
     ('sphrt_f64_to_f32', c_int, [c_vp, c_vp, c_i64, c_vp]),
     ('sphrt_trace_integrate_f32', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_i64, c_i64,
                                           c_i64, c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),

@@ -300,6 +300,9 @@ class Operator:
         if invalid:
             raise NotImplementedError('invalid=True (keep invalid segments) is not supported')
         self._csr = None
+        # 'transpose': deterministic voxel-major adjoint (default); 'atomic': float64 atomics
+        # (used anyway when views are paired with time slices)
+        self.adjoint_mode = 'transpose'
         if _compute:
             self._trace()
             if debug:
@@ -403,6 +406,43 @@ class Operator:
             out = out.to(device=density.device, dtype=in_dtype)
         return out
 
+    def _transposed(self):
+        """Voxel-major copy of the trace (built on the first adjoint): the adjoint then runs the
+        forward's segmented gather-reduce with rays and voxels swapped — no atomics,
+        bitwise reproducible."""
+        csr = self._csr
+        if 'T' in csr:
+            return csr['T']
+        lib, dev = _lib.load(), self._cdev
+        stream = _lib.stream_of(dev)
+        n_vox = math.prod(self.grid.shape[-3:])
+        total = csr['total']
+        col_ptr = tr.empty(n_vox + 1, dtype=tr.int64, device=dev)
+        t_ray = tr.empty(max(total, 1), dtype=tr.int32, device=dev)
+        t_len = tr.empty(max(total, 1), dtype=tr.float64, device=dev)
+        ws = tr.empty(lib.sphrt_transpose_workspace_bytes(total, n_vox), dtype=tr.uint8, device=dev)
+        _lib.check(lib.sphrt_csr_transpose(csr['desc'], n_vox, _lib.ptr(col_ptr), _lib.ptr(t_ray),
+                                           _lib.ptr(t_len), _lib.ptr(ws), ws.numel(), stream),
+                   'sphrt_csr_transpose')
+        del ws
+        nblocks = lib.sphrt_csr_blocks(total)
+        vox_list = tr.empty(n_vox, dtype=tr.int32, device=dev)
+        blocks = tr.empty(5 * nblocks, dtype=tr.int64, device=dev)
+        iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n_vox), dtype=tr.uint8, device=dev)
+        _lib.check(lib.sphrt_csr_index(_lib.ptr(col_ptr), n_vox, _lib.ptr(t_ray),
+                                       _lib.ptr(vox_list), _lib.ptr(blocks), nblocks,
+                                       _lib.ptr(iws), stream), 'sphrt_csr_index(T)')
+        t_len32 = tr.empty(t_len.shape, dtype=tr.float32, device=dev)
+        _lib.check(lib.sphrt_f64_to_f32(_lib.ptr(t_len), _lib.ptr(t_len32), t_len.numel(), stream),
+                   'sphrt_f64_to_f32')
+        c = _lib.CSR()
+        c.n_rays, c.n_segments, c.n_blocks = n_vox, total, nblocks
+        c.row_ptr, c.vox, c.len, c.len32 = (col_ptr.data_ptr(), t_ray.data_ptr(),
+                                            t_len.data_ptr(), t_len32.data_ptr())
+        c.row_ray, c.blocks = vox_list.data_ptr(), blocks.data_ptr()
+        csr['T'] = dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, blocks))
+        return csr['T']
+
     def _apply_adjoint(self, y, dshape, ddtype, ddevice):
         dev = self._cdev
         n_chan, div, out_shape = self._layout(dshape)
@@ -413,6 +453,15 @@ class Operator:
         yv = y.detach().to(device=dev, dtype=ydt).reshape(-1).contiguous()
         if yv.numel() != n_chan * n:
             raise ValueError(f'adjoint input has {yv.numel()} values, expected {n_chan * n}')
+        if div == 0 and self.adjoint_mode == 'transpose':
+            cdt = ddtype if ddtype in (tr.float32, tr.float64) else tr.float32
+            yv = yv.to(cdt)
+            res = tr.empty(n_chan * vol, dtype=cdt, device=dev)
+            lib = _lib.load()
+            fn = lib.sphrt_forward_f32 if cdt == tr.float32 else lib.sphrt_forward_f64
+            _lib.check(fn(self._transposed()['desc'], _lib.ptr(yv), n_chan, n, 0, _lib.ptr(res),
+                          vol, _lib.stream_of(dev)), 'adjoint (transposed forward)')
+            return res.reshape(dshape).to(device=ddevice, dtype=ddtype)
         acc = tr.zeros(math.prod(dshape), dtype=tr.float64, device=dev)
         _lib.check(_lib.load().sphrt_adjoint_accumulate(
             csr['desc'], _lib.ptr(yv), int(ydt == tr.float64), n_chan, n, div, _lib.ptr(acc), vol,

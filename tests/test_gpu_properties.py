@@ -1,0 +1,166 @@
+"""Size-independent properties of the HIP path at the BASELINE sizes (C1, C2 full; C5 geometry),
+plus oracle spot checks on rays sampled from the full-size traces.
+
+Tolerances: float64 identities within 1e-12 relative (1e-11 for sums over 10^5+ terms);
+segment voxels exact, lengths 1e-12 relative (golden_cases.compare_segments)."""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch as tr
+
+import golden_cases as gc
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+pytestmark = pytest.mark.gpu
+
+
+def _orbit(n_views, det, kind='rect', grid_shape=(50, 50, 50)):
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom, SphericalGrid
+    grid = SphericalGrid(shape=grid_shape)
+    geoms = []
+    for th in tr.linspace(0, 2 * tr.pi, n_views):
+        pos = (5 * tr.cos(th), 5 * tr.sin(th), 1)
+        geoms.append(ConeRectGeom(det, pos=pos, fov=(45, 45)) if kind == 'rect'
+                     else ConeCircGeom(shape=det, pos=pos, fov=(0, 45)))
+    return grid, sum(geoms)
+
+
+@pytest.fixture(scope='module')
+def c2(gpu):
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(50, (50, 100))
+    return grid, geom, Operator(grid, geom, device=gpu)
+
+
+def test_adjoint_identity_and_determinism(c2, gpu):
+    grid, geom, op = c2
+    g = tr.Generator(device=gpu).manual_seed(0)
+    x = tr.rand(grid.shape, dtype=tr.float64, device=gpu, generator=g)
+    y = tr.rand(geom.shape, dtype=tr.float64, device=gpu, generator=g)
+    ax = op(x)
+    aty = op.T(y)
+    lhs, rhs = float((ax * y).sum()), float((x * aty).sum())
+    assert abs(lhs - rhs) <= 1e-12 * abs(lhs), (lhs, rhs)
+    assert tr.equal(op(x), ax), 'forward not bitwise reproducible'
+    assert tr.equal(op.T(y), aty), 'adjoint not bitwise reproducible'
+    # deterministic transposed adjoint == float64-atomic adjoint (up to summation order)
+    op.adjoint_mode = 'atomic'
+    at2 = op.T(y)
+    op.adjoint_mode = 'transpose'
+    assert tr.allclose(at2, aty, rtol=1e-12, atol=1e-12 * float(aty.abs().max()))
+    # float32 forward/adjoint against float64
+    ax32 = op(x.float())
+    assert float(((ax32.double() - ax).abs() / ax.abs().clamp_min(1e-12)).max()) <= 1e-5
+    aty32 = op.T(y.float())
+    assert aty32.dtype == tr.float32
+    assert float((aty32.double() - aty).abs().max()) <= 1e-5 * float(aty.abs().max())
+
+
+def test_linearity_and_channels(c2, gpu):
+    grid, geom, op = c2
+    g = tr.Generator(device=gpu).manual_seed(1)
+    x1 = tr.rand(grid.shape, dtype=tr.float64, device=gpu, generator=g)
+    x2 = tr.rand(grid.shape, dtype=tr.float64, device=gpu, generator=g) - 0.5
+    lhs = op(2.5 * x1 - 3.0 * x2)
+    rhs = 2.5 * op(x1) - 3.0 * op(x2)
+    assert float((lhs - rhs).abs().max()) <= 1e-12 * float(rhs.abs().max())
+    # multichannel static input == per-channel calls (preview3d-style batching)
+    xc = tr.stack([x1, x2, x1 * x2])
+    out = op(xc)
+    assert out.shape == (3,) + tuple(geom.shape)
+    for i in range(3):
+        assert tr.equal(out[i], op(xc[i]))
+    yc = tr.rand((3,) + tuple(geom.shape), dtype=tr.float64, device=gpu, generator=g)
+    grad = tr.autograd.grad((op(xc.requires_grad_()) * yc).sum(), xc)[0]
+    for i in range(3):
+        assert tr.allclose(grad[i], op.T(yc[i]), rtol=1e-12, atol=1e-14)
+
+
+def test_chord_lengths(c2, gpu):
+    """With every voxel = 1, a ray's line integral is its chord through the outer sphere."""
+    grid, geom, op = c2
+    out = op(tr.ones(grid.shape, dtype=tr.float64, device=gpu)).cpu().numpy().reshape(-1)
+    xs = np.broadcast_to(geom.ray_starts.numpy(), geom.rays.shape).reshape(-1, 3)
+    d = geom.rays.numpy().reshape(-1, 3)
+    tc = -(xs * d).sum(1)
+    dd2 = (xs * xs).sum(1) - tc * tc
+    chord = 2 * np.sqrt(np.clip(1.0 - dd2, 0, None))
+    assert np.allclose(out, chord, rtol=1e-9, atol=1e-9)
+    assert (out > 0).mean() > 0.15
+
+
+def test_fused_equals_csr(c2, gpu):
+    from sph_raytracer_amd.raytracer import line_integrals
+    grid, geom, op = c2
+    x = tr.rand(grid.shape, dtype=tr.float64, device=gpu)
+    a = op(x)
+    b = line_integrals(grid, geom, x)
+    assert float((a - b).abs().max()) <= 1e-12 * float(a.abs().max())
+
+
+def test_full_size_trace_vs_oracle_sample(c2, gpu):
+    """2000 rays sampled from the full C2 trace, each checked against the C oracle."""
+    from oracle import oracle
+    from sph_raytracer_amd.raytracer import find_starts
+    grid, geom, op = c2
+    rng = np.random.default_rng(0)
+    n = math.prod(geom.shape)
+    pick = np.sort(rng.choice(n, 2000, replace=False))
+    xs = np.broadcast_to(geom.ray_starts.numpy(), geom.rays.shape).reshape(-1, 3)[pick]
+    rays = geom.rays.numpy().reshape(-1, 3)[pick]
+    starts = find_starts(grid, tr.from_numpy(xs)).numpy()
+    oracle.use_mkl_sqrt(False)
+    g = oracle.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy())
+    ref = oracle.trace_segments(g, xs, rays, starts)
+    rp, vx, ln = (t.cpu().numpy() for t in op.segments())
+    cnt = rp[pick + 1] - rp[pick]
+    ptr = np.concatenate([[0], np.cumsum(cnt)])
+    idx = np.concatenate([np.arange(rp[i], rp[i + 1]) for i in pick]).astype(np.int64)
+    msg = gc.compare_segments(ref, (ptr, vx[idx], ln[idx]), 5.1, 'C2 sample')
+    assert msg is None, msg
+
+
+def test_c5_geometry_vs_oracle_sample(gpu):
+    """C5 geometry (64^3, 64 ConeCirc views incl. rays through the origin) sampled vs oracle."""
+    from oracle import oracle
+    from sph_raytracer_amd import Operator
+    from sph_raytracer_amd.raytracer import find_starts
+    grid, geom = _orbit(64, (100, 50), kind='circ', grid_shape=(64, 64, 64))
+    op = Operator(grid, geom, device=gpu)
+    rng = np.random.default_rng(1)
+    n = math.prod(geom.shape)
+    pick = np.sort(rng.choice(n, 3000, replace=False))
+    xs = np.broadcast_to(geom.ray_starts.numpy(), geom.rays.shape).reshape(-1, 3)[pick]
+    rays = geom.rays.numpy().reshape(-1, 3)[pick]
+    starts = find_starts(grid, tr.from_numpy(xs)).numpy()
+    g = oracle.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy())
+    ref = oracle.trace_segments(g, xs, rays, starts)
+    rp, vx, ln = (t.cpu().numpy() for t in op.segments())
+    cnt = rp[pick + 1] - rp[pick]
+    ptr = np.concatenate([[0], np.cumsum(cnt)])
+    idx = np.concatenate([np.arange(rp[i], rp[i + 1]) for i in pick]).astype(np.int64)
+    msg = gc.compare_segments(ref, (ptr, vx[idx], ln[idx]), 5.1, 'C5 sample')
+    assert msg is None, msg
+
+
+def test_gd_retrieval_decreases_loss(gpu):
+    """static_retrieval.py's loop (FullyDenseModel, SquareLoss + NegRegularizer, Adam) on a small
+    grid: runs unchanged on the HIP operator and the fidelity loss drops."""
+    from sph_raytracer_amd import Operator
+    from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
+    from sph_raytracer_amd.model import FullyDenseModel
+    from sph_raytracer_amd.retrieval import gd
+    grid, geom = _orbit(12, (20, 16), kind='circ', grid_shape=(16, 16, 16))
+    x = tr.zeros(grid.shape, device=gpu)
+    x[:, 8:, :8] = 1
+    x[:, :8, 8:] = 1
+    op = Operator(grid, geom, device=x.device)
+    meas = op(x)
+    coeffs, y, losses = gd(op, meas, FullyDenseModel(grid), lr=1e-1, num_iterations=30,
+                           loss_fns=[1 * SquareLoss(), 1 * NegRegularizer()], progress_bar=False)
+    fid = list(losses.values())[0]
+    assert fid[-1] < 0.2 * fid[0]
+    assert y.shape == meas.shape

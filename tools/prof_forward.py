@@ -70,10 +70,22 @@ def main():
                                                  _lib.ptr(acc), acc.numel(),
                                                  _lib.stream_of(dev)), 'adjoint')
 
+    T = op._transposed()['desc']
+    nvox = acc.numel()
+    a64 = torch.empty(nvox, dtype=torch.float64, device=dev)
+    a32 = torch.empty(nvox, dtype=torch.float32, device=dev)
+    y32 = y.float()
+
+    def adjoint_t(yy, out):
+        fn = lib.sphrt_forward_f32 if yy.dtype == torch.float32 else lib.sphrt_forward_f64
+        _lib.check(fn(T, _lib.ptr(yy), 1, n, 0, _lib.ptr(out), nvox, _lib.stream_of(dev)), 'adjT')
+
     variants = {
         'forward_f32': (lambda: op._launch_forward(x32, o32, 1, 0), n * 8 + total * 12),
         'forward_f64': (lambda: op._launch_forward(x64, o64, 1, 0), n * 12 + total * 20),
-        'adjoint_f64': (adjoint, n * 12 + total * (4 + 8 + 16)),
+        'adjoint_T_f32': (lambda: adjoint_t(y32, a32), nvox * 8 + total * 12),
+        'adjoint_T_f64': (lambda: adjoint_t(y, a64), nvox * 12 + total * 20),
+        'adjoint_atomic_f64': (adjoint, n * 12 + total * (4 + 8 + 16)),
     }
     res = {k: [] for k in variants}
     for _ in range(args.rounds):
