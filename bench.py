@@ -173,8 +173,14 @@ def main():
     torch.cuda.reset_peak_memory_stats(dev)
     barrier()
     t0 = time.perf_counter()
-    grid, geom = build_geometry(cfg, rank, world)
-    op = Operator(grid, geom, device=dev)
+    if dist is None:
+        grid, geom = build_geometry(cfg, 0, 1)
+        sop = op = Operator(grid, geom, device=dev)
+    else:   # every rank sees the whole 50*N-view orbit and keeps its contiguous 50-view shard
+        from sph_raytracer_amd.distributed import ShardedOperator
+        grid, geom = build_geometry((shape, n_views * world) + cfg[2:], 0, 1)
+        sop = ShardedOperator(grid, geom, device=dev)
+        op = sop.local
     x = torch.rand(shape, dtype=dtype, device=dev)
     y = op(x)
     torch.cuda.synchronize(dev)
@@ -182,15 +188,9 @@ def main():
     n_rays = op._csr['n']
     total_seg = op._csr['total']
 
-    stack = None
-    if dist is not None:
-        stack = torch.empty((world,) + tuple(y.shape), dtype=y.dtype, device=dev)
-
     def step():
-        out = op(x)
-        if dist is not None:
-            dist.all_gather_into_tensor(stack, out)
-        return out
+        # one forward Operator call; with N ranks: local forward + RCCL all-gather of the stack
+        return op(x) if dist is None else sop.forward_full(x)
 
     for _ in range(args.warmup):
         step()
@@ -225,7 +225,24 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_warm_cold = tt.item()
 
+    # drop-in use with host tensors (the reference's device='cpu' default): H2D density, D2H image
+    x_host = x.cpu()
+    for _ in range(3):
+        op(x_host)
+    t0 = time.perf_counter()
+    reps_h = 50
+    for _ in range(reps_h):
+        op(x_host)
+    t_host = (time.perf_counter() - t0) / reps_h
+
     k_ms, k_method = kernel_time_ms(op, x)
+    kname = 'forward_kernel<float,float>' if dtype == torch.float32 else 'forward_kernel<double,double>'
+    traffic, traffic_src = None, None
+    pmc = os.path.join(ROOT, 'profiles', 'r01_forward_c2_pmc.json')
+    if os.path.exists(pmc):     # HBM bytes per launch from the committed rocprofv3 --pmc passes
+        rec_pmc = json.load(open(pmc))
+        if rec_pmc.get('kernel') == kname and rec_pmc.get('config') == args.config:
+            traffic, traffic_src = rec_pmc['traffic_bytes_per_launch'], os.path.relpath(pmc, ROOT)
     # bytes/ray = s_y + 4 + S*(4 + s_len + s_rho); f32 path s_len = s_rho = 4
     es = x.element_size()
     alg_bytes = n_rays * (es + 4) + total_seg * (4 + es + es)
@@ -248,14 +265,15 @@ def main():
                    'detector': list(det), 'rays_per_gpu': n_rays, 'segments_per_gpu': total_seg,
                    'parallelism': f'obs-sharded x{world}' + (' + RCCL all-gather' if world > 1 else '')},
         'peak_gb_resident': peak_gb,
+        'pcie_inclusive': {'rays_per_s': n_rays / t_host, 'ms_per_call': t_host * 1e3,
+                           'what': 'op(x) with x and the result in host memory (per rank)'},
         'cold': {'rays_per_s': n_rays * world / t_warm_cold, 'seconds': t_warm_cold,
                  'first_in_process_seconds': t_cold,
                  'what': 'geometry + Operator trace + first forward (median of 3, warm process; '
                          'first_in_process includes HIP/torch initialisation)'},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                     'kernel': 'forward_kernel<float,float>' if dtype == torch.float32
-                               else 'forward_kernel<double,double>',
+                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                     'traffic_source': traffic_src, 'kernel': kname,
                      'kernel_ms': k_ms, 'bytes_per_launch': alg_bytes, 'timing': k_method},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
