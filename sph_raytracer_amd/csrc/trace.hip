@@ -8,7 +8,7 @@
 //      non-negative crossings to a per-wave LDS list (ballot + mbcnt compaction); the most
 //      negative finite distance is reduced across the wave (it bounds the behind-start segment);
 //   2. the list is sorted by (distance, candidate index) — a total order equal to a stable sort
-//      of the reference's concatenation — in registers (<= 512 entries) or in LDS;
+//      of the reference's concatenation — in registers (<= 256 entries) or in LDS;
 //   3. 64-entry chunks are scanned (forward fill of the r/e/a rows), differenced and the
 //      non-zero in-grid segments compacted, in order, back into LDS;
 //   4. depending on MODE the segments are counted, copied to the CSR, or integrated against
@@ -171,6 +171,8 @@ struct TraceOut {
     int64_t out_chan_stride;
     unsigned long long* n_deferred;  // workspace: deferred-ray counter
     int64_t* deferred;               // workspace: deferred ray ids
+    unsigned* n_hits;                // workspace: screened hit-ray counter
+    int32_t* hits;                   // workspace: hit ray ids
 };
 
 // region rows a candidate updates: bit0 r, bit1 e, bit2 a (start entry: all)
@@ -320,7 +322,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     if (F <= 64) sort_regs<1>(keys, pays, F, lane);
     else if (F <= 128) sort_regs<2>(keys, pays, F, lane);
     else if (F <= 256) sort_regs<4>(keys, pays, F, lane);
-    else if (F <= 512) sort_regs<8>(keys, pays, F, lane);
     else sort_lds(keys, pays, F, lane);
 
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe, start_c = G.K - 1;
@@ -424,8 +425,41 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     wave_sync();
 }
 
+// Screen one ray per lane: a ray yields a segment only if it reaches the outer sphere or starts
+// in a voxel — otherwise every r-row value stays the (invalid) start region (t1c is NaN for every
+// shell when it is NaN for the outermost: monotone in R; tangents excluded).  Misses get their
+// zero outputs here; hits are appended (wave-aggregated) to the hit list the trace kernel drains.
 template <int MODE, typename T>
-__global__ __launch_bounds__(256) void trace_kernel(GridDev G, RaysDev R, TraceOut<T> o,
+__global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
+    const int lane = threadIdx.x & 63;
+    const int64_t ray = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool active = ray < R.n;
+    double x[3] = {0, 0, 0}, d[3] = {0, 0, 1};
+    int s[3] = {-1, -1, -1};
+    if (active) load_ray(R, ray, x, d, s);
+    const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
+    const double t1c_outer = __builtin_sqrt(G.r_outer * G.r_outer - g.dd * g.dd);
+    const bool start_r_ok = s[0] >= 0 && s[0] < G.nr;
+    const bool hit = active && !(!start_r_ok && __builtin_isnan(t1c_outer));
+    if (active && !hit) {
+        if (MODE == MODE_COUNT) o.counts[ray] = 0;
+        if (MODE == MODE_INTEGRATE) {
+            const int64_t nc = o.ray_chan_div > 0 ? 1 : o.n_chan;
+            for (int64_t c = 0; c < nc; ++c) o.out[c * o.out_chan_stride + ray] = (T)0;
+        }
+    }
+    const uint64_t m = __ballot(hit);
+    if (m == 0) return;
+    unsigned base = 0;
+    if (lane == __builtin_ctzll(m)) base = atomicAdd(o.n_hits, (unsigned)__popcll(m));
+    base = __shfl(base, __builtin_ctzll(m));
+    if (hit) o.hits[base + __popcll(m & lanemask_lt(lane))] = (int32_t)ray;
+}
+
+// Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
+// image looks like.  Every lane evaluates the (wave-uniform) ray set-up itself.
+template <int MODE, typename T>
+__global__ __launch_bounds__(256, 4) void trace_kernel(GridDev G, RaysDev R, TraceOut<T> o,
                                                     int cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
@@ -434,42 +468,15 @@ __global__ __launch_bounds__(256) void trace_kernel(GridDev G, RaysDev R, TraceO
     uint32_t* pays =
         reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(smem) + (size_t)kWavesPerBlock * cap) +
         (size_t)wid * cap;
-    const int64_t ntiles = (R.n + 63) / 64;
-    for (int64_t tile = (int64_t)blockIdx.x * kWavesPerBlock + wid; tile < ntiles;
-         tile += (int64_t)gridDim.x * kWavesPerBlock) {
-        const int64_t ray = tile * 64 + lane;
-        const bool active = ray < R.n;
-        double x[3] = {0, 0, 0}, d[3] = {0, 0, 1};
-        int s[3] = {-1, -1, -1};
-        if (active) load_ray(R, ray, x, d, s);
+    const int64_t n_hits = (int64_t)*o.n_hits;
+    for (int64_t h = (int64_t)blockIdx.x * kWavesPerBlock + wid; h < n_hits;
+         h += (int64_t)gridDim.x * kWavesPerBlock) {
+        const int64_t ray = o.hits[h];
+        double x[3], d[3];
+        int s[3];
+        load_ray(R, ray, x, d, s);
         const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
-        // A ray produces a non-zero segment only if it reaches the outer sphere or starts in a
-        // voxel: otherwise every r-row value stays the (invalid) start region.  t1c is NaN for
-        // every shell when it is NaN for the outermost (monotone in R), tangents excluded.
-        const double t1c_outer = __builtin_sqrt(G.r_outer * G.r_outer - g.dd * g.dd);
-        const bool start_r_ok = s[0] >= 0 && s[0] < G.nr;
-        const bool hit = active && !(!start_r_ok && __builtin_isnan(t1c_outer));
-        if (active && !hit) {
-            if (MODE == MODE_COUNT) o.counts[ray] = 0;
-            if (MODE == MODE_INTEGRATE) {
-                int64_t c_lo = 0, c_hi = o.n_chan;
-                if (o.ray_chan_div > 0) { c_lo = 0; c_hi = 1; }
-                for (int64_t c = c_lo; c < c_hi; ++c) o.out[c * o.out_chan_stride + ray] = (T)0;
-            }
-        }
-        uint64_t todo = __ballot(hit);
-        while (todo) {
-            const int src = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            RayGeo gw;
-            gw.x0 = __shfl(g.x0, src); gw.x1 = __shfl(g.x1, src); gw.x2 = __shfl(g.x2, src);
-            gw.u0 = __shfl(g.u0, src); gw.u1 = __shfl(g.u1, src); gw.u2 = __shfl(g.u2, src);
-            gw.w0 = __shfl(g.w0, src); gw.w1 = __shfl(g.w1, src); gw.w2 = __shfl(g.w2, src);
-            gw.tc = __shfl(g.tc, src); gw.dd = __shfl(g.dd, src);
-            gw.nx2 = __shfl(g.nx2, src); gw.wx = __shfl(g.wx, src);
-            const int sr = __shfl(s[0], src), se = __shfl(s[1], src), sa = __shfl(s[2], src);
-            trace_one<MODE, T>(G, gw, sr, se, sa, tile * 64 + src, keys, pays, lane, o);
-        }
+        trace_one<MODE, T>(G, g, s[0], s[1], s[2], ray, keys, pays, lane, o);
     }
 }
 
@@ -609,8 +616,10 @@ constexpr size_t kWsHead = 256;      // deferred counter, padded
 static size_t exact_scratch_bytes(const GridDev& G) {
     return (size_t)kExactBlocks * 64 * G.K * sizeof(Cand);
 }
+static size_t hits_bytes(int64_t n) { return (((size_t)n * sizeof(int32_t) + 255) / 256) * 256; }
 static size_t workspace_bytes(const GridDev& G, int64_t n) {
-    return kWsHead + (((size_t)n * sizeof(int64_t) + 255) / 256) * 256 + exact_scratch_bytes(G);
+    return kWsHead + (((size_t)n * sizeof(int64_t) + 255) / 256) * 256 + hits_bytes(n) +
+           exact_scratch_bytes(G);
 }
 
 template <int MODE, typename T>
@@ -626,12 +635,16 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     if (lds > 160 * 1024) return fail("grid too large for the per-wave LDS list (K=%d)", G.K);
     unsigned char* ws = (unsigned char*)workspace;
     o.n_deferred = (unsigned long long*)ws;
+    o.n_hits = (unsigned*)(ws + 64);
     o.deferred = (int64_t*)(ws + kWsHead);
+    o.hits = (int32_t*)(ws + kWsHead + (((size_t)R.n * sizeof(int64_t) + 255) / 256) * 256);
     Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
-    if (hipMemsetAsync(o.n_deferred, 0, kWsHead, st) != hipSuccess) return fail("memset failed");
-    const int64_t ntiles = (R.n + 63) / 64;
-    int64_t grid = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (grid > 4096) grid = 4096;
+    if (hipMemsetAsync(ws, 0, kWsHead, st) != hipSuccess) return fail("memset failed");
+    hipLaunchKernelGGL((screen_kernel<MODE, T>), dim3((unsigned)((R.n + 255) / 256)), dim3(256), 0,
+                       st, G, R, o);
+    if (int e = check_launch("screen_kernel")) return e;
+    // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
+    const int64_t grid = 2048;
     hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(256), lds, st, G, R, o,
                        cap);
     if (int e = check_launch("trace_kernel")) return e;
