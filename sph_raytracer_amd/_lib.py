@@ -11,7 +11,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'lib', 'libsphrt.so')
+# SPHRT_LIB selects another build of the same ABI (kernel A/B studies under tools/)
+LIB_PATH = os.environ.get('SPHRT_LIB') or os.path.join(_HERE, 'lib', 'libsphrt.so')
 MAX_DIMS = 6
 
 c_i32, c_i64, c_dbl, c_vp, c_int = (ctypes.c_int32, ctypes.c_int64, ctypes.c_double,
@@ -36,10 +37,13 @@ class RayBatch(ctypes.Structure):
 class CSR(ctypes.Structure):
     _fields_ = [('n_rays', c_i64), ('n_segments', c_i64), ('row_ptr', c_vp), ('vox', c_vp),
                 ('len', c_vp), ('len32', c_vp), ('row_ray', c_vp), ('blocks', c_vp),
-                ('n_blocks', c_i64)]
+                ('n_blocks', c_i64), ('loc', c_vp), ('tab', c_vp), ('n_cols', c_i64),
+                ('n_fallback', c_i64)]
 
 
 ROW_HEAD = 0x80000000
+BLOCK_FIELDS = 6           # SPHRT_BLOCK_FIELDS
+LOC_HEAD = 0x8000          # SPHRT_LOC_HEAD
 
 # (name, restype, argtypes) — mirrors include/sphrt.h one to one
 _SIGNATURES = [
@@ -59,6 +63,7 @@ _SIGNATURES = [
     ('sphrt_csr_blocks', c_i64, [c_i64]),
     ('sphrt_csr_index_workspace_bytes', ctypes.c_size_t, [c_i64]),
     ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    ('sphrt_csr_local', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_vp, c_vp]),
     ('sphrt_forward_f32', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,
                                   c_vp]),
     ('sphrt_forward_f64', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,

@@ -7,7 +7,7 @@
 // Layout built once per trace (sphrt_csr_index):
 //   vox[s]     linear voxel index, bit 31 set on the first segment of every non-empty ray
 //   row_ray[k] the ray of the k-th non-empty row
-//   blocks[b]  {ray_lo, ray_hi, seg_lo, seg_hi, row_lo}: workgroup b owns the rays whose rows
+//   blocks[b]  {ray_lo, ray_hi, seg_lo, seg_hi, row_lo, n_tab}: workgroup b owns the rays whose rows
 //              start in [b*kSegPerBlock, (b+1)*kSegPerBlock) — whole rows, so no row is ever
 //              split between workgroups and the result needs no cross-workgroup combine.
 // Forward per workgroup: each thread streams 8 consecutive segments (aligned vector loads),
@@ -24,6 +24,10 @@ constexpr int kPer = 8;                         // segments per thread per pass
 constexpr int kPass = kThreads * kPer;          // 2048 segments per pass
 constexpr int64_t kSegPerBlock = 1792;          // row starts per workgroup (leaves room for the
                                                 // last row's overhang inside one pass)
+constexpr int kBlockFields = 6;                 // ray_lo, ray_hi, seg_lo, seg_hi, row_lo, n_tab
+constexpr int kLocalMax = 4096;                 // segments per workgroup with a granule table
+constexpr int kMaxGran = 1024;                  // granules per table (16 KB of f32 in LDS)
+constexpr int kGranEach = kMaxGran / kThreads;
 
 // ---- index --------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* row_ptr, int64_t n,
@@ -60,12 +64,13 @@ __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
     };
     const int64_t lo = first_at_or_after(b * kSegPerBlock);
     const int64_t hi = (b + 1 == nblocks) ? n : first_at_or_after((b + 1) * kSegPerBlock);
-    int64_t* m = blocks + 5 * b;
+    int64_t* m = blocks + kBlockFields * b;
     m[0] = lo;
     m[1] = hi;
     m[2] = row_ptr[lo];
     m[3] = row_ptr[hi];
     m[4] = row_pre[lo];
+    m[5] = -1;                                  // no voxel table until sphrt_csr_local
 }
 
 // ---- block-level scans (256 threads = 4 waves) -----------------------------------------------
@@ -75,15 +80,45 @@ struct ScanShared {
     double sum[4];
 };
 
+// Wave-level inclusive scans on DPP lane moves (no LDS crossbar, no lane-index registers):
+// row_shr 1, 2, 4, 8 within each row of 16 lanes, then row_bcast 15 (rows 1, 3) and row_bcast 31
+// (rows 2, 3).  Lanes without a source read the identity (`old` = 0).
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ int dpp0(int x) {
+    return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ double dpp0(double x) {
+    const uint64_t b = __double_as_longlong(x);
+    const int lo = dpp0<CTRL, ROWS>((int)(uint32_t)b), hi = dpp0<CTRL, ROWS>((int)(uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+constexpr int kShr1 = 0x111, kShr2 = 0x112, kShr4 = 0x114, kShr8 = 0x118, kBcast15 = 0x142,
+              kBcast31 = 0x143, kWaveShr1 = 0x138;
+
+__device__ __forceinline__ int wave_incl_sum(int x) {
+    x += dpp0<kShr1>(x);
+    x += dpp0<kShr2>(x);
+    x += dpp0<kShr4>(x);
+    x += dpp0<kShr8>(x);
+    x += dpp0<kBcast15, 0xa>(x);
+    x += dpp0<kBcast31, 0xc>(x);
+    return x;
+}
+
+// segmented element (h, s): (h1,s1) o (h2,s2) = (h1|h2, h2 ? s2 : s1+s2)
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ void seg_step(int& h, double& s) {
+    const int hu = dpp0<CTRL, ROWS>(h);
+    const double su = dpp0<CTRL, ROWS>(s);
+    s = h ? s : su + s;
+    h |= hu;
+}
+
 // exclusive sum of one int per thread; returns the block total in `total`
 __device__ __forceinline__ int block_excl_count(int v, int& total, ScanShared& sh) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int inc = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int u = __shfl_up(inc, off);
-        if (lane >= off) inc += u;
-    }
+    const int inc = wave_incl_sum(v);
     if (lane == 63) sh.cnt[wid] = inc;
     __syncthreads();
     int base = 0;
@@ -93,28 +128,21 @@ __device__ __forceinline__ int block_excl_count(int v, int& total, ScanShared& s
     return base + inc - v;
 }
 
-// segmented scan: element (has_head, tail) combines as (h1,s1) o (h2,s2) = (h1|h2, h2 ? s2 : s1+s2).
-// Returns the exclusive prefix sum value (the open run entering this thread) and the block total.
+// Segmented scan of (has_head, tail) per thread.  Returns the exclusive prefix sum value (the
+// open run entering this thread) and the block total.
 __device__ __forceinline__ double block_excl_segsum(bool has, double tail, bool& tot_has,
                                                     double& tot_sum, ScanShared& sh) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    bool h = has;
+    int h = has ? 1 : 0;
     double s = tail;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const bool hu = __shfl_up((int)h, off) != 0;
-        const double su = __shfl_up(s, off);
-        if (lane >= off) {
-            s = h ? s : su + s;
-            h = h || hu;
-        }
-    }
-    bool eh = __shfl_up((int)h, 1) != 0;
-    double es = __shfl_up(s, 1);
-    if (lane == 0) {
-        eh = false;
-        es = 0.0;
-    }
+    seg_step<kShr1>(h, s);
+    seg_step<kShr2>(h, s);
+    seg_step<kShr4>(h, s);
+    seg_step<kShr8>(h, s);
+    seg_step<kBcast15, 0xa>(h, s);
+    seg_step<kBcast31, 0xc>(h, s);
+    const int eh = dpp0<kWaveShr1>(h);       // lane 0 reads the identity
+    const double es = dpp0<kWaveShr1>(s);
     if (lane == 63) {
         sh.has[wid] = h;
         sh.sum[wid] = s;
@@ -133,24 +161,200 @@ __device__ __forceinline__ double block_excl_segsum(bool has, double tail, bool&
     return eh ? es : cs + es;
 }
 
+// Per-segment arrays are readable up to the next multiple of 8 entries (sphrt.h), so every chunk
+// that starts before s1 is one aligned 32-byte (vox) / 32- or 64-byte (len) vector load; entries
+// outside [s0, s1) are masked to zero.  Pointers are pass-relative, offsets 32-bit.
+template <typename L>
+__device__ __forceinline__ void load_len8(const L* __restrict__ len, int p0, L (&l)[kPer]) {
+    if constexpr (sizeof(L) == 4) {
+        const float4* lp = reinterpret_cast<const float4*>(len + p0);
+        const float4 f = lp[0], g = lp[1];
+        l[0] = f.x; l[1] = f.y; l[2] = f.z; l[3] = f.w;
+        l[4] = g.x; l[5] = g.y; l[6] = g.z; l[7] = g.w;
+    } else {
+        const double2* lp = reinterpret_cast<const double2*>(len + p0);
+#pragma unroll
+        for (int k = 0; k < kPer / 2; ++k) {
+            const double2 f = lp[k];
+            l[2 * k] = f.x;
+            l[2 * k + 1] = f.y;
+        }
+    }
+}
+
+template <typename L>
+__device__ __forceinline__ void mask8(int p0, int s0, int s1, uint32_t (&v)[kPer], L (&l)[kPer]) {
+    const int first = s0 - p0, end = s1 - p0;   // chunk-relative window: compare against k
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+        if (k < first || k >= end) {
+            v[k] = 0u;
+            l[k] = (L)0;
+        }
+}
+
 template <typename L>
 __device__ __forceinline__ void load8(const int32_t* __restrict__ vox, const L* __restrict__ len,
-                                      int64_t p0, int64_t s0, int64_t s1, uint32_t (&v)[kPer],
-                                      L (&l)[kPer]) {
-    if (p0 >= s0 && p0 + kPer <= s1) {        // whole chunk inside: 16-byte vector loads
+                                      int p0, int s0, int s1, uint32_t (&v)[kPer], L (&l)[kPer]) {
+    if (p0 < s1) {
         const uint4* vp = reinterpret_cast<const uint4*>(vox + p0);
         const uint4 a = vp[0], b = vp[1];
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
         v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) l[k] = len[p0 + k];
+        load_len8(len, p0, l);
+        if (p0 < s0 || p0 + kPer > s1) mask8(p0, s0, s1, v, l);
     } else {
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            const int64_t s = p0 + k;
-            const bool ok = s >= s0 && s < s1;
-            v[k] = ok ? (uint32_t)vox[s] : 0u;
-            l[k] = ok ? len[s] : (L)0;
+            v[k] = 0u;
+            l[k] = (L)0;
+        }
+    }
+}
+
+// ---- per-workgroup granule table ----------------------------------------------------------
+// Per-segment density gathers are the forward's bottleneck: every segment is one divergent 4-byte
+// lane access, and the load path's per-lane rate, not bytes, bounds the kernel (C2: ~7 of 13 us).
+// Built once per trace: for every workgroup, the sorted distinct 4-voxel granules its segments
+// read (tab[s0 .. s0+n_tab), granule g = voxels 4g..4g+3) and, per segment, the slot
+// 4*rank + (voxel & 3) of its voxel, with the row-head flag in bit 15 (loc).  The forward stages
+// the granules into LDS with 16-byte LDS-DMA loads (one lane per granule, ~3x fewer lane accesses
+// than segments) and the segments read LDS.  n_tab = -1 marks a workgroup left on the
+// per-segment gather (more than kLocalMax segments or kMaxGran granules).
+__global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restrict__ blocks,
+                                                               const int32_t* __restrict__ vox,
+                                                               uint16_t* __restrict__ loc,
+                                                               int32_t* __restrict__ tab,
+                                                               unsigned long long* n_fallback) {
+    __shared__ uint64_t key[kLocalMax];
+    __shared__ ScanShared sh;
+    int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
+    const int64_t s0 = m[2], s1 = m[3];
+    const int n = (int)min<int64_t>(s1 - s0, (int64_t)kLocalMax + 1);
+    const int tid = threadIdx.x;
+    if (n > kLocalMax) {
+        if (tid == 0) {
+            m[5] = -1;
+            atomicAdd(n_fallback, 1ull);
+        }
+        return;
+    }
+    int p = 1;
+    while (p < n) p <<= 1;
+    // key = voxel << 13 | position << 1 | head; voxel >> 2 is the granule
+    for (int i = tid; i < p; i += kThreads) {
+        uint64_t k = ~0ull;
+        if (i < n) {
+            const uint32_t x = (uint32_t)vox[s0 + i];
+            k = ((uint64_t)(x & ~kHead) << 13) | ((uint64_t)i << 1) | (uint64_t)(x >> 31);
+        }
+        key[i] = k;
+    }
+    __syncthreads();
+    for (int k = 2; k <= p; k <<= 1)          // bitonic sort, ascending
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < p; i += kThreads) {
+                const int ij = i ^ j;
+                if (ij > i) {
+                    const uint64_t x = key[i], y = key[ij];
+                    if (((i & k) == 0) == (x > y)) {
+                        key[i] = y;
+                        key[ij] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // distinct granules: thread t owns sorted entries [16t, 16t+16)
+    constexpr int kEach = kLocalMax / kThreads;
+    auto gran = [](uint64_t k) { return k >> 15; };
+    int first_new = 0;
+#pragma unroll
+    for (int q = 0; q < kEach; ++q) {
+        const int i = tid * kEach + q;
+        if (i < n && (i == 0 || gran(key[i]) != gran(key[i - 1]))) ++first_new;
+    }
+    int n_tab;
+    int rank = block_excl_count(first_new, n_tab, sh) - 1;
+    if (n_tab > kMaxGran) {
+        if (tid == 0) {
+            m[5] = -1;
+            atomicAdd(n_fallback, 1ull);
+        }
+        return;
+    }
+#pragma unroll
+    for (int q = 0; q < kEach; ++q) {
+        const int i = tid * kEach + q;
+        if (i >= n) break;
+        const uint64_t k = key[i];
+        if (i == 0 || gran(k) != gran(key[i - 1])) {
+            ++rank;
+            tab[s0 + rank] = (int32_t)gran(k);
+        }
+        const int pos = (int)((k >> 1) & 0xfff);
+        const int slot = 4 * rank + (int)((k >> 13) & 3);
+        loc[s0 + pos] = (uint16_t)(slot | ((k & 1) ? 0x8000 : 0));
+    }
+    if (tid == 0) m[5] = n_tab;
+}
+
+// LDS image of the staged granules.  float: granule j at dens[4j .. 4j+3].  double (32-byte
+// granules, two 16-byte DMA halves): voxels 0-1 of granule j at dens[2j ..], voxels 2-3 at
+// dens[2*kMaxGran + 2j ..].
+template <typename T>
+__device__ __forceinline__ int dens_index(uint32_t slot) {
+    if constexpr (sizeof(T) == 4) return (int)slot;
+    else return (int)(((slot & 2u) ? 2 * kMaxGran : 0) + ((slot >> 2) << 1) + (slot & 1u));
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_granules(const T* __restrict__ rho, const int32_t (&ti)[kGranEach],
+                                               int n_tab, int64_t n_cols, T* dens) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < kGranEach; ++q) {
+        const int j0 = q * kThreads + w * 64;   // this wave's 64 granules of round q
+        const int j = j0 + lane;
+        if (j >= n_tab) continue;
+        const int64_t v0 = 4 * (int64_t)ti[q];
+        if (v0 + 4 <= n_cols) {
+            if constexpr (sizeof(T) == 4) {
+                __builtin_amdgcn_global_load_lds((const void*)(rho + v0),
+                    (__attribute__((address_space(3))) void*)(dens + 4 * j0), 16, 0, 0);
+            } else {
+                __builtin_amdgcn_global_load_lds((const void*)(rho + v0),
+                    (__attribute__((address_space(3))) void*)(dens + 2 * j0), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((const void*)(rho + v0 + 2),
+                    (__attribute__((address_space(3))) void*)(dens + 2 * kMaxGran + 2 * j0), 16, 0, 0);
+            }
+        } else {                                 // the volume's last, partial granule
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                dens[dens_index<T>(4 * j + i)] = v0 + i < n_cols ? rho[v0 + i] : (T)0;
+        }
+    }
+}
+
+template <typename L>
+__device__ __forceinline__ void load8_loc(const uint16_t* __restrict__ loc,
+                                          const L* __restrict__ len, int p0, int s0, int s1,
+                                          uint32_t (&v)[kPer], L (&l)[kPer]) {
+    if (p0 < s1) {                            // 16 bytes of slots, 8 lengths
+        const uint4 a = *reinterpret_cast<const uint4*>(loc + p0);
+        const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t x = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+            v[k] = (x & 0x7fffu) | ((x & 0x8000u) << 16);
+        }
+        load_len8(len, p0, l);
+        if (p0 < s0 || p0 + kPer > s1) mask8(p0, s0, s1, v, l);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            v[k] = 0u;
+            l[k] = (L)0;
         }
     }
 }
@@ -158,50 +362,117 @@ __device__ __forceinline__ void load8(const int32_t* __restrict__ vox, const L* 
 // ---- forward ------------------------------------------------------------------------------
 // Channels: static multichannel -> every ray for every channel c < n_chan; ray_chan_div > 0 ->
 // ray i reads channel i / div (a time slice per view) and writes out[i].
-template <typename T, typename L>
+// Per workgroup: block record -> {segment stream, voxel table, row_ptr of its share of the empty
+// rays} -> table gather into LDS -> count scan -> segmented sum scan -> row->ray lookup -> stores.
+// Modes (one instantiation each, so each carries only its own registers):
+//   kFwdTable    static channels, density staged per workgroup from its granule table; skips the
+//                workgroups without a table (n_tab < 0)
+//   kFwdGather   static channels, per-segment gathers through vox; with `fallback_only`, only the
+//                workgroups a kFwdTable launch skipped (and no empty-ray zeroing)
+//   kFwdDynamic  ray i reads channel i / div
+enum FwdMode { kFwdTable = 0, kFwdGather = 1, kFwdDynamic = 2 };
+
+template <typename T, typename L, int MODE>
 __global__ __launch_bounds__(kThreads) void forward_kernel(
     const int64_t* __restrict__ blocks, const int64_t* __restrict__ row_ptr,
-    const int32_t* __restrict__ vox, const L* __restrict__ len,
+    const int32_t* __restrict__ vox, const uint16_t* __restrict__ loc,
+    const int32_t* __restrict__ tab, const L* __restrict__ len,
     const int32_t* __restrict__ row_ray, const T* __restrict__ density, int64_t n_chan,
-    int64_t cs, int64_t div, T* __restrict__ out, int64_t ocs) {
+    int64_t cs, int64_t div, T* __restrict__ out, int64_t ocs, int64_t n_rays, int64_t n_cols,
+    int fallback_only) {
     __shared__ ScanShared sh;
-    const int64_t* m = blocks + 5 * (int64_t)blockIdx.x;
-    const int64_t lo = m[0], hi = m[1], s0 = m[2], s1 = m[3], k0 = m[4];
+    __shared__ __attribute__((aligned(16))) T dens[4 * kMaxGran];
+    const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
+    const int64_t s0 = m[2], k0 = m[4], n_tab = m[5];
+    int64_t s1 = m[3];
     const int tid = threadIdx.x;
-    const int64_t nc = div > 0 ? 1 : n_chan;
-    // empty rays integrate to zero
-    for (int64_t r = lo + tid; r < hi; r += kThreads)
-        if (row_ptr[r + 1] == row_ptr[r])
-            for (int64_t c = 0; c < nc; ++c) out[c * ocs + r] = (T)0;
+    const int o = tid * kPer;                       // this thread's chunk within a pass
+    const int64_t nc = MODE == kFwdDynamic ? 1 : n_chan;
+    const int64_t a0 = s0 & ~(int64_t)(kPer - 1);   // passes start 8-aligned
+    constexpr bool local = MODE == kFwdTable;
+    if (MODE == kFwdTable && n_tab < 0) s1 = s0;      // left to the kFwdGather fallback launch
+    if (MODE == kFwdGather && fallback_only && n_tab >= 0) return;
+    // pass-relative segment window [lo, hi) of this workgroup (32-bit lane arithmetic)
+    auto window = [&](int64_t base, int& lo, int& hi) {
+        lo = (int)max<int64_t>(s0 - base, -1);
+        hi = (int)min<int64_t>(s1 - base, (int64_t)kPass + 1);
+    };
+    auto load_pass = [&](int64_t base, uint32_t (&v)[kPer], L (&l)[kPer]) {
+        int lo, hi;
+        window(base, lo, hi);
+        if (local) load8_loc(loc + base, len + base, o, lo, hi, v, l);
+        else load8(vox + base, len + base, o, lo, hi, v, l);
+    };
+    uint32_t v[kPer];
+    L l[kPer];
+    int32_t ti[kGranEach];
+    if (s0 < s1) {
+        load_pass(a0, v, l);
+        if (local) {
+#pragma unroll
+            for (int q = 0; q < kGranEach; ++q) {
+                const int j = tid + q * kThreads;
+                ti[q] = j < n_tab ? tab[s0 + j] : 0;
+            }
+        }
+    }
+    // Empty rays integrate to zero.  They are split evenly over the workgroups, independently of
+    // the segment partition (a block whose rows start late may own thousands of empty rays).
+    // Their row_ptr loads go out with the segment loads and are retired right away.
+    if (!fallback_only) {
+        const int64_t e_chunk = (n_rays + gridDim.x - 1) / gridDim.x;
+        const int64_t e_lo = min<int64_t>((int64_t)blockIdx.x * e_chunk, n_rays);
+        const int e_n = (int)(min<int64_t>(e_lo + e_chunk, n_rays) - e_lo);
+        const int64_t* rp = row_ptr + e_lo;
+        for (int r = tid; r < e_n; r += kThreads)
+            if (rp[r + 1] == rp[r])
+                for (int64_t c = 0; c < nc; ++c) out[c * ocs + e_lo + r] = (T)0;
+    }
     if (s0 >= s1) return;
-    const int64_t a0 = s0 & ~(int64_t)(kPer - 1);   // chunk grid aligned to 8 segments (32 B)
     for (int64_t c = 0; c < nc; ++c) {
-        double carry = 0.0;      // open run entering the pass
-        int64_t heads_done = 0;  // heads in earlier passes
+        const T* rho = density + c * cs;
+        T* oc = out + c * ocs;
+        if (local) {
+            if (c > 0) {
+#pragma unroll
+                for (int q = 0; q < kGranEach; ++q) {
+                    const int j = tid + q * kThreads;
+                    ti[q] = j < n_tab ? tab[s0 + j] : 0;
+                }
+            }
+            stage_granules<T>(rho, ti, (int)n_tab, n_cols, dens);
+        }
+        double carry = 0.0;                 // open run entering the pass
+        const int32_t* rows = row_ray + k0;   // rows of heads seen in earlier passes skipped below
         for (int64_t base = a0; base < s1; base += kPass) {
-            const int64_t p0 = base + (int64_t)tid * kPer;
-            uint32_t v[kPer];
-            L l[kPer];
-            load8(vox, len, p0, s0, s1, v, l);
+            if (base != a0 || c != 0) load_pass(base, v, l);
+            int lo, hi;
+            window(base, lo, hi);
             int hcount = 0;
 #pragma unroll
             for (int k = 0; k < kPer; ++k) hcount += (v[k] & kHead) ? 1 : 0;
             T rv[kPer];
-            if (div == 0) {           // static: gathers go out before any scan
-                const T* rho = density + c * cs;
+            if (MODE == kFwdGather) {       // per-segment gathers go out before any scan
 #pragma unroll
-                for (int k = 0; k < kPer; ++k) rv[k] = l[k] != (L)0 ? rho[v[k] & ~kHead] : (T)0;
+                for (int k = 0; k < kPer; ++k)
+                    rv[k] = l[k] != (L)0 ? rho[v[k] & ~kHead] : (T)0;
             }
             int pass_heads;
-            const int hb = block_excl_count(hcount, pass_heads, sh);
-            if (div > 0) {            // time slice of each segment's ray
+            const int hb = block_excl_count(hcount, pass_heads, sh);   // barrier: dens ready
+            pass_heads = __builtin_amdgcn_readfirstlane(pass_heads);
+            if (local) {
+#pragma unroll
+                for (int k = 0; k < kPer; ++k)
+                    rv[k] = l[k] != (L)0 ? dens[dens_index<T>(v[k] & ~kHead)] : (T)0;
+            }
+            if (MODE == kFwdDynamic) {      // time slice of each segment's ray
                 int rank = 0;
 #pragma unroll
                 for (int k = 0; k < kPer; ++k) {
                     rank += (v[k] & kHead) ? 1 : 0;
                     T x = (T)0;
                     if (l[k] != (L)0) {
-                        const int64_t ray = row_ray[k0 + heads_done + hb + rank - 1];
+                        const int64_t ray = rows[hb + rank - 1];
                         x = density[(ray / div) * cs + (v[k] & ~kHead)];
                     }
                     rv[k] = x;
@@ -224,27 +495,23 @@ __global__ __launch_bounds__(kThreads) void forward_kernel(
             // the run open at this thread's start: the segmented prefix of the earlier threads,
             // plus the carry of earlier passes when no earlier thread of this pass saw a head
             double run = hb > 0 ? ex : carry + ex;
-            int seen = 0;
+            int seen = hb - 1;
+            const int first = lo - o, end = hi - o;   // chunk-relative window
+            const bool opens = base != a0;            // a head at the window start closes a row
+            const bool closes = base + kPass >= s1;   // the window end closes the last row
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
-                const int64_t s = p0 + k;
-                if (s < s0 || s >= s1) continue;
+                if (k < first || k >= end) continue;
                 if (v[k] & kHead) {
-                    if (s > s0) {
-                        const int64_t ray = row_ray[k0 + heads_done + hb + seen - 1];
-                        out[c * ocs + ray] = (T)run;
-                    }
+                    if (k > first || opens) oc[rows[seen]] = (T)run;   // close the previous row
                     run = 0.0;
                     ++seen;
                 }
                 run += (double)rv[k] * (double)l[k];
-                if (s == s1 - 1) {
-                    const int64_t ray = row_ray[k0 + heads_done + hb + seen - 1];
-                    out[c * ocs + ray] = (T)run;
-                }
+                if (k == end - 1 && closes) oc[rows[seen]] = (T)run;   // last row
             }
             carry = tot_has ? tot_sum : carry + tot_sum;
-            heads_done += pass_heads;
+            rows += pass_heads;
         }
     }
 }
@@ -257,7 +524,7 @@ __global__ __launch_bounds__(kThreads) void adjoint_kernel(
     const TY* __restrict__ y, int64_t n_chan, int64_t ycs, int64_t div, double* acc,
     int64_t cs) {
     __shared__ ScanShared sh;
-    const int64_t* m = blocks + 5 * (int64_t)blockIdx.x;
+    const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
     const int64_t s0 = m[2], s1 = m[3], k0 = m[4];
     if (s0 >= s1) return;
     const int tid = threadIdx.x;
@@ -265,10 +532,10 @@ __global__ __launch_bounds__(kThreads) void adjoint_kernel(
     const int64_t nc = div > 0 ? 1 : n_chan;
     int64_t heads_done = 0;
     for (int64_t base = a0; base < s1; base += kPass) {
-        const int64_t p0 = base + (int64_t)tid * kPer;
         uint32_t v[kPer];
         double l[kPer];
-        load8(vox, len, p0, s0, s1, v, l);
+        load8(vox + base, len + base, tid * kPer, (int)max<int64_t>(s0 - base, -1),
+              (int)min<int64_t>(s1 - base, (int64_t)kPass + 1), v, l);
         int hcount = 0;
 #pragma unroll
         for (int k = 0; k < kPer; ++k) hcount += (v[k] & kHead) ? 1 : 0;
@@ -330,6 +597,20 @@ extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* 
     return check_launch("block_meta");
 }
 
+extern "C" int sphrt_csr_local(const sphrt_csr* c, int64_t* blocks, uint16_t* loc, int32_t* tab,
+                               int64_t* n_fallback, void* stream) {
+    if (!c || !c->vox || !blocks || !loc || !tab || !n_fallback)
+        return fail("incomplete CSR for the granule tables");
+    if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(n_fallback, 0, sizeof(int64_t), st) != hipSuccess)
+        return fail("hipMemsetAsync failed");
+    if (c->n_segments == 0) return 0;
+    hipLaunchKernelGGL(local_table_kernel, dim3((unsigned)c->n_blocks), dim3(kThreads), 0, st,
+                       blocks, c->vox, loc, tab, (unsigned long long*)n_fallback);
+    return check_launch("local_table_kernel");
+}
+
 static int check_csr(const sphrt_csr* c, int64_t n_chan, int64_t div) {
     if (!c || !c->row_ptr || !c->vox || !c->row_ray || !c->blocks) return fail("incomplete CSR");
     if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
@@ -338,16 +619,46 @@ static int check_csr(const sphrt_csr* c, int64_t n_chan, int64_t div) {
     return 0;
 }
 
+// The granule tables apply to static channels whose granules are 16-byte (float) / 32-byte
+// (double) aligned; anything else takes the per-segment gather through vox.
+template <typename T>
+static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int64_t chan_stride,
+                       int64_t div) {
+    if (!c->loc || !c->tab || c->n_cols <= 0 || div > 0) return false;
+    if ((uintptr_t)density % (4 * sizeof(T)) != 0) return false;
+    if (n_chan > 1 && chan_stride % 4 != 0) return false;
+    return true;
+}
+
+template <typename T, typename L>
+static int launch_forward(const sphrt_csr* c, const L* len, const T* density, int64_t n_chan,
+                          int64_t chan_stride, int64_t div, T* out, int64_t ocs, void* stream) {
+    const dim3 grid((unsigned)c->n_blocks), block(kThreads);
+    hipStream_t st = (hipStream_t)stream;
+#define SPHRT_FWD_ARGS c->blocks, c->row_ptr, c->vox, c->loc, c->tab, len, c->row_ray, density, \
+                       n_chan, chan_stride, div, out, ocs, c->n_rays, c->n_cols
+    if (div > 0) {
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic>), grid, block, 0, st, SPHRT_FWD_ARGS, 0);
+    } else if (use_tables(c, density, n_chan, chan_stride, div)) {
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable>), grid, block, 0, st, SPHRT_FWD_ARGS, 0);
+        if (c->n_fallback > 0) {
+            if (int e = check_launch("forward_kernel<table>")) return e;
+            hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather>), grid, block, 0, st, SPHRT_FWD_ARGS, 1);
+        }
+    } else {
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather>), grid, block, 0, st, SPHRT_FWD_ARGS, 0);
+    }
+#undef SPHRT_FWD_ARGS
+    return check_launch(sizeof(T) == 4 ? "forward_kernel<f32>" : "forward_kernel<f64>");
+}
+
 extern "C" int sphrt_forward_f32(const sphrt_csr* c, const float* density, int64_t n_chan,
                                  int64_t chan_stride, int64_t div, float* out, int64_t ocs,
                                  void* stream) {
     if (int e = check_csr(c, n_chan, div)) return e;
     if (!c->len32) return fail("the float32 forward needs the float32 length copy (len32)");
     if (c->n_rays == 0) return 0;
-    hipLaunchKernelGGL((forward_kernel<float, float>), dim3((unsigned)c->n_blocks), dim3(kThreads),
-                       0, (hipStream_t)stream, c->blocks, c->row_ptr, c->vox, c->len32,
-                       c->row_ray, density, n_chan, chan_stride, div, out, ocs);
-    return check_launch("forward_kernel<f32>");
+    return launch_forward(c, c->len32, density, n_chan, chan_stride, div, out, ocs, stream);
 }
 
 extern "C" int sphrt_forward_f64(const sphrt_csr* c, const double* density, int64_t n_chan,
@@ -356,10 +667,7 @@ extern "C" int sphrt_forward_f64(const sphrt_csr* c, const double* density, int6
     if (int e = check_csr(c, n_chan, div)) return e;
     if (!c->len) return fail("missing segment lengths");
     if (c->n_rays == 0) return 0;
-    hipLaunchKernelGGL((forward_kernel<double, double>), dim3((unsigned)c->n_blocks),
-                       dim3(kThreads), 0, (hipStream_t)stream, c->blocks, c->row_ptr, c->vox,
-                       c->len, c->row_ray, density, n_chan, chan_stride, div, out, ocs);
-    return check_launch("forward_kernel<f64>");
+    return launch_forward(c, c->len, density, n_chan, chan_stride, div, out, ocs, stream);
 }
 
 extern "C" int sphrt_adjoint_accumulate(const sphrt_csr* c, const void* y, int y_is_f64,

@@ -229,6 +229,24 @@ def _layout_for(grid, ray_shape, shape):
     return math.prod(lead), 0, lead + R
 
 
+def _seg_alloc(total):
+    """Per-segment arrays are allocated to a multiple of 8 entries (the apply kernels read whole
+    aligned 8-segment chunks; entries past the total are masked, never used)."""
+    return max((total + 7) // 8 * 8, 8)
+
+
+def _local_tables(lib, desc, blocks, total, dev, stream):
+    """Per-workgroup granule tables of a CSR (sphrt_csr_local); sets desc.loc/.tab."""
+    loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
+    tab = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+    n_fallback = tr.empty(1, dtype=tr.int64, device=dev)
+    _lib.check(lib.sphrt_csr_local(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(tab),
+                                   _lib.ptr(n_fallback), stream), 'sphrt_csr_local')
+    desc.n_fallback = int(n_fallback.item())
+    desc.loc, desc.tab = loc.data_ptr(), tab.data_ptr()
+    return loc, tab
+
+
 def _workspace(lib, plan, n, dev):
     return tr.empty(lib.sphrt_trace_workspace_bytes(plan.handle, n), dtype=tr.uint8, device=dev)
 
@@ -327,8 +345,8 @@ class Operator:
         _lib.check(lib.sphrt_scan_counts(_lib.ptr(counts), n, _lib.ptr(row_ptr), _lib.ptr(ws),
                                          stream), 'sphrt_scan_counts')
         total = int(row_ptr[n].item())          # the one host sync of the trace
-        vox = tr.empty(max(total, 1), dtype=tr.int32, device=dev)
-        seg_len = tr.empty(max(total, 1), dtype=tr.float64, device=dev)
+        vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+        seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
         _lib.check(lib.sphrt_trace_fill(self._plan.handle, batch.desc, _lib.ptr(row_ptr),
                                         _lib.ptr(vox), _lib.ptr(seg_len), _lib.ptr(tws),
                                         tws.numel(), stream), 'sphrt_trace_fill')
@@ -336,7 +354,7 @@ class Operator:
         # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
         nblocks = lib.sphrt_csr_blocks(total)
         row_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
-        blocks = tr.empty(5 * nblocks, dtype=tr.int64, device=dev)
+        blocks = tr.empty(_lib.BLOCK_FIELDS * nblocks, dtype=tr.int64, device=dev)
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(row_ptr), n, _lib.ptr(vox), _lib.ptr(row_ray),
                                        _lib.ptr(blocks), nblocks, _lib.ptr(iws), stream),
@@ -346,8 +364,10 @@ class Operator:
         c.n_rays, c.n_segments, c.n_blocks = n, total, nblocks
         c.row_ptr, c.vox, c.len = row_ptr.data_ptr(), vox.data_ptr(), seg_len.data_ptr()
         c.row_ray, c.blocks, c.len32 = row_ray.data_ptr(), blocks.data_ptr(), None
+        c.n_cols = math.prod(self.grid.shape[-3:])
+        loc, tab = _local_tables(lib, c, blocks, total, dev, stream)
         self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, row_ray=row_ray, blocks=blocks,
-                         nblocks=nblocks, n=n, total=total, desc=c)
+                         loc=loc, tab=tab, nblocks=nblocks, n=n, total=total, desc=c)
         self._batch = batch
 
     # -- shape logic of raytracer.py:703-712 -----------------------------------------------------
@@ -418,8 +438,8 @@ class Operator:
         n_vox = math.prod(self.grid.shape[-3:])
         total = csr['total']
         col_ptr = tr.empty(n_vox + 1, dtype=tr.int64, device=dev)
-        t_ray = tr.empty(max(total, 1), dtype=tr.int32, device=dev)
-        t_len = tr.empty(max(total, 1), dtype=tr.float64, device=dev)
+        t_ray = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+        t_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
         ws = tr.empty(lib.sphrt_transpose_workspace_bytes(total, n_vox), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_transpose(csr['desc'], n_vox, _lib.ptr(col_ptr), _lib.ptr(t_ray),
                                            _lib.ptr(t_len), _lib.ptr(ws), ws.numel(), stream),
@@ -427,7 +447,7 @@ class Operator:
         del ws
         nblocks = lib.sphrt_csr_blocks(total)
         vox_list = tr.empty(n_vox, dtype=tr.int32, device=dev)
-        blocks = tr.empty(5 * nblocks, dtype=tr.int64, device=dev)
+        blocks = tr.empty(_lib.BLOCK_FIELDS * nblocks, dtype=tr.int64, device=dev)
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n_vox), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(col_ptr), n_vox, _lib.ptr(t_ray),
                                        _lib.ptr(vox_list), _lib.ptr(blocks), nblocks,
@@ -440,7 +460,9 @@ class Operator:
         c.row_ptr, c.vox, c.len, c.len32 = (col_ptr.data_ptr(), t_ray.data_ptr(),
                                             t_len.data_ptr(), t_len32.data_ptr())
         c.row_ray, c.blocks = vox_list.data_ptr(), blocks.data_ptr()
-        csr['T'] = dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, blocks))
+        c.n_cols = csr['n']
+        loc, tab = _local_tables(lib, c, blocks, total, dev, stream)
+        csr['T'] = dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, blocks, loc, tab))
         return csr['T']
 
     def _apply_adjoint(self, y, dshape, ddtype, ddevice):

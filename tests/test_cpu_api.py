@@ -220,6 +220,11 @@ def test_library_builds_and_exports_header():
     for name in declared:
         assert hasattr(lib, name), f'{name} declared in include/sphrt.h but not exported'
     assert sorted(_lib.EXPORTED) == declared, 'ctypes bindings out of sync with the header'
+    hdr = open(os.path.join(ROOT, 'include', 'sphrt.h')).read()
+    for name, val in (('SPHRT_ROW_HEAD', _lib.ROW_HEAD), ('SPHRT_BLOCK_FIELDS', _lib.BLOCK_FIELDS),
+                      ('SPHRT_LOC_HEAD', _lib.LOC_HEAD)):
+        m = re.search(rf'#define {name} (0x[0-9a-fA-F]+|\d+)', hdr)
+        assert m and int(m.group(1).rstrip('u'), 0) == val, name
     lib = _lib.load()
     assert lib.sphrt_version().startswith(b'sph_raytracer_amd')
     assert lib.sphrt_scan_workspace_bytes(10_000) > 0

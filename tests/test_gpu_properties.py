@@ -101,6 +101,71 @@ def test_fused_equals_csr(c2, gpu):
     assert float((a - b).abs().max()) <= 1e-12 * float(a.abs().max())
 
 
+def test_granule_tables(c2, gpu):
+    """Per-workgroup granule tables (sphrt_csr_local): each table ascending and distinct, every
+    segment's slot names its voxel's granule and lane and carries its row-head flag; the table
+    forward equals the per-segment-gather forward bitwise, for the forward and the transposed
+    adjoint."""
+    from sph_raytracer_amd import _lib
+    grid, geom, op = c2
+    csr = op._csr
+    blocks = csr['blocks'].cpu().numpy().reshape(-1, _lib.BLOCK_FIELDS)
+    vox = csr['vox'].cpu().numpy().view(np.uint32)[:csr['total']]
+    loc = csr['loc'].cpu().numpy().view(np.uint16)[:csr['total']]
+    tab = csr['tab'].cpu().numpy()
+    s0, s1, n_tab = blocks[:, 2], blocks[:, 3], blocks[:, 5]
+    assert (n_tab >= 0).all() and (n_tab <= s1 - s0).all() and csr['desc'].n_fallback == 0
+    owner = np.repeat(np.arange(len(blocks)), s1 - s0)
+    slot = (loc & 0x7fff).astype(np.int64)
+    assert (slot // 4 < n_tab[owner]).all()
+    v = (vox & 0x7fffffff).astype(np.int64)
+    assert np.array_equal(tab[s0[owner] + slot // 4], v >> 2)
+    assert np.array_equal(slot % 4, v % 4)
+    assert np.array_equal(loc >> 15, vox >> 31)
+    for b in range(0, len(blocks), 97):
+        assert (np.diff(tab[s0[b]:s0[b] + n_tab[b]]) > 0).all()
+    g = tr.Generator(device=gpu).manual_seed(3)
+    for dt in (tr.float32, tr.float64):
+        x = tr.rand(grid.shape, dtype=dt, device=gpu, generator=g)
+        y = tr.rand(geom.shape, dtype=dt, device=gpu, generator=g)
+        xc = tr.rand((2,) + tuple(grid.shape), dtype=dt, device=gpu, generator=g)
+        a, at, ac = op(x), op.T(y), op(xc)
+        descs = [csr['desc'], op._transposed()['desc']]
+        saved = [(d.loc, d.tab) for d in descs]
+        try:
+            for d in descs:
+                d.loc, d.tab = None, None
+            assert tr.equal(op(x), a)
+            assert tr.equal(op.T(y), at)
+            assert tr.equal(op(xc), ac)
+        finally:
+            for d, (lc, tb) in zip(descs, saved):
+                d.loc, d.tab = lc, tb
+
+
+def test_long_rows_fall_back_to_per_segment_gather(gpu):
+    """Rays of ~3300 segments through 1650 shells: their workgroups exceed the granule table
+    (n_tab = -1) and use the per-segment gather; results against the C oracle's trace + forward."""
+    from oracle import oracle
+    from sph_raytracer_amd import ConeRectGeom, Operator, SphericalGrid, _lib
+    from sph_raytracer_amd.raytracer import find_starts
+    grid = SphericalGrid(shape=(1650, 2, 3))
+    geom = ConeRectGeom((4, 5), pos=(3, 0.01, 0.02), fov=(2, 2))
+    op = Operator(grid, geom, device=gpu)
+    blocks = op._csr['blocks'].cpu().numpy().reshape(-1, _lib.BLOCK_FIELDS)
+    assert (blocks[:, 5] == -1).any()
+    assert op._csr['desc'].n_fallback == int((blocks[:, 5] == -1).sum())
+    x = tr.rand(grid.shape, dtype=tr.float64)
+    got = op(x.to(gpu)).cpu().numpy().reshape(-1)
+    g = oracle.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy())
+    xs = np.broadcast_to(geom.ray_starts.numpy(), geom.rays.shape).reshape(-1, 3).copy()
+    d = geom.rays.numpy().reshape(-1, 3).copy()
+    ptr, vox, seg = oracle.trace_segments(g, xs, d, find_starts(grid, tr.from_numpy(xs)).numpy())
+    assert np.diff(ptr).max() > 3000
+    ref = oracle.forward(ptr, vox, seg, x.numpy(), math.prod(grid.shape))
+    assert np.allclose(got, np.asarray(ref).reshape(-1), rtol=1e-12, atol=1e-12)
+
+
 def test_full_size_trace_vs_oracle_sample(c2, gpu):
     """2000 rays sampled from the full C2 trace, each checked against the C oracle."""
     from oracle import oracle
