@@ -111,18 +111,19 @@ int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64
 /* A traced operator: the CSR above plus
  *   vox     — bit 31 (SPHRT_ROW_HEAD) set on the first segment of every non-empty ray,
  *   row_ray — ray id of every non-empty row, in order,
- *   blocks  — n_blocks x 6 int64 {ray_lo, ray_hi, seg_lo, seg_hi, row_lo, n_tab}: one workgroup
- *             per block owns the whole rows starting in its slice of segments,
- *   tab     — (optional) per block, its n_tab distinct 4-voxel granules (voxel >> 2) ascending
- *             at tab[seg_lo ..),
+ *   empty_ray — the rays without segments, ascending (n_rays entries suffice),
+ *   blocks  — n_blocks x 6 int64 {ray_lo, row_hi, seg_lo, seg_hi, row_lo, n_tab}: block b owns
+ *             the whole rows starting in segments [b*1792, (b+1)*1792),
+ *   tab     — (optional) per block b, its n_tab distinct 4-voxel granules (voxel >> 2) ascending
+ *             at tab[b*1024 ..) (n_blocks * 1024 entries),
  *   loc     — (optional) per segment, 4 * (rank of its granule in the block's table) +
  *             (voxel & 3), with the row-head flag in bit 15 (SPHRT_LOC_HEAD).
- * sphrt_csr_index() fills vox heads, row_ray and blocks from row_ptr (n_tab = -1);
- * n_blocks = sphrt_csr_blocks(n_segments).  sphrt_csr_local() then builds tab/loc (int32 and
- * uint16 arrays of n_segments entries) and sets n_tab for every block of at most 4096 segments
+ * sphrt_csr_index() fills vox heads, row_ray, empty_ray and blocks from row_ptr (n_tab = -1);
+ * n_blocks = sphrt_csr_blocks(n_segments).  sphrt_csr_local() then builds tab and loc (uint16,
+ * n_segments entries) and sets n_tab for every block of at most 4096 segments
  * and 1024 granules; with loc/tab/n_cols set, a static forward on a 16-byte-aligned density
  * stages each block's granules in LDS instead of gathering per segment.
- * Per-segment arrays (vox, len, len32, loc, tab) are read in aligned 8-entry chunks: allocate
+ * Per-segment arrays (vox, len, len32, loc) are read in aligned 8-entry chunks: allocate
  * them to round_up(n_segments, 8) entries (the entries past n_segments are never used).  `len32` is
  * the float32 copy of `len` used by the float32 forward (sphrt_f64_to_f32). */
 #define SPHRT_ROW_HEAD 0x80000000u
@@ -142,12 +143,14 @@ typedef struct sphrt_csr {
     const int32_t *tab;
     int64_t n_cols;        /* column ids (vox & ~head) are < n_cols: voxels, or rays if transposed */
     int64_t n_fallback;    /* blocks without a granule table (n_tab = -1), from sphrt_csr_local */
+    const int32_t *empty_ray;  /* the rays without segments, ascending (n_rays - rows entries) */
 } sphrt_csr;
 
 int64_t sphrt_csr_blocks(int64_t n_segments);
 size_t sphrt_csr_index_workspace_bytes(int64_t n_rays);
 int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_t *row_ray,
-                    int64_t *blocks, int64_t n_blocks, void *workspace, void *stream);
+                    int32_t *empty_ray, int64_t *blocks, int64_t n_blocks, void *workspace,
+                    void *stream);
 /* n_fallback: one device int64, set to the number of blocks left without a table; copy it into
  * csr->n_fallback before the forward (it decides whether a second, per-segment launch runs). */
 int sphrt_csr_local(const sphrt_csr *csr, int64_t *blocks, uint16_t *loc, int32_t *tab,

@@ -7,7 +7,7 @@
 // Layout built once per trace (sphrt_csr_index):
 //   vox[s]     linear voxel index, bit 31 set on the first segment of every non-empty ray
 //   row_ray[k] the ray of the k-th non-empty row
-//   blocks[b]  {ray_lo, ray_hi, seg_lo, seg_hi, row_lo, n_tab}: workgroup b owns the rays whose rows
+//   blocks[b]  {ray_lo, row_hi, seg_lo, seg_hi, row_lo, n_tab}: workgroup b owns the rays whose rows
 //              start in [b*kSegPerBlock, (b+1)*kSegPerBlock) — whole rows, so no row is ever
 //              split between workgroups and the result needs no cross-workgroup combine.
 // Forward per workgroup: each thread streams 8 consecutive segments (aligned vector loads),
@@ -24,7 +24,7 @@ constexpr int kPer = 8;                         // segments per thread per pass
 constexpr int kPass = kThreads * kPer;          // 2048 segments per pass
 constexpr int64_t kSegPerBlock = 1792;          // row starts per workgroup (leaves room for the
                                                 // last row's overhang inside one pass)
-constexpr int kBlockFields = 6;                 // ray_lo, ray_hi, seg_lo, seg_hi, row_lo, n_tab
+constexpr int kBlockFields = 6;                 // ray_lo, row_hi, seg_lo, seg_hi, row_lo, n_tab
 constexpr int kLocalMax = 4096;                 // segments per workgroup with a granule table
 constexpr int kMaxGran = 1024;                  // granules per table (16 KB of f32 in LDS)
 constexpr int kGranEach = kMaxGran / kThreads;
@@ -42,10 +42,11 @@ __global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* row_ptr, 
 
 __global__ __launch_bounds__(256) void row_list_kernel(const int64_t* row_ptr,
                                                        const int64_t* row_pre, int64_t n,
-                                                       int32_t* row_ray) {
+                                                       int32_t* row_ray, int32_t* empty_ray) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= n) return;
     if (row_ptr[r + 1] > row_ptr[r]) row_ray[row_pre[r]] = (int32_t)r;
+    else empty_ray[r - row_pre[r]] = (int32_t)r;
 }
 
 __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
@@ -66,11 +67,11 @@ __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
     const int64_t hi = (b + 1 == nblocks) ? n : first_at_or_after((b + 1) * kSegPerBlock);
     int64_t* m = blocks + kBlockFields * b;
     m[0] = lo;
-    m[1] = hi;
+    m[1] = row_pre[hi];
     m[2] = row_ptr[lo];
     m[3] = row_ptr[hi];
     m[4] = row_pre[lo];
-    m[5] = -1;                                  // no voxel table until sphrt_csr_local
+    m[5] = -1;                                  // no granule table until sphrt_csr_local
 }
 
 // ---- block-level scans (256 threads = 4 waves) -----------------------------------------------
@@ -161,6 +162,64 @@ __device__ __forceinline__ double block_excl_segsum(bool has, double tail, bool&
     return eh ? es : cs + es;
 }
 
+// ---- one-barrier block scans for the forward ------------------------------------------------
+// The wave totals go to one of two LDS slot sets chosen by the caller's pass parity, so the slots
+// a scan reads are rewritten two scans later at the earliest, after barriers every thread has
+// passed: no trailing barrier.  `lds_barrier` waits for LDS traffic only, so global loads issued
+// before it (row prefetches, per-segment gathers) stay in flight across it.
+struct FwdShared {
+    int cnt[2][4];
+    int has[2][4];
+    double sum[2][4];
+};
+
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <bool kDrain>   // kDrain: a full barrier (also retires LDS-DMA granule loads)
+__device__ __forceinline__ int block_excl_count1(int v, int& total, int (&cnt)[4]) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int inc = wave_incl_sum(v);
+    if (lane == 63) cnt[wid] = inc;
+    if (kDrain) __syncthreads();
+    else lds_barrier();
+    int base = 0;
+    for (int w = 0; w < wid; ++w) base += cnt[w];
+    total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+    return base + inc - v;
+}
+
+__device__ __forceinline__ double block_excl_segsum1(bool has, double tail, bool& tot_has,
+                                                     double& tot_sum, int (&hs)[4],
+                                                     double (&sm)[4]) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int h = has ? 1 : 0;
+    double s = tail;
+    seg_step<kShr1>(h, s);
+    seg_step<kShr2>(h, s);
+    seg_step<kShr4>(h, s);
+    seg_step<kShr8>(h, s);
+    seg_step<kBcast15, 0xa>(h, s);
+    seg_step<kBcast31, 0xc>(h, s);
+    const int eh = dpp0<kWaveShr1>(h);
+    const double es = dpp0<kWaveShr1>(s);
+    if (lane == 63) {
+        hs[wid] = h;
+        sm[wid] = s;
+    }
+    lds_barrier();
+    double cs = 0.0;
+    for (int w = 0; w < wid; ++w) cs = hs[w] ? sm[w] : cs + sm[w];
+    tot_has = false;
+    tot_sum = 0.0;
+    for (int w = 0; w < 4; ++w) {
+        tot_sum = hs[w] ? sm[w] : tot_sum + sm[w];
+        tot_has = tot_has || hs[w];
+    }
+    return eh ? es : cs + es;
+}
+
 // Per-segment arrays are readable up to the next multiple of 8 entries (sphrt.h), so every chunk
 // that starts before s1 is one aligned 32-byte (vox) / 32- or 64-byte (len) vector load; entries
 // outside [s0, s1) are masked to zero.  Pointers are pass-relative, offsets 32-bit.
@@ -215,8 +274,8 @@ __device__ __forceinline__ void load8(const int32_t* __restrict__ vox, const L* 
 // ---- per-workgroup granule table ----------------------------------------------------------
 // Per-segment density gathers are the forward's bottleneck: every segment is one divergent 4-byte
 // lane access, and the load path's per-lane rate, not bytes, bounds the kernel (C2: ~7 of 13 us).
-// Built once per trace: for every workgroup, the sorted distinct 4-voxel granules its segments
-// read (tab[s0 .. s0+n_tab), granule g = voxels 4g..4g+3) and, per segment, the slot
+// Built once per trace: for every workgroup b, the sorted distinct 4-voxel granules its segments
+// read (tab[b*kMaxGran ..+n_tab), granule g = voxels 4g..4g+3) and, per segment, the slot
 // 4*rank + (voxel & 3) of its voxel, with the row-head flag in bit 15 (loc).  The forward stages
 // the granules into LDS with 16-byte LDS-DMA loads (one lane per granule, ~3x fewer lane accesses
 // than segments) and the segments read LDS.  n_tab = -1 marks a workgroup left on the
@@ -290,7 +349,7 @@ __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restri
         const uint64_t k = key[i];
         if (i == 0 || gran(k) != gran(key[i - 1])) {
             ++rank;
-            tab[s0 + rank] = (int32_t)gran(k);
+            tab[(int64_t)blockIdx.x * kMaxGran + rank] = (int32_t)gran(k);
         }
         const int pos = (int)((k >> 1) & 0xfff);
         const int slot = 4 * rank + (int)((k >> 13) & 3);
@@ -308,13 +367,23 @@ __device__ __forceinline__ int dens_index(uint32_t slot) {
     else return (int)(((slot & 2u) ? 2 * kMaxGran : 0) + ((slot >> 2) << 1) + (slot & 1u));
 }
 
+// The volume's last granule may be partial (only the table's last entry can be): copied lane by
+// lane, out of line so its addressing does not stay live in the caller.
+template <typename T>
+__device__ __noinline__ void stage_partial_granule(const T* __restrict__ rho, int64_t v0,
+                                                   int64_t n_cols, int j, T* dens) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dens[dens_index<T>(4 * j + i)] = v0 + i < n_cols ? rho[v0 + i] : (T)0;
+}
+
 template <typename T>
 __device__ __forceinline__ void stage_granules(const T* __restrict__ rho, const int32_t (&ti)[kGranEach],
                                                int n_tab, int64_t n_cols, T* dens) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
     for (int q = 0; q < kGranEach; ++q) {
-        const int j0 = q * kThreads + w * 64;   // this wave's 64 granules of round q
+        const int j0 = q * kThreads + w * 64;   // this wave's 64 granules of round q (uniform)
         const int j = j0 + lane;
         if (j >= n_tab) continue;
         const int64_t v0 = 4 * (int64_t)ti[q];
@@ -328,10 +397,8 @@ __device__ __forceinline__ void stage_granules(const T* __restrict__ rho, const 
                 __builtin_amdgcn_global_load_lds((const void*)(rho + v0 + 2),
                     (__attribute__((address_space(3))) void*)(dens + 2 * kMaxGran + 2 * j0), 16, 0, 0);
             }
-        } else {                                 // the volume's last, partial granule
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                dens[dens_index<T>(4 * j + i)] = v0 + i < n_cols ? rho[v0 + i] : (T)0;
+        } else {
+            stage_partial_granule<T>(rho, v0, n_cols, j, dens);
         }
     }
 }
@@ -372,82 +439,85 @@ __device__ __forceinline__ void load8_loc(const uint16_t* __restrict__ loc,
 //   kFwdDynamic  ray i reads channel i / div
 enum FwdMode { kFwdTable = 0, kFwdGather = 1, kFwdDynamic = 2 };
 
+#ifndef SPHRT_FWD_MIN_BLOCKS
+#define SPHRT_FWD_MIN_BLOCKS 6   // 6 resident workgroups per CU: <= 80 VGPRs
+#endif
 template <typename T, typename L, int MODE>
-__global__ __launch_bounds__(kThreads) void forward_kernel(
-    const int64_t* __restrict__ blocks, const int64_t* __restrict__ row_ptr,
-    const int32_t* __restrict__ vox, const uint16_t* __restrict__ loc,
-    const int32_t* __restrict__ tab, const L* __restrict__ len,
-    const int32_t* __restrict__ row_ray, const T* __restrict__ density, int64_t n_chan,
-    int64_t cs, int64_t div, T* __restrict__ out, int64_t ocs, int64_t n_rays, int64_t n_cols,
-    int fallback_only) {
-    __shared__ ScanShared sh;
+__global__ __launch_bounds__(kThreads, SPHRT_FWD_MIN_BLOCKS) void forward_kernel(
+    const int64_t* __restrict__ blocks, const int32_t* __restrict__ vox,
+    const uint16_t* __restrict__ loc, const int32_t* __restrict__ tab, const L* __restrict__ len,
+    const int32_t* __restrict__ row_ray, const int32_t* __restrict__ empty_ray,
+    const T* __restrict__ density, int64_t n_chan, int64_t cs, int64_t div, T* __restrict__ out,
+    int64_t ocs, int64_t n_rays, int64_t n_seg, int64_t n_cols, int fallback_only) {
+    __shared__ FwdShared sh;
     __shared__ __attribute__((aligned(16))) T dens[4 * kMaxGran];
-    const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
-    const int64_t s0 = m[2], k0 = m[4], n_tab = m[5];
-    int64_t s1 = m[3];
+    constexpr bool local = MODE == kFwdTable;
+    int par = 0;                                    // scan slot parity
     const int tid = threadIdx.x;
     const int o = tid * kPer;                       // this thread's chunk within a pass
     const int64_t nc = MODE == kFwdDynamic ? 1 : n_chan;
-    const int64_t a0 = s0 & ~(int64_t)(kPer - 1);   // passes start 8-aligned
-    constexpr bool local = MODE == kFwdTable;
+    // Everything addressed by the workgroup index alone goes out before the block record
+    // arrives: the first pass (rows of block b start in [b*kSegPerBlock, (b+1)*kSegPerBlock),
+    // so its first pass is [b*kSegPerBlock, +kPass)) and the granule table (fixed stride).
+    const int64_t base0 = (int64_t)blockIdx.x * kSegPerBlock;
+    uint32_t v[kPer];
+    L l[kPer];
+    int32_t ti[kGranEach];
+    const int n_here = (int)min<int64_t>(n_seg - base0, (int64_t)kPass + 1);
+    if (local) load8_loc(loc + base0, len + base0, o, 0, n_here, v, l);
+    else load8(vox + base0, len + base0, o, 0, n_here, v, l);
+    const int32_t* tab_b = tab + (int64_t)blockIdx.x * kMaxGran;
+    if (local) {
+#pragma unroll
+        for (int q = 0; q < kGranEach; ++q) ti[q] = tab_b[tid + q * kThreads];
+    }
+    const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
+    const int64_t s0 = m[2], k0 = m[4], n_tab = m[5];
+    int64_t s1 = m[3];
     if (MODE == kFwdTable && n_tab < 0) s1 = s0;      // left to the kFwdGather fallback launch
     if (MODE == kFwdGather && fallback_only && n_tab >= 0) return;
+    // Empty rays integrate to zero: the list of them is split evenly over the workgroups.
+    if (!fallback_only) {
+        const int64_t n_rows = blocks[kBlockFields * (int64_t)(gridDim.x - 1) + 1];
+        const int64_t n_empty = n_rays - n_rows;
+        const int64_t e_chunk = (n_empty + gridDim.x - 1) / gridDim.x;
+        const int64_t e_lo = min<int64_t>((int64_t)blockIdx.x * e_chunk, n_empty);
+        const int e_n = (int)(min<int64_t>(e_lo + e_chunk, n_empty) - e_lo);
+        for (int j = tid; j < e_n; j += kThreads) {
+            const int64_t r = empty_ray[e_lo + j];
+            for (int64_t c = 0; c < nc; ++c) out[c * ocs + r] = (T)0;
+        }
+    }
+    if (s0 >= s1) return;
     // pass-relative segment window [lo, hi) of this workgroup (32-bit lane arithmetic)
     auto window = [&](int64_t base, int& lo, int& hi) {
         lo = (int)max<int64_t>(s0 - base, -1);
         hi = (int)min<int64_t>(s1 - base, (int64_t)kPass + 1);
     };
-    auto load_pass = [&](int64_t base, uint32_t (&v)[kPer], L (&l)[kPer]) {
+    {
         int lo, hi;
-        window(base, lo, hi);
-        if (local) load8_loc(loc + base, len + base, o, lo, hi, v, l);
-        else load8(vox + base, len + base, o, lo, hi, v, l);
-    };
-    uint32_t v[kPer];
-    L l[kPer];
-    int32_t ti[kGranEach];
-    if (s0 < s1) {
-        load_pass(a0, v, l);
-        if (local) {
-#pragma unroll
-            for (int q = 0; q < kGranEach; ++q) {
-                const int j = tid + q * kThreads;
-                ti[q] = j < n_tab ? tab[s0 + j] : 0;
-            }
-        }
+        window(base0, lo, hi);
+        mask8(o, lo, hi, v, l);
     }
-    // Empty rays integrate to zero.  They are split evenly over the workgroups, independently of
-    // the segment partition (a block whose rows start late may own thousands of empty rays).
-    // Their row_ptr loads go out with the segment loads and are retired right away.
-    if (!fallback_only) {
-        const int64_t e_chunk = (n_rays + gridDim.x - 1) / gridDim.x;
-        const int64_t e_lo = min<int64_t>((int64_t)blockIdx.x * e_chunk, n_rays);
-        const int e_n = (int)(min<int64_t>(e_lo + e_chunk, n_rays) - e_lo);
-        const int64_t* rp = row_ptr + e_lo;
-        for (int r = tid; r < e_n; r += kThreads)
-            if (rp[r + 1] == rp[r])
-                for (int64_t c = 0; c < nc; ++c) out[c * ocs + e_lo + r] = (T)0;
-    }
-    if (s0 >= s1) return;
     for (int64_t c = 0; c < nc; ++c) {
         const T* rho = density + c * cs;
         T* oc = out + c * ocs;
         if (local) {
             if (c > 0) {
 #pragma unroll
-                for (int q = 0; q < kGranEach; ++q) {
-                    const int j = tid + q * kThreads;
-                    ti[q] = j < n_tab ? tab[s0 + j] : 0;
-                }
+                for (int q = 0; q < kGranEach; ++q) ti[q] = tab_b[tid + q * kThreads];
             }
             stage_granules<T>(rho, ti, (int)n_tab, n_cols, dens);
         }
         double carry = 0.0;                 // open run entering the pass
-        const int32_t* rows = row_ray + k0;   // rows of heads seen in earlier passes skipped below
-        for (int64_t base = a0; base < s1; base += kPass) {
-            if (base != a0 || c != 0) load_pass(base, v, l);
+        const int32_t* rows = row_ray + k0;   // advanced past the heads of earlier passes
+        for (int64_t base = base0; base < s1; base += kPass) {
             int lo, hi;
             window(base, lo, hi);
+            if (base != base0 || c != 0) {
+                if (local) load8_loc(loc + base, len + base, o, lo, hi, v, l);
+                else load8(vox + base, len + base, o, lo, hi, v, l);
+            }
             int hcount = 0;
 #pragma unroll
             for (int k = 0; k < kPer; ++k) hcount += (v[k] & kHead) ? 1 : 0;
@@ -458,8 +528,14 @@ __global__ __launch_bounds__(kThreads) void forward_kernel(
                     rv[k] = l[k] != (L)0 ? rho[v[k] & ~kHead] : (T)0;
             }
             int pass_heads;
-            const int hb = block_excl_count(hcount, pass_heads, sh);   // barrier: dens ready
+            // (table mode: the full barrier also retires the granule LDS-DMA)
+            const int hb = block_excl_count1<local>(hcount, pass_heads, sh.cnt[par]);
             pass_heads = __builtin_amdgcn_readfirstlane(pass_heads);
+            // rows this thread closes: rows[hb-1] (the run open at its start) and rows[hb] (its
+            // first own row) are fetched now, under the segmented scan; more are rare
+            const bool has_prev = hb > 0 || base != base0;
+            const int32_t r_prev = has_prev ? rows[hb - 1] : 0;
+            const int32_t r_first = hcount > 0 ? rows[hb] : 0;
             if (local) {
 #pragma unroll
                 for (int k = 0; k < kPer; ++k)
@@ -472,7 +548,8 @@ __global__ __launch_bounds__(kThreads) void forward_kernel(
                     rank += (v[k] & kHead) ? 1 : 0;
                     T x = (T)0;
                     if (l[k] != (L)0) {
-                        const int64_t ray = rows[hb + rank - 1];
+                        const int64_t ray = rank == 0 ? r_prev : rank == 1 ? r_first
+                                                                         : rows[hb + rank - 1];
                         x = density[(ray / div) * cs + (v[k] & ~kHead)];
                     }
                     rv[k] = x;
@@ -491,24 +568,28 @@ __global__ __launch_bounds__(kThreads) void forward_kernel(
             }
             bool tot_has;
             double tot_sum;
-            const double ex = block_excl_segsum(has, tail, tot_has, tot_sum, sh);
+            const double ex = block_excl_segsum1(has, tail, tot_has, tot_sum, sh.has[par],
+                                                 sh.sum[par]);
+            par ^= 1;
             // the run open at this thread's start: the segmented prefix of the earlier threads,
             // plus the carry of earlier passes when no earlier thread of this pass saw a head
             double run = hb > 0 ? ex : carry + ex;
-            int seen = hb - 1;
+            int seen = -1;                            // own heads passed so far, minus one
             const int first = lo - o, end = hi - o;   // chunk-relative window
-            const bool opens = base != a0;            // a head at the window start closes a row
             const bool closes = base + kPass >= s1;   // the window end closes the last row
+            auto row_of = [&](int i) -> int64_t {     // ray of the row after i own heads
+                return i < 0 ? r_prev : i == 0 ? r_first : rows[hb + i];
+            };
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 if (k < first || k >= end) continue;
                 if (v[k] & kHead) {
-                    if (k > first || opens) oc[rows[seen]] = (T)run;   // close the previous row
+                    if (k > first || base != base0) oc[row_of(seen)] = (T)run;   // close a row
                     run = 0.0;
                     ++seen;
                 }
                 run += (double)rv[k] * (double)l[k];
-                if (k == end - 1 && closes) oc[rows[seen]] = (T)run;   // last row
+                if (k == end - 1 && closes) oc[row_of(seen)] = (T)run;   // the last row
             }
             carry = tot_has ? tot_sum : carry + tot_sum;
             rows += pass_heads;
@@ -577,7 +658,8 @@ extern "C" size_t sphrt_csr_index_workspace_bytes(int64_t n_rays) {
 }
 
 extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* vox,
-                               int32_t* row_ray, int64_t* blocks, int64_t n_blocks,
+                               int32_t* row_ray, int32_t* empty_ray, int64_t* blocks,
+                               int64_t n_blocks,
                                void* workspace, void* stream) {
     if (n_rays < 0 || n_blocks < 1) return fail("bad CSR index sizes");
     if (n_rays == 0) return 0;
@@ -590,7 +672,8 @@ extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* 
     hipLaunchKernelGGL(mark_rows_kernel, dim3(g), dim3(256), 0, st, row_ptr, n_rays, vox, flags);
     if (int e = check_launch("mark_rows")) return e;
     if (int e = sphrt_scan_counts(flags, n_rays, pre, scan_ws, stream)) return e;
-    hipLaunchKernelGGL(row_list_kernel, dim3(g), dim3(256), 0, st, row_ptr, pre, n_rays, row_ray);
+    hipLaunchKernelGGL(row_list_kernel, dim3(g), dim3(256), 0, st, row_ptr, pre, n_rays, row_ray,
+                       empty_ray);
     if (int e = check_launch("row_list")) return e;
     hipLaunchKernelGGL(block_meta_kernel, dim3((unsigned)((n_blocks + 255) / 256)), dim3(256), 0,
                        st, row_ptr, pre, n_rays, n_blocks, blocks);
@@ -612,7 +695,8 @@ extern "C" int sphrt_csr_local(const sphrt_csr* c, int64_t* blocks, uint16_t* lo
 }
 
 static int check_csr(const sphrt_csr* c, int64_t n_chan, int64_t div) {
-    if (!c || !c->row_ptr || !c->vox || !c->row_ray || !c->blocks) return fail("incomplete CSR");
+    if (!c || !c->row_ptr || !c->vox || !c->row_ray || !c->empty_ray || !c->blocks)
+        return fail("incomplete CSR");
     if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
     if (n_chan < 1) return fail("n_chan must be >= 1");
     if (div > 0 && n_chan != 1) return fail("ray_chan_div requires n_chan == 1");
@@ -635,8 +719,8 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
                           int64_t chan_stride, int64_t div, T* out, int64_t ocs, void* stream) {
     const dim3 grid((unsigned)c->n_blocks), block(kThreads);
     hipStream_t st = (hipStream_t)stream;
-#define SPHRT_FWD_ARGS c->blocks, c->row_ptr, c->vox, c->loc, c->tab, len, c->row_ray, density, \
-                       n_chan, chan_stride, div, out, ocs, c->n_rays, c->n_cols
+#define SPHRT_FWD_ARGS c->blocks, c->vox, c->loc, c->tab, len, c->row_ray, c->empty_ray, density, \
+                       n_chan, chan_stride, div, out, ocs, c->n_rays, c->n_segments, c->n_cols
     if (div > 0) {
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic>), grid, block, 0, st, SPHRT_FWD_ARGS, 0);
     } else if (use_tables(c, density, n_chan, chan_stride, div)) {

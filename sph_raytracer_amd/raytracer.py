@@ -235,10 +235,10 @@ def _seg_alloc(total):
     return max((total + 7) // 8 * 8, 8)
 
 
-def _local_tables(lib, desc, blocks, total, dev, stream):
+def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
     """Per-workgroup granule tables of a CSR (sphrt_csr_local); sets desc.loc/.tab."""
     loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
-    tab = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+    tab = tr.empty(nblocks * _lib.TABLE_STRIDE, dtype=tr.int32, device=dev)
     n_fallback = tr.empty(1, dtype=tr.int64, device=dev)
     _lib.check(lib.sphrt_csr_local(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(tab),
                                    _lib.ptr(n_fallback), stream), 'sphrt_csr_local')
@@ -354,20 +354,23 @@ class Operator:
         # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
         nblocks = lib.sphrt_csr_blocks(total)
         row_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
+        empty_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
         blocks = tr.empty(_lib.BLOCK_FIELDS * nblocks, dtype=tr.int64, device=dev)
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(row_ptr), n, _lib.ptr(vox), _lib.ptr(row_ray),
-                                       _lib.ptr(blocks), nblocks, _lib.ptr(iws), stream),
-                   'sphrt_csr_index')
+                                       _lib.ptr(empty_ray), _lib.ptr(blocks), nblocks,
+                                       _lib.ptr(iws), stream), 'sphrt_csr_index')
         del iws
         c = _lib.CSR()
         c.n_rays, c.n_segments, c.n_blocks = n, total, nblocks
         c.row_ptr, c.vox, c.len = row_ptr.data_ptr(), vox.data_ptr(), seg_len.data_ptr()
         c.row_ray, c.blocks, c.len32 = row_ray.data_ptr(), blocks.data_ptr(), None
+        c.empty_ray = empty_ray.data_ptr()
         c.n_cols = math.prod(self.grid.shape[-3:])
-        loc, tab = _local_tables(lib, c, blocks, total, dev, stream)
-        self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, row_ray=row_ray, blocks=blocks,
-                         loc=loc, tab=tab, nblocks=nblocks, n=n, total=total, desc=c)
+        loc, tab = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
+        self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, row_ray=row_ray,
+                         empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, nblocks=nblocks,
+                         n=n, total=total, desc=c)
         self._batch = batch
 
     # -- shape logic of raytracer.py:703-712 -----------------------------------------------------
@@ -447,11 +450,12 @@ class Operator:
         del ws
         nblocks = lib.sphrt_csr_blocks(total)
         vox_list = tr.empty(n_vox, dtype=tr.int32, device=dev)
+        empty_vox = tr.empty(n_vox, dtype=tr.int32, device=dev)
         blocks = tr.empty(_lib.BLOCK_FIELDS * nblocks, dtype=tr.int64, device=dev)
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n_vox), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(col_ptr), n_vox, _lib.ptr(t_ray),
-                                       _lib.ptr(vox_list), _lib.ptr(blocks), nblocks,
-                                       _lib.ptr(iws), stream), 'sphrt_csr_index(T)')
+                                       _lib.ptr(vox_list), _lib.ptr(empty_vox), _lib.ptr(blocks),
+                                       nblocks, _lib.ptr(iws), stream), 'sphrt_csr_index(T)')
         t_len32 = tr.empty(t_len.shape, dtype=tr.float32, device=dev)
         _lib.check(lib.sphrt_f64_to_f32(_lib.ptr(t_len), _lib.ptr(t_len32), t_len.numel(), stream),
                    'sphrt_f64_to_f32')
@@ -460,9 +464,11 @@ class Operator:
         c.row_ptr, c.vox, c.len, c.len32 = (col_ptr.data_ptr(), t_ray.data_ptr(),
                                             t_len.data_ptr(), t_len32.data_ptr())
         c.row_ray, c.blocks = vox_list.data_ptr(), blocks.data_ptr()
+        c.empty_ray = empty_vox.data_ptr()
         c.n_cols = csr['n']
-        loc, tab = _local_tables(lib, c, blocks, total, dev, stream)
-        csr['T'] = dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, blocks, loc, tab))
+        loc, tab = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
+        csr['T'] = dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, empty_vox, blocks,
+                                      loc, tab))
         return csr['T']
 
     def _apply_adjoint(self, y, dshape, ddtype, ddevice):

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(kThreads) void table_ablate(const int64_t* __restri
 #pragma unroll
     for (int q = 0; q < kGranEach; ++q) {
         const int j = tid + q * kThreads;
-        ti[q] = j < n_tab ? tab[s0 + j] : 0;
+        ti[q] = j < n_tab ? tab[(int64_t)blockIdx.x * kMaxGran + j] : 0;
     }
     if constexpr (MODE == 12) {
         stage_granules<float>(rho, ti, (int)n_tab, 1 << 30, dens);
