@@ -15,6 +15,7 @@ Differences from the reference, by design:
 - forward sums accumulate in float64 and round once to the density dtype;
 - the caller's ``geom.rays`` tensor is never normalised in place.
 """
+import ctypes
 import math
 
 import torch as tr
@@ -229,6 +230,13 @@ def _layout_for(grid, ray_shape, shape):
     return math.prod(lead), 0, lead + R
 
 
+try:   # the current HIP stream as an int without building a torch Stream object (~0.3 vs 1.9 us)
+    _raw_stream = tr._C._cuda_getCurrentRawStream
+except AttributeError:   # pragma: no cover - older torch
+    def _raw_stream(index):
+        return tr.cuda.current_stream(index).cuda_stream
+
+
 def _seg_alloc(total):
     """Per-segment arrays are allocated to a multiple of 8 entries (the apply kernels read whole
     aligned 8-segment chunks; entries past the total are masked, never used)."""
@@ -318,6 +326,7 @@ class Operator:
         if invalid:
             raise NotImplementedError('invalid=True (keep invalid segments) is not supported')
         self._csr = None
+        self._fast = {}     # (shape, dtype, device) -> bound forward launch (steady-state calls)
         # 'transpose': deterministic voxel-major adjoint (default); 'atomic': float64 atomics
         # (used anyway when views are paired with time slices)
         self.adjoint_mode = 'transpose'
@@ -383,6 +392,17 @@ class Operator:
         (T, H, W) for a dynamic one (raytracer.py:692-713).  Differentiable in ``density``."""
         if self._csr is None:
             raise RuntimeError('Operator was built with _compute=False')
+        if type(density) is tr.Tensor and not (density.requires_grad and tr.is_grad_enabled()):
+            # steady-state fast path: a density already on the compute device, in a dtype and
+            # shape seen before -> one allocation and one C call
+            ent = self._fast.get((density.shape, density.dtype, density.device))
+            if ent is not None and density.is_contiguous():
+                fn, desc, n_chan, n_vox, div, n, alloc, shape = ent
+                out = tr.empty(alloc, dtype=density.dtype, device=density.device)
+                st = _raw_stream(density.device.index)
+                if fn(desc, density.data_ptr(), n_chan, n_vox, div, out.data_ptr(), n, st):
+                    _lib.check(-1, 'sphrt_forward')
+                return out.view(shape)
         density = tr.as_tensor(density)
         if density.requires_grad and tr.is_grad_enabled():
             return _LineIntegral.apply(density, self)
@@ -422,8 +442,15 @@ class Operator:
         if d.device != dev or d.dtype != cdt or not d.is_contiguous():
             d = d.to(device=dev, dtype=cdt).contiguous()
         n = self._csr['n']
-        out = tr.empty((n_chan, n) if div == 0 else (n,), dtype=cdt, device=dev)
+        alloc = (n_chan, n) if div == 0 else (n,)
+        out = tr.empty(alloc, dtype=cdt, device=dev)
         self._launch_forward(d, out, n_chan, div)
+        if density.device == dev and density.dtype == cdt and density.is_contiguous():
+            lib = _lib.load()
+            fn = lib.sphrt_forward_f32 if cdt == tr.float32 else lib.sphrt_forward_f64
+            self._fast[(density.shape, density.dtype, density.device)] = (
+                fn, ctypes.byref(self._csr['desc']), n_chan, math.prod(self.grid.shape[-3:]), div,
+                n, alloc, tuple(out_shape))
         out = out.view(out_shape)
         if out.device != density.device or cdt != in_dtype:
             out = out.to(device=density.device, dtype=in_dtype)
