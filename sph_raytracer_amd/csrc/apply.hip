@@ -7,7 +7,7 @@
 // Layout built once per trace (sphrt_csr_index):
 //   vox[s]     linear voxel index, bit 31 set on the first segment of every non-empty ray
 //   row_ray[k] the ray of the k-th non-empty row
-//   blocks[b]  {ray_lo, row_hi, seg_lo, seg_hi, row_lo, n_tab}: workgroup b owns the rays whose rows
+//   blocks[b]  {empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab}: workgroup b owns the rays whose rows
 //              start in [b*kSegPerBlock, (b+1)*kSegPerBlock) — whole rows, so no row is ever
 //              split between workgroups and the result needs no cross-workgroup combine.
 // Forward per workgroup: each thread streams 8 consecutive segments (aligned vector loads),
@@ -24,7 +24,7 @@ constexpr int kPer = 8;                         // segments per thread per pass
 constexpr int kPass = kThreads * kPer;          // 2048 segments per pass
 constexpr int64_t kSegPerBlock = 1792;          // row starts per workgroup (leaves room for the
                                                 // last row's overhang inside one pass)
-constexpr int kBlockFields = 6;                 // ray_lo, row_hi, seg_lo, seg_hi, row_lo, n_tab
+constexpr int kBlockFields = 6;                 // empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab
 constexpr int kLocalMax = 4096;                 // segments per workgroup with a granule table
 constexpr int kMaxGran = 1024;                  // granules per table (16 KB of f32 in LDS)
 constexpr int kGranEach = kMaxGran / kThreads;
@@ -66,8 +66,11 @@ __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
     const int64_t lo = first_at_or_after(b * kSegPerBlock);
     const int64_t hi = (b + 1 == nblocks) ? n : first_at_or_after((b + 1) * kSegPerBlock);
     int64_t* m = blocks + kBlockFields * b;
-    m[0] = lo;
-    m[1] = row_pre[hi];
+    // this block's share of the empty-ray list (split evenly, independent of the segments)
+    const int64_t n_empty = n - row_pre[n];
+    const int64_t e_chunk = (n_empty + nblocks - 1) / nblocks;
+    m[0] = min<int64_t>(b * e_chunk, n_empty);
+    m[1] = min<int64_t>((b + 1) * e_chunk, n_empty);
     m[2] = row_ptr[lo];
     m[3] = row_ptr[hi];
     m[4] = row_pre[lo];
@@ -478,11 +481,8 @@ __global__ __launch_bounds__(kThreads, SPHRT_FWD_MIN_BLOCKS) void forward_kernel
     if (MODE == kFwdGather && fallback_only && n_tab >= 0) return;
     // Empty rays integrate to zero: the list of them is split evenly over the workgroups.
     if (!fallback_only) {
-        const int64_t n_rows = blocks[kBlockFields * (int64_t)(gridDim.x - 1) + 1];
-        const int64_t n_empty = n_rays - n_rows;
-        const int64_t e_chunk = (n_empty + gridDim.x - 1) / gridDim.x;
-        const int64_t e_lo = min<int64_t>((int64_t)blockIdx.x * e_chunk, n_empty);
-        const int e_n = (int)(min<int64_t>(e_lo + e_chunk, n_empty) - e_lo);
+        const int64_t e_lo = m[0];
+        const int e_n = (int)(m[1] - e_lo);
         for (int j = tid; j < e_n; j += kThreads) {
             const int64_t r = empty_ray[e_lo + j];
             for (int64_t c = 0; c < nc; ++c) out[c * ocs + r] = (T)0;

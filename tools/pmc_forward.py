@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""rocprofv3 PMC passes over the bare float32 forward (tools/prof_forward.py --only) and the
+per-launch numbers the bench roofline uses.  Runs rocprofv3 as a child process (this driver never
+touches the GPU itself); one counter group per pass (MI355X_MICROARCH.md § rocprofv3 PMC slots).
+
+    python tools/pmc_forward.py --out profiles/r01_forward_c2_pmc.json [--config c2]
+
+HBM traffic per launch = 2 * FETCH_SIZE + WRITE_SIZE (KB = 1024 B): gfx950 FETCH_SIZE counts half
+the bytes of wide streaming reads (MI355X_MICROARCH.md § HBM); WRITE_SIZE is exact.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PASSES = [
+    ['FETCH_SIZE'],
+    ['WRITE_SIZE'],
+    ['SQ_WAVES', 'SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_INSTS_LDS', 'SQ_INSTS_VMEM_RD',
+     'SQ_INSTS_VMEM_WR', 'SQ_WAVE_CYCLES', 'SQ_BUSY_CYCLES'],
+    ['SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY', 'SQ_WAIT_INST_LDS',
+     'GRBM_GUI_ACTIVE'],
+]
+
+
+def run_pass(counters, workdir, config, reps, kernel):
+    d = os.path.join(workdir, '_'.join(c.lower() for c in counters[:2]))
+    shutil.rmtree(d, ignore_errors=True)
+    cmd = ['rocprofv3', '--pmc', *counters, '-d', d, '-o', 'pmc', '--output-format', 'csv', '--',
+           sys.executable, os.path.join(ROOT, 'tools', 'prof_forward.py'), '--only', '--reps',
+           str(reps), '--config', config]
+    subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.DEVNULL)
+    files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
+    if not files:
+        raise RuntimeError(f'no counter_collection.csv under {d}')
+    vals = {}
+    disp = {}
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if kernel not in row['Kernel_Name']:
+                continue
+            name = row['Counter_Name']
+            vals.setdefault(name, []).append(float(row['Counter_Value']))
+            disp.setdefault(name, set()).add(row['Dispatch_Id'])
+    return {k: sum(v) / len(disp[k]) for k, v in vals.items()}, {k: len(v) for k, v in disp.items()}, files
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--out', required=True)
+    ap.add_argument('--config', default='c2')
+    ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--kernel', default='forward_kernel<float, float, 0>')
+    ap.add_argument('--workdir', default=os.path.join(ROOT, 'gpurun_out', 'pmc'))
+    args = ap.parse_args()
+    per_launch, dispatches, raw = {}, {}, []
+    for counters in PASSES:
+        v, n, files = run_pass(counters, args.workdir, args.config, args.reps, args.kernel)
+        per_launch.update(v)
+        dispatches.update(n)
+        raw += files
+    rec = {
+        'kernel': args.kernel, 'config': args.config, 'dispatches': dispatches,
+        'per_launch': per_launch,
+        'correction': 'MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of wide streaming reads on '
+                      'gfx950 -> doubled; WRITE_SIZE exact; KB = 1024 B; one counter group per pass',
+        'traffic_bytes_per_launch': (2 * per_launch['FETCH_SIZE'] + per_launch['WRITE_SIZE']) * 1024,
+        'commands': [f'rocprofv3 --pmc {" ".join(c)} -d ... -- python tools/prof_forward.py --only '
+                     f'--reps {args.reps} --config {args.config}' for c in PASSES],
+    }
+    os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
+    with open(args.out, 'w') as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec))
+
+
+if __name__ == '__main__':
+    main()
