@@ -116,14 +116,14 @@ int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64
  *             owns the whole rows starting in segments [b*1792, (b+1)*1792) and zeroes the empty
  *             rays empty_ray[empty_lo .. empty_hi),
  *   tab     — (optional) per block b, its n_tab distinct 4-voxel granules (voxel >> 2) ascending
- *             at tab[b*1024 ..) (n_blocks * 1024 entries),
+ *             at tab[b*tab_stride ..) (n_blocks * tab_stride entries),
  *   loc     — (optional) per segment, 4 * (rank of its granule in the block's table) +
  *             (voxel & 3), with the row-head flag in bit 15 (SPHRT_LOC_HEAD).
  * sphrt_csr_index() fills vox heads, row_ray, empty_ray and blocks from row_ptr (n_tab = -1);
- * n_blocks = sphrt_csr_blocks(n_segments).  sphrt_csr_local() then builds tab and loc (uint16,
- * n_segments entries) and sets n_tab for every block of at most 4096 segments
- * and 1024 granules; with loc/tab/n_cols set, a static forward on a 16-byte-aligned density
- * stages each block's granules in LDS instead of gathering per segment.
+ * n_blocks = sphrt_csr_blocks(n_segments).  sphrt_csr_local_count/_fill then build tab and loc
+ * (uint16, n_segments entries) for every block of at most 4096 segments and 2048 granules; with
+ * loc/tab/n_cols/tab_stride set, a static forward on a 16-byte-aligned density stages each
+ * block's granules in LDS (4 * tab_stride elements, up to 48 KB) instead of gathering per segment.
  * Per-segment arrays (vox, len, len32, loc) are read in aligned 8-entry chunks: allocate
  * them to round_up(n_segments, 8) entries (the entries past n_segments are never used).  `len32` is
  * the float32 copy of `len` used by the float32 forward (sphrt_f64_to_f32). */
@@ -145,6 +145,7 @@ typedef struct sphrt_csr {
     int64_t n_cols;        /* column ids (vox & ~head) are < n_cols: voxels, or rays if transposed */
     int64_t n_fallback;    /* blocks without a granule table (n_tab = -1), from sphrt_csr_local */
     const int32_t *empty_ray;  /* the rays without segments, ascending (n_rays - rows entries) */
+    int64_t tab_stride;    /* granule-table entries per block (>= the largest n_tab) */
 } sphrt_csr;
 
 int64_t sphrt_csr_blocks(int64_t n_segments);
@@ -152,10 +153,13 @@ size_t sphrt_csr_index_workspace_bytes(int64_t n_rays);
 int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_t *row_ray,
                     int32_t *empty_ray, int64_t *blocks, int64_t n_blocks, void *workspace,
                     void *stream);
-/* n_fallback: one device int64, set to the number of blocks left without a table; copy it into
- * csr->n_fallback before the forward (it decides whether a second, per-segment launch runs). */
-int sphrt_csr_local(const sphrt_csr *csr, int64_t *blocks, uint16_t *loc, int32_t *tab,
-                    int64_t *n_fallback, void *stream);
+/* Granule tables in two passes.  _count sets n_tab in blocks (-1: no table) and writes two
+ * device int64 to stats: {blocks without a table, largest n_tab}; the caller copies the first to
+ * csr->n_fallback, picks tab_stride >= the second (csr->tab_stride; tab holds n_blocks *
+ * tab_stride entries) and runs _fill. */
+int sphrt_csr_local_count(const sphrt_csr *csr, int64_t *blocks, int64_t *stats, void *stream);
+int sphrt_csr_local_fill(const sphrt_csr *csr, const int64_t *blocks, uint16_t *loc, int32_t *tab,
+                         int64_t tab_stride, void *stream);
 
 /* ---- forward line integral on the CSR (replaces Operator.__call__, raytracer.py:692-713) -- */
 /* out[c*out_chan_stride + i] = sum_s density[c*chan_stride + vox[s]] * len[s] over ray i's row.

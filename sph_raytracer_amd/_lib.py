@@ -38,13 +38,12 @@ class CSR(ctypes.Structure):
     _fields_ = [('n_rays', c_i64), ('n_segments', c_i64), ('row_ptr', c_vp), ('vox', c_vp),
                 ('len', c_vp), ('len32', c_vp), ('row_ray', c_vp), ('blocks', c_vp),
                 ('n_blocks', c_i64), ('loc', c_vp), ('tab', c_vp), ('n_cols', c_i64),
-                ('n_fallback', c_i64), ('empty_ray', c_vp)]
+                ('n_fallback', c_i64), ('empty_ray', c_vp), ('tab_stride', c_i64)]
 
 
 ROW_HEAD = 0x80000000
 BLOCK_FIELDS = 6           # SPHRT_BLOCK_FIELDS
 LOC_HEAD = 0x8000          # SPHRT_LOC_HEAD
-TABLE_STRIDE = 1024        # granule-table entries per block
 
 # (name, restype, argtypes) — mirrors include/sphrt.h one to one
 _SIGNATURES = [
@@ -64,7 +63,8 @@ _SIGNATURES = [
     ('sphrt_csr_blocks', c_i64, [c_i64]),
     ('sphrt_csr_index_workspace_bytes', ctypes.c_size_t, [c_i64]),
     ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
-    ('sphrt_csr_local', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ('sphrt_csr_local_count', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp]),
+    ('sphrt_csr_local_fill', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp]),
     ('sphrt_forward_f32', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,
                                   c_vp]),
     ('sphrt_forward_f64', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,

@@ -26,8 +26,8 @@ constexpr int64_t kSegPerBlock = 1792;          // row starts per workgroup (lea
                                                 // last row's overhang inside one pass)
 constexpr int kBlockFields = 6;                 // empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab
 constexpr int kLocalMax = 4096;                 // segments per workgroup with a granule table
-constexpr int kMaxGran = 1024;                  // granules per table (16 KB of f32 in LDS)
-constexpr int kGranEach = kMaxGran / kThreads;
+constexpr int kMaxGran = 2048;                  // granules per table (sphrt_csr_local)
+constexpr int kGranEarly = 4;                   // table chunks of 256 fetched before the record
 
 // ---- index --------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* row_ptr, int64_t n,
@@ -278,26 +278,29 @@ __device__ __forceinline__ void load8(const int32_t* __restrict__ vox, const L* 
 // Per-segment density gathers are the forward's bottleneck: every segment is one divergent 4-byte
 // lane access, and the load path's per-lane rate, not bytes, bounds the kernel (C2: ~7 of 13 us).
 // Built once per trace: for every workgroup b, the sorted distinct 4-voxel granules its segments
-// read (tab[b*kMaxGran ..+n_tab), granule g = voxels 4g..4g+3) and, per segment, the slot
+// read (tab[b*tab_stride ..+n_tab), granule g = voxels 4g..4g+3) and, per segment, the slot
 // 4*rank + (voxel & 3) of its voxel, with the row-head flag in bit 15 (loc).  The forward stages
 // the granules into LDS with 16-byte LDS-DMA loads (one lane per granule, ~3x fewer lane accesses
 // than segments) and the segments read LDS.  n_tab = -1 marks a workgroup left on the
 // per-segment gather (more than kLocalMax segments or kMaxGran granules).
+template <bool FILL>
 __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restrict__ blocks,
                                                                const int32_t* __restrict__ vox,
                                                                uint16_t* __restrict__ loc,
                                                                int32_t* __restrict__ tab,
-                                                               unsigned long long* n_fallback) {
+                                                               int64_t tab_stride,
+                                                               unsigned long long* stats) {
     __shared__ uint64_t key[kLocalMax];
     __shared__ ScanShared sh;
     int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
     const int64_t s0 = m[2], s1 = m[3];
+    if (FILL && m[5] < 0) return;
     const int n = (int)min<int64_t>(s1 - s0, (int64_t)kLocalMax + 1);
     const int tid = threadIdx.x;
     if (n > kLocalMax) {
         if (tid == 0) {
             m[5] = -1;
-            atomicAdd(n_fallback, 1ull);
+            atomicAdd(stats, 1ull);
         }
         return;
     }
@@ -338,10 +341,15 @@ __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restri
     }
     int n_tab;
     int rank = block_excl_count(first_new, n_tab, sh) - 1;
-    if (n_tab > kMaxGran) {
+    if (!FILL) {                               // pass 1: table sizes, fallbacks, largest table
         if (tid == 0) {
-            m[5] = -1;
-            atomicAdd(n_fallback, 1ull);
+            if (n_tab > kMaxGran) {
+                m[5] = -1;
+                atomicAdd(stats, 1ull);
+            } else {
+                m[5] = n_tab;
+                atomicMax(stats + 1, (unsigned long long)n_tab);
+            }
         }
         return;
     }
@@ -352,57 +360,68 @@ __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restri
         const uint64_t k = key[i];
         if (i == 0 || gran(k) != gran(key[i - 1])) {
             ++rank;
-            tab[(int64_t)blockIdx.x * kMaxGran + rank] = (int32_t)gran(k);
+            tab[(int64_t)blockIdx.x * tab_stride + rank] = (int32_t)gran(k);
         }
         const int pos = (int)((k >> 1) & 0xfff);
         const int slot = 4 * rank + (int)((k >> 13) & 3);
         loc[s0 + pos] = (uint16_t)(slot | ((k & 1) ? 0x8000 : 0));
     }
-    if (tid == 0) m[5] = n_tab;
 }
 
-// LDS image of the staged granules.  float: granule j at dens[4j .. 4j+3].  double (32-byte
-// granules, two 16-byte DMA halves): voxels 0-1 of granule j at dens[2j ..], voxels 2-3 at
-// dens[2*kMaxGran + 2j ..].
+// LDS image of the staged granules (capacity `cap` granules = the table stride).  float: granule
+// j at dens[4j .. 4j+3].  double (32-byte granules, two 16-byte DMA halves): voxels 0-1 of
+// granule j at dens[2j ..], voxels 2-3 at dens[2*cap + 2j ..].
 template <typename T>
-__device__ __forceinline__ int dens_index(uint32_t slot) {
+__device__ __forceinline__ int dens_index(uint32_t slot, int cap) {
     if constexpr (sizeof(T) == 4) return (int)slot;
-    else return (int)(((slot & 2u) ? 2 * kMaxGran : 0) + ((slot >> 2) << 1) + (slot & 1u));
+    else return (int)(((slot & 2u) ? 2 * cap : 0) + ((slot >> 2) << 1) + (slot & 1u));
 }
 
 // The volume's last granule may be partial (only the table's last entry can be): copied lane by
 // lane, out of line so its addressing does not stay live in the caller.
 template <typename T>
 __device__ __noinline__ void stage_partial_granule(const T* __restrict__ rho, int64_t v0,
-                                                   int64_t n_cols, int j, T* dens) {
+                                                   int64_t n_cols, int j, int cap, T* dens) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dens[dens_index<T>(4 * j + i)] = v0 + i < n_cols ? rho[v0 + i] : (T)0;
+    for (int i = 0; i < 4; ++i)
+        dens[dens_index<T>(4 * j + i, cap)] = v0 + i < n_cols ? rho[v0 + i] : (T)0;
 }
 
 template <typename T>
-__device__ __forceinline__ void stage_granules(const T* __restrict__ rho, const int32_t (&ti)[kGranEach],
-                                               int n_tab, int64_t n_cols, T* dens) {
+__device__ __forceinline__ void stage_one(const T* __restrict__ rho, int64_t g, int j, int j0,
+                                          int64_t n_cols, int cap, T* dens) {
+    const int64_t v0 = 4 * g;
+    if (v0 + 4 <= n_cols) {
+        if constexpr (sizeof(T) == 4) {
+            __builtin_amdgcn_global_load_lds((const void*)(rho + v0),
+                (__attribute__((address_space(3))) void*)(dens + 4 * j0), 16, 0, 0);
+        } else {
+            __builtin_amdgcn_global_load_lds((const void*)(rho + v0),
+                (__attribute__((address_space(3))) void*)(dens + 2 * j0), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(rho + v0 + 2),
+                (__attribute__((address_space(3))) void*)(dens + 2 * cap + 2 * j0), 16, 0, 0);
+        }
+    } else {
+        stage_partial_granule<T>(rho, v0, n_cols, j, cap, dens);
+    }
+}
+
+// Granules [0, kGranEarly*256) come from the table entries fetched early (ti); any beyond that
+// (large tables) are fetched here, one 256-chunk per round.
+template <typename T>
+__device__ __forceinline__ void stage_granules(const T* __restrict__ rho, const int32_t (&ti)[kGranEarly],
+                                               const int32_t* __restrict__ tab_b, int n_tab,
+                                               int64_t n_cols, int cap, T* dens) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #pragma unroll
-    for (int q = 0; q < kGranEach; ++q) {
+    for (int q = 0; q < kGranEarly; ++q) {
         const int j0 = q * kThreads + w * 64;   // this wave's 64 granules of round q (uniform)
-        const int j = j0 + lane;
-        if (j >= n_tab) continue;
-        const int64_t v0 = 4 * (int64_t)ti[q];
-        if (v0 + 4 <= n_cols) {
-            if constexpr (sizeof(T) == 4) {
-                __builtin_amdgcn_global_load_lds((const void*)(rho + v0),
-                    (__attribute__((address_space(3))) void*)(dens + 4 * j0), 16, 0, 0);
-            } else {
-                __builtin_amdgcn_global_load_lds((const void*)(rho + v0),
-                    (__attribute__((address_space(3))) void*)(dens + 2 * j0), 16, 0, 0);
-                __builtin_amdgcn_global_load_lds((const void*)(rho + v0 + 2),
-                    (__attribute__((address_space(3))) void*)(dens + 2 * kMaxGran + 2 * j0), 16, 0, 0);
-            }
-        } else {
-            stage_partial_granule<T>(rho, v0, n_cols, j, dens);
-        }
+        if (j0 + lane < n_tab) stage_one<T>(rho, ti[q], j0 + lane, j0, n_cols, cap, dens);
+    }
+    for (int q = kGranEarly; q * kThreads < n_tab; ++q) {
+        const int j0 = q * kThreads + w * 64;
+        if (j0 + lane < n_tab) stage_one<T>(rho, tab_b[j0 + lane], j0 + lane, j0, n_cols, cap, dens);
     }
 }
 
@@ -442,18 +461,22 @@ __device__ __forceinline__ void load8_loc(const uint16_t* __restrict__ loc,
 //   kFwdDynamic  ray i reads channel i / div
 enum FwdMode { kFwdTable = 0, kFwdGather = 1, kFwdDynamic = 2 };
 
-#ifndef SPHRT_FWD_MIN_BLOCKS
-#define SPHRT_FWD_MIN_BLOCKS 6   // 6 resident workgroups per CU: <= 80 VGPRs
-#endif
+// Resident workgroups per CU the register allocation aims for: 6 (<= 80 VGPRs) lets a C2-sized
+// launch (~1500 workgroups) be resident at once; the float64 table mode stops at 5 (no spills).
+template <typename T, int MODE>
+constexpr int fwd_min_blocks() { return sizeof(T) == 8 && MODE == 0 ? 5 : 6; }
+
 template <typename T, typename L, int MODE>
-__global__ __launch_bounds__(kThreads, SPHRT_FWD_MIN_BLOCKS) void forward_kernel(
+__global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward_kernel(
     const int64_t* __restrict__ blocks, const int32_t* __restrict__ vox,
     const uint16_t* __restrict__ loc, const int32_t* __restrict__ tab, const L* __restrict__ len,
     const int32_t* __restrict__ row_ray, const int32_t* __restrict__ empty_ray,
     const T* __restrict__ density, int64_t n_chan, int64_t cs, int64_t div, T* __restrict__ out,
-    int64_t ocs, int64_t n_rays, int64_t n_seg, int64_t n_cols, int fallback_only) {
+    int64_t ocs, int64_t n_rays, int64_t n_seg, int64_t n_cols, int64_t tab_stride,
+    int fallback_only) {
     __shared__ FwdShared sh;
-    __shared__ __attribute__((aligned(16))) T dens[4 * kMaxGran];
+    extern __shared__ __attribute__((aligned(16))) unsigned char fwd_dyn_lds[];
+    T* dens = reinterpret_cast<T*>(fwd_dyn_lds);   // 4 * tab_stride entries (table mode)
     constexpr bool local = MODE == kFwdTable;
     int par = 0;                                    // scan slot parity
     const int tid = threadIdx.x;
@@ -465,14 +488,16 @@ __global__ __launch_bounds__(kThreads, SPHRT_FWD_MIN_BLOCKS) void forward_kernel
     const int64_t base0 = (int64_t)blockIdx.x * kSegPerBlock;
     uint32_t v[kPer];
     L l[kPer];
-    int32_t ti[kGranEach];
+    int32_t ti[kGranEarly];
     const int n_here = (int)min<int64_t>(n_seg - base0, (int64_t)kPass + 1);
     if (local) load8_loc(loc + base0, len + base0, o, 0, n_here, v, l);
     else load8(vox + base0, len + base0, o, 0, n_here, v, l);
-    const int32_t* tab_b = tab + (int64_t)blockIdx.x * kMaxGran;
+    const int32_t* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
+    const int cap = (int)tab_stride;
     if (local) {
 #pragma unroll
-        for (int q = 0; q < kGranEach; ++q) ti[q] = tab_b[tid + q * kThreads];
+        for (int q = 0; q < kGranEarly; ++q)
+            ti[q] = q * kThreads < cap ? tab_b[tid + q * kThreads] : 0;
     }
     const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
     const int64_t s0 = m[2], k0 = m[4], n_tab = m[5];
@@ -505,9 +530,10 @@ __global__ __launch_bounds__(kThreads, SPHRT_FWD_MIN_BLOCKS) void forward_kernel
         if (local) {
             if (c > 0) {
 #pragma unroll
-                for (int q = 0; q < kGranEach; ++q) ti[q] = tab_b[tid + q * kThreads];
+                for (int q = 0; q < kGranEarly; ++q)
+                    ti[q] = q * kThreads < cap ? tab_b[tid + q * kThreads] : 0;
             }
-            stage_granules<T>(rho, ti, (int)n_tab, n_cols, dens);
+            stage_granules<T>(rho, ti, tab_b, (int)n_tab, n_cols, cap, dens);
         }
         double carry = 0.0;                 // open run entering the pass
         const int32_t* rows = row_ray + k0;   // advanced past the heads of earlier passes
@@ -539,7 +565,7 @@ __global__ __launch_bounds__(kThreads, SPHRT_FWD_MIN_BLOCKS) void forward_kernel
             if (local) {
 #pragma unroll
                 for (int k = 0; k < kPer; ++k)
-                    rv[k] = l[k] != (L)0 ? dens[dens_index<T>(v[k] & ~kHead)] : (T)0;
+                    rv[k] = l[k] != (L)0 ? dens[dens_index<T>(v[k] & ~kHead, cap)] : (T)0;
             }
             if (MODE == kFwdDynamic) {      // time slice of each segment's ray
                 int rank = 0;
@@ -680,18 +706,29 @@ extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* 
     return check_launch("block_meta");
 }
 
-extern "C" int sphrt_csr_local(const sphrt_csr* c, int64_t* blocks, uint16_t* loc, int32_t* tab,
-                               int64_t* n_fallback, void* stream) {
-    if (!c || !c->vox || !blocks || !loc || !tab || !n_fallback)
-        return fail("incomplete CSR for the granule tables");
+extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_t* stats,
+                                     void* stream) {
+    if (!c || !c->vox || !blocks || !stats) return fail("incomplete CSR for the granule tables");
     if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
     hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(n_fallback, 0, sizeof(int64_t), st) != hipSuccess)
+    if (hipMemsetAsync(stats, 0, 2 * sizeof(int64_t), st) != hipSuccess)
         return fail("hipMemsetAsync failed");
     if (c->n_segments == 0) return 0;
-    hipLaunchKernelGGL(local_table_kernel, dim3((unsigned)c->n_blocks), dim3(kThreads), 0, st,
-                       blocks, c->vox, loc, tab, (unsigned long long*)n_fallback);
-    return check_launch("local_table_kernel");
+    hipLaunchKernelGGL(local_table_kernel<false>, dim3((unsigned)c->n_blocks), dim3(kThreads), 0,
+                       st, blocks, c->vox, nullptr, nullptr, 0, (unsigned long long*)stats);
+    return check_launch("local_table_kernel<count>");
+}
+
+extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, uint16_t* loc,
+                                    int32_t* tab, int64_t tab_stride, void* stream) {
+    if (!c || !c->vox || !blocks || !loc || !tab) return fail("incomplete CSR for the granule tables");
+    if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
+    if (tab_stride < 1 || tab_stride > kMaxGran) return fail("bad granule table stride");
+    if (c->n_segments == 0) return 0;
+    hipLaunchKernelGGL(local_table_kernel<true>, dim3((unsigned)c->n_blocks), dim3(kThreads), 0,
+                       (hipStream_t)stream, (int64_t*)blocks, c->vox, loc, tab, tab_stride,
+                       nullptr);
+    return check_launch("local_table_kernel<fill>");
 }
 
 static int check_csr(const sphrt_csr* c, int64_t n_chan, int64_t div) {
@@ -705,10 +742,13 @@ static int check_csr(const sphrt_csr* c, int64_t n_chan, int64_t div) {
 
 // The granule tables apply to static channels whose granules are 16-byte (float) / 32-byte
 // (double) aligned; anything else takes the per-segment gather through vox.
+constexpr size_t kTableLdsMax = 48 * 1024;   // dynamic LDS for the staged granules, per workgroup
+
 template <typename T>
 static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int64_t chan_stride,
                        int64_t div) {
     if (!c->loc || !c->tab || c->n_cols <= 0 || div > 0) return false;
+    if (c->tab_stride < 1 || (size_t)c->tab_stride * 4 * sizeof(T) > kTableLdsMax) return false;
     if ((uintptr_t)density % (4 * sizeof(T)) != 0) return false;
     if (n_chan > 1 && chan_stride % 4 != 0) return false;
     return true;
@@ -720,11 +760,13 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
     const dim3 grid((unsigned)c->n_blocks), block(kThreads);
     hipStream_t st = (hipStream_t)stream;
 #define SPHRT_FWD_ARGS c->blocks, c->vox, c->loc, c->tab, len, c->row_ray, c->empty_ray, density, \
-                       n_chan, chan_stride, div, out, ocs, c->n_rays, c->n_segments, c->n_cols
+                       n_chan, chan_stride, div, out, ocs, c->n_rays, c->n_segments, c->n_cols, \
+                       c->tab_stride
     if (div > 0) {
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic>), grid, block, 0, st, SPHRT_FWD_ARGS, 0);
     } else if (use_tables(c, density, n_chan, chan_stride, div)) {
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable>), grid, block, 0, st, SPHRT_FWD_ARGS, 0);
+        const size_t lds = (size_t)c->tab_stride * 4 * sizeof(T);
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable>), grid, block, lds, st, SPHRT_FWD_ARGS, 0);
         if (c->n_fallback > 0) {
             if (int e = check_launch("forward_kernel<table>")) return e;
             hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather>), grid, block, 0, st, SPHRT_FWD_ARGS, 1);

@@ -244,13 +244,18 @@ def _seg_alloc(total):
 
 
 def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
-    """Per-workgroup granule tables of a CSR (sphrt_csr_local); sets desc.loc/.tab."""
+    """Per-workgroup granule tables of a CSR (sphrt_csr_local_count/_fill); sets desc.loc/.tab/
+    .tab_stride/.n_fallback.  One host sync (the largest table decides the stride)."""
+    stats = tr.empty(2, dtype=tr.int64, device=dev)
+    _lib.check(lib.sphrt_csr_local_count(desc, _lib.ptr(blocks), _lib.ptr(stats), stream),
+               'sphrt_csr_local_count')
+    n_fallback, max_tab = stats.tolist()
+    stride = max(64, (max_tab + 63) // 64 * 64)
     loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
-    tab = tr.empty(nblocks * _lib.TABLE_STRIDE, dtype=tr.int32, device=dev)
-    n_fallback = tr.empty(1, dtype=tr.int64, device=dev)
-    _lib.check(lib.sphrt_csr_local(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(tab),
-                                   _lib.ptr(n_fallback), stream), 'sphrt_csr_local')
-    desc.n_fallback = int(n_fallback.item())
+    tab = tr.empty(nblocks * stride, dtype=tr.int32, device=dev)
+    _lib.check(lib.sphrt_csr_local_fill(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(tab),
+                                        stride, stream), 'sphrt_csr_local_fill')
+    desc.n_fallback, desc.tab_stride = n_fallback, stride
     desc.loc, desc.tab = loc.data_ptr(), tab.data_ptr()
     return loc, tab
 

@@ -87,7 +87,8 @@ __global__ __launch_bounds__(kThreads) void table_ablate(const int64_t* __restri
                                                          const int32_t* __restrict__ tab,
                                                          const float* __restrict__ len,
                                                          const float* __restrict__ rho,
-                                                         float* __restrict__ sink) {
+                                                         float* __restrict__ sink,
+                                                         int64_t stride) {
     __shared__ __attribute__((aligned(16))) float dens[4 * kMaxGran];
     const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
     const int64_t s0 = m[2], s1 = m[3], n_tab = m[5];
@@ -98,17 +99,18 @@ __global__ __launch_bounds__(kThreads) void table_ablate(const int64_t* __restri
     float l[kPer];
     load8_loc(loc + base, len + base, tid * kPer, (int)(s0 - base),
               (int)min<int64_t>(s1 - base, (int64_t)kPass + 1), v, l);
-    int32_t ti[kGranEach];
+    const int32_t* tab_b = tab + (int64_t)blockIdx.x * stride;
+    int32_t ti[kGranEarly];
 #pragma unroll
-    for (int q = 0; q < kGranEach; ++q) {
+    for (int q = 0; q < kGranEarly; ++q) {
         const int j = tid + q * kThreads;
-        ti[q] = j < n_tab ? tab[(int64_t)blockIdx.x * kMaxGran + j] : 0;
+        ti[q] = j < n_tab ? tab_b[j] : 0;
     }
     if constexpr (MODE == 12) {
-        stage_granules<float>(rho, ti, (int)n_tab, 1 << 30, dens);
+        stage_granules<float>(rho, ti, tab_b, (int)n_tab, 1 << 30, (int)stride, dens);
     } else if constexpr (MODE == 13) {
 #pragma unroll
-        for (int q = 0; q < kGranEach; ++q) {
+        for (int q = 0; q < kGranEarly; ++q) {
             const int j = tid + q * kThreads;
             if (j < n_tab)
                 reinterpret_cast<float4*>(dens)[j] = reinterpret_cast<const float4*>(rho)[ti[q]];
@@ -116,7 +118,7 @@ __global__ __launch_bounds__(kThreads) void table_ablate(const int64_t* __restri
     } else {
         int acc = 0;
 #pragma unroll
-        for (int q = 0; q < kGranEach; ++q) acc += ti[q];
+        for (int q = 0; q < kGranEarly; ++q) acc += ti[q];
         if (acc == 0x7fffffff) dens[tid] = 1.f;
     }
     __syncthreads();
@@ -143,9 +145,9 @@ extern "C" int sphrt_ablate(int stage, const sphrt_csr* c, const float* rho, flo
         case 9: hipLaunchKernelGGL(ablate_kernel<9>, g, b, 0, st, c->blocks, c->vox, c->len32, rho, sink); break;
         case 10: hipLaunchKernelGGL(ablate_kernel<10>, g, b, 0, st, c->blocks, c->vox, c->len32, rho, sink); break;
         case 11: hipLaunchKernelGGL(ablate_kernel<11>, g, b, 0, st, c->blocks, c->vox, c->len32, rho, sink); break;
-        case 12: hipLaunchKernelGGL(table_ablate<12>, g, b, 0, st, c->blocks, c->loc, c->tab, c->len32, rho, sink); break;
-        case 13: hipLaunchKernelGGL(table_ablate<13>, g, b, 0, st, c->blocks, c->loc, c->tab, c->len32, rho, sink); break;
-        case 14: hipLaunchKernelGGL(table_ablate<14>, g, b, 0, st, c->blocks, c->loc, c->tab, c->len32, rho, sink); break;
+        case 12: hipLaunchKernelGGL(table_ablate<12>, g, b, 0, st, c->blocks, c->loc, c->tab, c->len32, rho, sink, c->tab_stride); break;
+        case 13: hipLaunchKernelGGL(table_ablate<13>, g, b, 0, st, c->blocks, c->loc, c->tab, c->len32, rho, sink, c->tab_stride); break;
+        case 14: hipLaunchKernelGGL(table_ablate<14>, g, b, 0, st, c->blocks, c->loc, c->tab, c->len32, rho, sink, c->tab_stride); break;
         default: return 1;
     }
     return hipGetLastError() == hipSuccess ? 0 : 2;
