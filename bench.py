@@ -236,9 +236,9 @@ def main():
     t_host = (time.perf_counter() - t0) / reps_h
 
     k_ms, k_method = kernel_time_ms(op, x)
-    kname = 'forward_kernel<float,float>' if dtype == torch.float32 else 'forward_kernel<double,double>'
+    kname = op._forward_kernel_name(x)
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, 'profiles', 'r01_forward_c2_pmc.json')
+    pmc = os.path.join(ROOT, 'profiles', f'r01_forward_{args.config}_pmc.json')
     if os.path.exists(pmc):     # HBM bytes per launch from the committed rocprofv3 --pmc passes
         rec_pmc = json.load(open(pmc))
         if rec_pmc.get('kernel') == kname and rec_pmc.get('config') == args.config:

@@ -438,6 +438,17 @@ class Operator:
         _lib.check(fn(csr['desc'], _lib.ptr(d), n_chan, math.prod(self.grid.shape[-3:]), div,
                       _lib.ptr(out), csr['n'], _lib.stream_of(self._cdev)), 'sphrt_forward')
 
+    def _forward_kernel_name(self, d):
+        """The forward kernel instantiation a launch on `d` runs (sphrt_forward_*'s choice, for
+        reports): 0 = granule tables staged in LDS, 1 = per-segment gathers, 2 = time slices."""
+        c = self._csr['desc']
+        t = 'float, float' if d.dtype == tr.float32 else 'double, double'
+        n_chan, div, _ = self._layout(d.shape)
+        es = d.element_size()
+        table = (c.loc and div == 0 and 0 < c.tab_stride and c.tab_stride * 4 * es <= 48 * 1024
+                 and d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0))
+        return f'forward_kernel<{t}, {0 if table else (2 if div else 1)}>'
+
     def _apply_forward(self, density):
         dev = self._cdev
         n_chan, div, out_shape = self._layout(density.shape)
