@@ -111,7 +111,7 @@ int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64
 /* A traced operator: the CSR above plus
  *   vox     — bit 31 (SPHRT_ROW_HEAD) set on the first segment of every non-empty ray,
  *   row_ray — ray id of every non-empty row, in order,
- *   empty_ray — the rays without segments, ascending (n_rays entries suffice),
+ *   empty_ray — the rays without segments, ascending (allocate n_rays + 1 entries),
  *   blocks  — n_blocks x 6 int64 {empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab}: block b
  *             owns the whole rows starting in segments [b*1792, (b+1)*1792) and zeroes the empty
  *             rays empty_ray[empty_lo .. empty_hi),

@@ -27,7 +27,20 @@ constexpr int64_t kSegPerBlock = 1792;          // row starts per workgroup (lea
 constexpr int kBlockFields = 6;                 // empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab
 constexpr int kLocalMax = 4096;                 // segments per workgroup with a granule table
 constexpr int kMaxGran = 2048;                  // granules per table (sphrt_csr_local)
-constexpr int kGranEarly = 4;                   // table chunks of 256 fetched before the record
+constexpr int kGranEarly = 3;                   // table chunks of 256 fetched before the record
+
+// Diagnostic build only (-DSPHRT_FWD_STAMPS, tools/fwd_timeline.py): s_memrealtime (100 MHz)
+// stamps of wave 0 of every forward workgroup at its phase boundaries.
+#ifdef SPHRT_FWD_STAMPS
+__device__ unsigned long long g_fwd_stamps[1 << 20];
+#define FWD_STAMP(i)                                                                          \
+    do {                                                                                      \
+        if (threadIdx.x == 0 && blockIdx.x < (1u << 17))                                      \
+            g_fwd_stamps[8 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime();            \
+    } while (0)
+#else
+#define FWD_STAMP(i) do {} while (0)
+#endif
 
 // ---- index --------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* row_ptr, int64_t n,
@@ -377,52 +390,80 @@ __device__ __forceinline__ int dens_index(uint32_t slot, int cap) {
     else return (int)(((slot & 2u) ? 2 * cap : 0) + ((slot >> 2) << 1) + (slot & 1u));
 }
 
-// The volume's last granule may be partial (only the table's last entry can be): copied lane by
-// lane, out of line so its addressing does not stay live in the caller.
+// One granule by LDS-DMA: float, 16 B at dens[4*j0 + 4*lane]; double, two 16-B halves.  `off`
+// is the granule's byte offset in the channel (32-bit: volumes under 4 GiB per channel).
 template <typename T>
-__device__ __noinline__ void stage_partial_granule(const T* __restrict__ rho, int64_t v0,
-                                                   int64_t n_cols, int j, int cap, T* dens) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        dens[dens_index<T>(4 * j + i, cap)] = v0 + i < n_cols ? rho[v0 + i] : (T)0;
+__device__ __forceinline__ void stage_one(const T* __restrict__ rho, uint32_t off, int j0, int cap,
+                                          T* dens) {
+    const char* src = reinterpret_cast<const char*>(rho) + off;
+    if constexpr (sizeof(T) == 4) {
+        __builtin_amdgcn_global_load_lds((const void*)src,
+            (__attribute__((address_space(3))) void*)(dens + 4 * j0), 16, 0, 0);
+    } else {
+        __builtin_amdgcn_global_load_lds((const void*)src,
+            (__attribute__((address_space(3))) void*)(dens + 2 * j0), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(src + 16),
+            (__attribute__((address_space(3))) void*)(dens + 2 * cap + 2 * j0), 16, 0, 0);
+    }
 }
 
+// The volume's last granule, if partial (voxel count not a multiple of 4), can only be the
+// table's last entry: the DMA skips it (no read past the volume) and one lane copies it here.
 template <typename T>
-__device__ __forceinline__ void stage_one(const T* __restrict__ rho, int64_t g, int j, int j0,
-                                          int64_t n_cols, int cap, T* dens) {
-    const int64_t v0 = 4 * g;
-    if (v0 + 4 <= n_cols) {
-        if constexpr (sizeof(T) == 4) {
-            __builtin_amdgcn_global_load_lds((const void*)(rho + v0),
-                (__attribute__((address_space(3))) void*)(dens + 4 * j0), 16, 0, 0);
-        } else {
-            __builtin_amdgcn_global_load_lds((const void*)(rho + v0),
-                (__attribute__((address_space(3))) void*)(dens + 2 * j0), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)(rho + v0 + 2),
-                (__attribute__((address_space(3))) void*)(dens + 2 * cap + 2 * j0), 16, 0, 0);
+__device__ __forceinline__ void stage_partial_tail(const T* __restrict__ rho,
+                                                   const int32_t* __restrict__ tab_b, int n_tab,
+                                                   int64_t n_cols, int cap, T* dens) {
+    if ((n_cols & 3) != 0 && n_tab > 0 && (int)threadIdx.x == (n_tab - 1) % kThreads) {
+        const int j = n_tab - 1;
+        const int64_t v0 = 4 * (int64_t)tab_b[j];
+        if (v0 + 4 > n_cols)
+            for (int i = 0; i < 4; ++i)
+                dens[dens_index<T>(4 * j + i, cap)] = v0 + i < n_cols ? rho[v0 + i] : (T)0;
+    }
+}
+
+// Chunks [q0, ..) of the table, read from memory one 256-chunk per round.
+template <typename T>
+__device__ __forceinline__ void stage_granules_late(const T* __restrict__ rho,
+                                                    const int32_t* __restrict__ tab_b, int q0,
+                                                    int n_tab, int64_t n_cols, int cap, T* dens) {
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t g_full = n_cols >> 2;
+    constexpr int kShift = sizeof(T) == 4 ? 4 : 5;
+    for (int q = q0; q * kThreads < n_tab; ++q) {
+        const int j0 = q * kThreads + w * 64;
+        if (j0 + lane < n_tab) {
+            const int32_t g = tab_b[j0 + lane];
+            if (g < g_full) stage_one<T>(rho, (uint32_t)g << kShift, j0, cap, dens);
         }
-    } else {
-        stage_partial_granule<T>(rho, v0, n_cols, j, cap, dens);
     }
 }
 
 // Granules [0, kGranEarly*256) come from the table entries fetched early (ti); any beyond that
-// (large tables) are fetched here, one 256-chunk per round.
+// (large tables) are fetched here, one 256-chunk per round.  When the volume's voxel count is
+// not a multiple of 4 its last granule is partial: only the table's last entry can be, it is
+// skipped by the DMA (no read past the volume) and copied lane by lane at the end.
 template <typename T>
 __device__ __forceinline__ void stage_granules(const T* __restrict__ rho, const int32_t (&ti)[kGranEarly],
                                                const int32_t* __restrict__ tab_b, int n_tab,
                                                int64_t n_cols, int cap, T* dens) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t g_full = n_cols >> 2;        // granules below this one are whole
+    constexpr int kShift = sizeof(T) == 4 ? 4 : 5;
+    // every early table entry is consumed before the first DMA goes out (one wait, not one per
+    // DMA: the wait-count model serialises VMEM results read after an LDS-DMA)
+    static_assert(kGranEarly == 3, "the register pin below names every early entry");
+    asm volatile("" ::"v"(ti[0]), "v"(ti[1]), "v"(ti[2]));   // one wait for all of them, here
 #pragma unroll
     for (int q = 0; q < kGranEarly; ++q) {
         const int j0 = q * kThreads + w * 64;   // this wave's 64 granules of round q (uniform)
-        if (j0 + lane < n_tab) stage_one<T>(rho, ti[q], j0 + lane, j0, n_cols, cap, dens);
+        if (j0 + lane < n_tab && ti[q] < g_full)
+            stage_one<T>(rho, (uint32_t)ti[q] << kShift, j0, cap, dens);
     }
-    for (int q = kGranEarly; q * kThreads < n_tab; ++q) {
-        const int j0 = q * kThreads + w * 64;
-        if (j0 + lane < n_tab) stage_one<T>(rho, tab_b[j0 + lane], j0 + lane, j0, n_cols, cap, dens);
-    }
+    stage_granules_late<T>(rho, tab_b, kGranEarly, n_tab, n_cols, cap, dens);
+    stage_partial_tail<T>(rho, tab_b, n_tab, n_cols, cap, dens);
 }
 
 template <typename L>
@@ -448,6 +489,54 @@ __device__ __forceinline__ void load8_loc(const uint16_t* __restrict__ loc,
     }
 }
 
+// The first pass's loads, issued before anything is known about the workgroup and decoded
+// later (raw registers keep the compiler from waiting on them early).
+template <typename L, bool LOCAL>
+struct RawChunk {
+    uint4 ix[LOCAL ? 1 : 2];
+    L l[kPer];
+};
+
+template <typename L, bool LOCAL>
+__device__ __forceinline__ void raw_load(const int32_t* __restrict__ vox,
+                                         const uint16_t* __restrict__ loc,
+                                         const L* __restrict__ len, int p0, int s1,
+                                         RawChunk<L, LOCAL>& r) {
+    if (p0 < s1) {
+        if constexpr (LOCAL) {
+            r.ix[0] = *reinterpret_cast<const uint4*>(loc + p0);
+        } else {
+            const uint4* vp = reinterpret_cast<const uint4*>(vox + p0);
+            r.ix[0] = vp[0];
+            r.ix[1] = vp[1];
+        }
+        load_len8(len, p0, r.l);
+    } else {
+        r.ix[0] = make_uint4(0, 0, 0, 0);
+        if constexpr (!LOCAL) r.ix[1] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) r.l[k] = (L)0;
+    }
+}
+
+template <typename L, bool LOCAL>
+__device__ __forceinline__ void decode(const RawChunk<L, LOCAL>& r, uint32_t (&v)[kPer],
+                                       L (&l)[kPer]) {
+    if constexpr (LOCAL) {
+        const uint32_t w[4] = {r.ix[0].x, r.ix[0].y, r.ix[0].z, r.ix[0].w};
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t x = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+            v[k] = (x & 0x7fffu) | ((x & 0x8000u) << 16);
+        }
+    } else {
+        v[0] = r.ix[0].x; v[1] = r.ix[0].y; v[2] = r.ix[0].z; v[3] = r.ix[0].w;
+        v[4] = r.ix[1].x; v[5] = r.ix[1].y; v[6] = r.ix[1].z; v[7] = r.ix[1].w;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) l[k] = r.l[k];
+}
+
 // ---- forward ------------------------------------------------------------------------------
 // Channels: static multichannel -> every ray for every channel c < n_chan; ray_chan_div > 0 ->
 // ray i reads channel i / div (a time slice per view) and writes out[i].
@@ -462,9 +551,12 @@ __device__ __forceinline__ void load8_loc(const uint16_t* __restrict__ loc,
 enum FwdMode { kFwdTable = 0, kFwdGather = 1, kFwdDynamic = 2 };
 
 // Resident workgroups per CU the register allocation aims for: 6 (<= 80 VGPRs) lets a C2-sized
-// launch (~1500 workgroups) be resident at once; the float64 table mode stops at 5 (no spills).
+// launch (~1500 workgroups) be resident at once; float64 stops at 5 (no spills).
 template <typename T, int MODE>
-constexpr int fwd_min_blocks() { return sizeof(T) == 8 && MODE == 0 ? 5 : 6; }
+constexpr int fwd_min_blocks() { return sizeof(T) == 8 ? 5 : 6; }
+
+template <typename T>
+using AccumOf = typename std::conditional<sizeof(T) == 4, float, double>::type;
 
 template <typename T, typename L, int MODE>
 __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward_kernel(
@@ -478,6 +570,7 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
     extern __shared__ __attribute__((aligned(16))) unsigned char fwd_dyn_lds[];
     T* dens = reinterpret_cast<T*>(fwd_dyn_lds);   // 4 * tab_stride entries (table mode)
     constexpr bool local = MODE == kFwdTable;
+    using A = AccumOf<T>;
     int par = 0;                                    // scan slot parity
     const int tid = threadIdx.x;
     const int o = tid * kPer;                       // this thread's chunk within a pass
@@ -485,58 +578,72 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
     // Everything addressed by the workgroup index alone goes out before the block record
     // arrives: the first pass (rows of block b start in [b*kSegPerBlock, (b+1)*kSegPerBlock),
     // so its first pass is [b*kSegPerBlock, +kPass)) and the granule table (fixed stride).
+    FWD_STAMP(0);
     const int64_t base0 = (int64_t)blockIdx.x * kSegPerBlock;
-    uint32_t v[kPer];
-    L l[kPer];
-    int32_t ti[kGranEarly];
     const int n_here = (int)min<int64_t>(n_seg - base0, (int64_t)kPass + 1);
-    if (local) load8_loc(loc + base0, len + base0, o, 0, n_here, v, l);
-    else load8(vox + base0, len + base0, o, 0, n_here, v, l);
+    RawChunk<L, local> raw;
+    raw_load<L, local>(vox + base0, loc + base0, len + base0, o, n_here, raw);
+    // table chunks beyond the stride read the next workgroup's entries (tab is padded by
+    // kGranEarly*kThreads entries); they are never staged (j >= n_tab)
     const int32_t* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
     const int cap = (int)tab_stride;
+    int32_t ti[kGranEarly];
     if (local) {
 #pragma unroll
-        for (int q = 0; q < kGranEarly; ++q)
-            ti[q] = q * kThreads < cap ? tab_b[tid + q * kThreads] : 0;
+        for (int q = 0; q < kGranEarly; ++q) ti[q] = tab_b[tid + q * kThreads];
     }
+    __builtin_amdgcn_sched_barrier(0);
     const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
     const int64_t s0 = m[2], k0 = m[4], n_tab = m[5];
     int64_t s1 = m[3];
     if (MODE == kFwdTable && n_tab < 0) s1 = s0;      // left to the kFwdGather fallback launch
     if (MODE == kFwdGather && fallback_only && n_tab >= 0) return;
-    // Empty rays integrate to zero: the list of them is split evenly over the workgroups.
-    if (!fallback_only) {
-        const int64_t e_lo = m[0];
-        const int e_n = (int)(m[1] - e_lo);
-        for (int j = tid; j < e_n; j += kThreads) {
+    // Empty rays integrate to zero: this workgroup's share of the list is fetched now and
+    // written at the very end, off the critical path.
+    const int64_t e_lo = m[0];
+    const int e_n = fallback_only ? 0 : (int)(m[1] - e_lo);
+    // (unconditional load: empty_ray holds n_rays + 1 entries; a predicated load would make
+    // the wait-count model drain every load before the granule DMA)
+    int32_t r_empty = empty_ray[e_lo + min(tid, max(e_n - 1, 0))];
+    auto zero_empty = [&]() {
+        asm volatile("" : "+v"(r_empty));     // keep every use (and its wait) down here
+        if (tid < e_n)
+            for (int64_t c = 0; c < nc; ++c) out[c * ocs + r_empty] = (T)0;
+        for (int j = tid + kThreads; j < e_n; j += kThreads) {
             const int64_t r = empty_ray[e_lo + j];
             for (int64_t c = 0; c < nc; ++c) out[c * ocs + r] = (T)0;
         }
+    };
+    if (s0 >= s1) {
+        zero_empty();
+        return;
     }
-    if (s0 >= s1) return;
+    if (local) stage_granules<T>(density, ti, tab_b, (int)n_tab, n_cols, cap, dens);
     // pass-relative segment window [lo, hi) of this workgroup (32-bit lane arithmetic)
     auto window = [&](int64_t base, int& lo, int& hi) {
         lo = (int)max<int64_t>(s0 - base, -1);
         hi = (int)min<int64_t>(s1 - base, (int64_t)kPass + 1);
     };
+    uint32_t v[kPer];
+    L l[kPer];
+    decode<L, local>(raw, v, l);
     {
         int lo, hi;
         window(base0, lo, hi);
         mask8(o, lo, hi, v, l);
     }
+    int64_t rbase = 0;                            // rows started in earlier passes
+    FWD_STAMP(1);
     for (int64_t c = 0; c < nc; ++c) {
         const T* rho = density + c * cs;
         T* oc = out + c * ocs;
-        if (local) {
-            if (c > 0) {
-#pragma unroll
-                for (int q = 0; q < kGranEarly; ++q)
-                    ti[q] = q * kThreads < cap ? tab_b[tid + q * kThreads] : 0;
-            }
-            stage_granules<T>(rho, ti, tab_b, (int)n_tab, n_cols, cap, dens);
+        if (local && c > 0) {
+            stage_granules_late<T>(rho, tab_b, 0, (int)n_tab, n_cols, cap, dens);
+            stage_partial_tail<T>(rho, tab_b, (int)n_tab, n_cols, cap, dens);
         }
+        FWD_STAMP(2);
         double carry = 0.0;                 // open run entering the pass
-        const int32_t* rows = row_ray + k0;   // advanced past the heads of earlier passes
+        rbase = 0;
         for (int64_t base = base0; base < s1; base += kPass) {
             int lo, hi;
             window(base, lo, hi);
@@ -544,9 +651,10 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
                 if (local) load8_loc(loc + base, len + base, o, lo, hi, v, l);
                 else load8(vox + base, len + base, o, lo, hi, v, l);
             }
-            int hcount = 0;
+            uint32_t hmask = 0;                 // row heads of this chunk, bit k = segment k
 #pragma unroll
-            for (int k = 0; k < kPer; ++k) hcount += (v[k] & kHead) ? 1 : 0;
+            for (int k = 0; k < kPer; ++k) hmask |= (v[k] >> 31) << k;
+            const int hcount = __builtin_popcount(hmask);
             T rv[kPer];
             if (MODE == kFwdGather) {       // per-segment gathers go out before any scan
 #pragma unroll
@@ -556,12 +664,16 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             int pass_heads;
             // (table mode: the full barrier also retires the granule LDS-DMA)
             const int hb = block_excl_count1<local>(hcount, pass_heads, sh.cnt[par]);
+            FWD_STAMP(3);
             pass_heads = __builtin_amdgcn_readfirstlane(pass_heads);
-            // rows this thread closes: rows[hb-1] (the run open at its start) and rows[hb] (its
-            // first own row) are fetched now, under the segmented scan; more are rare
-            const bool has_prev = hb > 0 || base != base0;
-            const int32_t r_prev = has_prev ? rows[hb - 1] : 0;
-            const int32_t r_first = hcount > 0 ? rows[hb] : 0;
+            // rows this thread closes: the run open at its start (row hb-1) and its first own row
+            // (row hb) are fetched now, under the segmented scan; further ones (rare) at the store
+            const int32_t* rows = row_ray + k0 + rbase + hb;
+            const int32_t r_prev = hb > 0 || base != base0 ? rows[-1] : 0;
+            const int32_t r_first = hcount > 0 ? rows[0] : 0;
+            auto row_of = [&](int i) -> int64_t {     // ray of the row after i own heads
+                return i < 0 ? r_prev : i == 0 ? r_first : rows[i];
+            };
             if (local) {
 #pragma unroll
                 for (int k = 0; k < kPer; ++k)
@@ -571,56 +683,60 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
                 int rank = 0;
 #pragma unroll
                 for (int k = 0; k < kPer; ++k) {
-                    rank += (v[k] & kHead) ? 1 : 0;
+                    rank += (hmask >> k) & 1;
                     T x = (T)0;
                     if (l[k] != (L)0) {
-                        const int64_t ray = rank == 0 ? r_prev : rank == 1 ? r_first
-                                                                         : rows[hb + rank - 1];
+                        const int64_t ray = row_of(rank - 1);
                         x = density[(ray / div) * cs + (v[k] & ~kHead)];
                     }
                     rv[k] = x;
                 }
             }
-            // thread-local runs
-            double tail = 0.0;
-            bool has = false;
+            // Products and thread-local runs in A (float for a float density: the reference's own
+            // precision, 4-cycle VALU ops instead of 8-cycle f64 ones); runs that cross threads are
+            // stitched in double.
+            A p[kPer];
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) p[k] = (A)rv[k] * (A)l[k];
+            A tail = (A)0;
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
-                if (v[k] & kHead) {
-                    has = true;
-                    tail = 0.0;
-                }
-                tail += (double)rv[k] * (double)l[k];
+                if ((hmask >> k) & 1) tail = (A)0;
+                tail += p[k];
             }
             bool tot_has;
             double tot_sum;
-            const double ex = block_excl_segsum1(has, tail, tot_has, tot_sum, sh.has[par],
-                                                 sh.sum[par]);
+            const double ex = block_excl_segsum1(hmask != 0, (double)tail, tot_has, tot_sum,
+                                                 sh.has[par], sh.sum[par]);
             par ^= 1;
+            FWD_STAMP(4);
             // the run open at this thread's start: the segmented prefix of the earlier threads,
             // plus the carry of earlier passes when no earlier thread of this pass saw a head
-            double run = hb > 0 ? ex : carry + ex;
+            const double run0 = hb > 0 ? ex : carry + ex;
+            A lr = (A)0;                              // this thread's part of the current run
+            bool open0 = true;                        // the current run started before this thread
             int seen = -1;                            // own heads passed so far, minus one
             const int first = lo - o, end = hi - o;   // chunk-relative window
             const bool closes = base + kPass >= s1;   // the window end closes the last row
-            auto row_of = [&](int i) -> int64_t {     // ray of the row after i own heads
-                return i < 0 ? r_prev : i == 0 ? r_first : rows[hb + i];
-            };
+            auto value = [&]() { return open0 ? (T)(run0 + (double)lr) : (T)lr; };
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 if (k < first || k >= end) continue;
-                if (v[k] & kHead) {
-                    if (k > first || base != base0) oc[row_of(seen)] = (T)run;   // close a row
-                    run = 0.0;
+                if ((hmask >> k) & 1) {
+                    if (k > first || base != base0) oc[row_of(seen)] = value();   // close a row
+                    lr = (A)0;
+                    open0 = false;
                     ++seen;
                 }
-                run += (double)rv[k] * (double)l[k];
-                if (k == end - 1 && closes) oc[row_of(seen)] = (T)run;   // the last row
+                lr += p[k];
+                if (k == end - 1 && closes) oc[row_of(seen)] = value();   // the last row
             }
             carry = tot_has ? tot_sum : carry + tot_sum;
-            rows += pass_heads;
+            rbase += pass_heads;
         }
     }
+    zero_empty();
+    FWD_STAMP(5);
 }
 
 // ---- adjoint (float64 atomics into a float64 accumulator) -------------------------------------
@@ -705,6 +821,13 @@ extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* 
                        st, row_ptr, pre, n_rays, n_blocks, blocks);
     return check_launch("block_meta");
 }
+
+#ifdef SPHRT_FWD_STAMPS
+extern "C" int sphrt_diag_fwd_stamps(unsigned long long* host, int64_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_stamps), n * sizeof(unsigned long long), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_t* stats,
                                      void* stream) {

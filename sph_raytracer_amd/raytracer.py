@@ -252,7 +252,7 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
     n_fallback, max_tab = stats.tolist()
     stride = max(64, (max_tab + 63) // 64 * 64)
     loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
-    tab = tr.empty(nblocks * stride, dtype=tr.int32, device=dev)
+    tab = tr.empty(nblocks * stride + 3 * 256, dtype=tr.int32, device=dev)   # + early-fetch pad
     _lib.check(lib.sphrt_csr_local_fill(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(tab),
                                         stride, stream), 'sphrt_csr_local_fill')
     desc.n_fallback, desc.tab_stride = n_fallback, stride
@@ -368,7 +368,7 @@ class Operator:
         # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
         nblocks = lib.sphrt_csr_blocks(total)
         row_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
-        empty_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
+        empty_ray = tr.empty(n + 1, dtype=tr.int32, device=dev)
         blocks = tr.empty(_lib.BLOCK_FIELDS * nblocks, dtype=tr.int64, device=dev)
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(row_ptr), n, _lib.ptr(vox), _lib.ptr(row_ray),
@@ -493,7 +493,7 @@ class Operator:
         del ws
         nblocks = lib.sphrt_csr_blocks(total)
         vox_list = tr.empty(n_vox, dtype=tr.int32, device=dev)
-        empty_vox = tr.empty(n_vox, dtype=tr.int32, device=dev)
+        empty_vox = tr.empty(n_vox + 1, dtype=tr.int32, device=dev)
         blocks = tr.empty(_lib.BLOCK_FIELDS * nblocks, dtype=tr.int64, device=dev)
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n_vox), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(col_ptr), n_vox, _lib.ptr(t_ray),
