@@ -31,6 +31,7 @@ namespace sphrt {
 enum { MODE_COUNT = 0, MODE_FILL = 1, MODE_INTEGRATE = 2 };
 constexpr int kNone = 0x7fffffff;  // "no update" in the forward-fill scans
 constexpr int kWavesPerBlock = 4;
+constexpr size_t kLdsBytes = 160 * 1024;        // LDS per CU; one workgroup may take all of it
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -464,13 +465,14 @@ __global__ __launch_bounds__(256, 4) void trace_kernel(GridDev G, RaysDev R, Tra
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
+    const int waves = blockDim.x >> 6;          // 4, or fewer when K needs the LDS (see launch)
     uint64_t* keys = reinterpret_cast<uint64_t*>(smem) + (size_t)wid * cap;
     uint32_t* pays =
-        reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(smem) + (size_t)kWavesPerBlock * cap) +
+        reinterpret_cast<uint32_t*>(reinterpret_cast<uint64_t*>(smem) + (size_t)waves * cap) +
         (size_t)wid * cap;
     const int64_t n_hits = (int64_t)*o.n_hits;
-    for (int64_t h = (int64_t)blockIdx.x * kWavesPerBlock + wid; h < n_hits;
-         h += (int64_t)gridDim.x * kWavesPerBlock) {
+    for (int64_t h = (int64_t)blockIdx.x * waves + wid; h < n_hits;
+         h += (int64_t)gridDim.x * waves) {
         const int64_t ray = o.hits[h];
         double x[3], d[3];
         int s[3];
@@ -631,8 +633,13 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
         return fail("trace workspace too small: %zu < %zu bytes", workspace_size,
                     workspace_bytes(G, R.n));
     const int cap = trace_cap(G);
-    const size_t lds = (size_t)kWavesPerBlock * cap * (sizeof(uint64_t) + sizeof(uint32_t));
-    if (lds > 160 * 1024) return fail("grid too large for the per-wave LDS list (K=%d)", G.K);
+    // one LDS list of K entries per wave: 4 waves per workgroup, fewer for large K (a workgroup
+    // may hold all 160 KiB of a CU's LDS), K <= 13653 with one wave
+    const size_t per_wave = (size_t)cap * (sizeof(uint64_t) + sizeof(uint32_t));
+    int waves = kWavesPerBlock;
+    while (waves > 1 && (size_t)waves * per_wave > kLdsBytes) waves >>= 1;
+    const size_t lds = (size_t)waves * per_wave;
+    if (lds > kLdsBytes) return fail("grid too large for the per-wave LDS list (K=%d > 13653)", G.K);
     unsigned char* ws = (unsigned char*)workspace;
     o.n_deferred = (unsigned long long*)ws;
     o.n_hits = (unsigned*)(ws + 64);
@@ -644,9 +651,9 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
                        st, G, R, o);
     if (int e = check_launch("screen_kernel")) return e;
     // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
-    const int64_t grid = 2048;
-    hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(256), lds, st, G, R, o,
-                       cap);
+    const int64_t grid = 2048 * kWavesPerBlock / waves;
+    hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,
+                       R, o, cap);
     if (int e = check_launch("trace_kernel")) return e;
     hipLaunchKernelGGL((exact_kernel<MODE, T>), dim3(kExactBlocks), dim3(64), 0, st, G, R, o,
                        scratch);

@@ -169,6 +169,29 @@ def test_long_rows_fall_back_to_per_segment_gather(gpu):
     assert np.allclose(got, np.asarray(ref).reshape(-1), rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize('nr', [2500, 6000])
+def test_large_k_trace_vs_oracle(nr, gpu):
+    """K = 2(Nr+1)+... beyond what four per-wave LDS lists fit (K 5013 -> 2 waves per workgroup,
+    K 12013 -> 1): segments and line integrals against the C oracle."""
+    from oracle import oracle
+    from sph_raytracer_amd import ConeRectGeom, Operator, SphericalGrid
+    from sph_raytracer_amd.raytracer import find_starts
+    grid = SphericalGrid(shape=(nr, 2, 3))
+    geom = ConeRectGeom((2, 3), pos=(3, 0.01, 0.02), fov=(2, 2))
+    op = Operator(grid, geom, device=gpu)
+    g = oracle.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy())
+    xs = np.broadcast_to(geom.ray_starts.numpy(), geom.rays.shape).reshape(-1, 3).copy()
+    d = geom.rays.numpy().reshape(-1, 3).copy()
+    ptr, vox, seg = oracle.trace_segments(g, xs, d, find_starts(grid, tr.from_numpy(xs)).numpy())
+    row_ptr, gvox, glen = (t.cpu().numpy() for t in op.segments())
+    msg = gc.compare_segments((ptr, vox, seg), (row_ptr, gvox, glen), scale=1.0, what=f'nr={nr}')
+    assert msg is None, msg
+    x = tr.rand(grid.shape, dtype=tr.float64)
+    ref = np.asarray(oracle.forward(ptr, vox, seg, x.numpy(), math.prod(grid.shape))).reshape(-1)
+    got = op(x.to(gpu)).cpu().numpy().reshape(-1)
+    assert np.allclose(got, ref, rtol=1e-10, atol=1e-12)
+
+
 def test_full_size_trace_vs_oracle_sample(c2, gpu):
     """2000 rays sampled from the full C2 trace, each checked against the C oracle."""
     from oracle import oracle
