@@ -107,6 +107,16 @@ int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64
                      int32_t *vox, double *len, void *workspace, size_t workspace_size,
                      void *stream);
 
+/* ---- on-device cone-beam ray directions (replaces ConeRectGeom.rays, geometry.py:493-508, and
+ * ConeCircGeom.rays, geometry.py:570-582) ----------------------------------------------------- */
+/* rays[v][a][b][0..2] for n_views views of h x w pixels, bit-identical to the torch expressions.
+ * frame: per view {lookdir, lookdir x updir, updir} (9 doubles).  circ == 0 (rect): row[v][a] =
+ * linspace(-ulim, ulim, h), col[v][b] = linspace(-vlim, vlim, w).  circ == 1: row[v][a] = r,
+ * col[v] = {cos(theta) (w values), sin(theta) (w values)}, r*cos and r*sin in double; circ == 2:
+ * the same with r*cos and r*sin rounded to float (the host tensors are float32). */
+int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const double *frame,
+                    const double *row, const double *col, double *rays, void *stream);
+
 /* ---- row index of the trace, built once (the apply kernels' work partition) ---------------- */
 /* A traced operator: the CSR above plus
  *   vox     — bit 31 (SPHRT_ROW_HEAD) set on the first segment of every non-empty ray,

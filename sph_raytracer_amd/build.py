@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 OUT = os.path.join(HERE, 'lib', 'libsphrt.so')
-SOURCES = ['api.hip', 'trace.hip', 'apply.hip', 'transpose.hip']
+SOURCES = ['api.hip', 'trace.hip', 'apply.hip', 'transpose.hip', 'rays.hip']
 HEADERS = ['common.hpp', 'solve.hpp', 'introsort.hpp']
 ARCH = os.environ.get('SPHRT_ARCH', 'gfx950')
 

@@ -1,0 +1,72 @@
+// rays.hip — on-device cone-beam ray directions.
+//
+// Replaces ConeRectGeom.rays (geometry.py:493-508) and ConeCircGeom.rays (geometry.py:570-582)
+// for the trace: the per-pixel directions are generated where they are used instead of being
+// computed by torch on the host and copied over PCIe (24 B per ray).  Bit-identical to the torch
+// CPU expressions: the per-axis values that need transcendental functions (tan of the half field
+// of view through linspace, cos/sin of the polar angle) are computed on the host by the same torch
+// calls and passed in; the per-pixel arithmetic is restated operation by operation in IEEE double
+// (device code is compiled with -ffp-contract=off, fused multiply-adds only where written):
+//   rect: d = (look + right * a_i) + up * b_j
+//   circ: d = (look + (r_i * cos_j) * right) + (r_i * sin_j) * up, the products r_i * cos_j in
+//         the host tensors' precision (float32 by default: torch.linspace of tensor endpoints)
+//   ray  = d / sqrt(fma(d2, d2, fma(d1, d1, d0 * d0)))        (torch.linalg.norm, last axis of 3)
+#include "common.hpp"
+
+namespace sphrt {
+
+__global__ __launch_bounds__(256) void cone_rays_kernel(int64_t n_views, int64_t h, int64_t w,
+                                                        int circ, const double* __restrict__ frame,
+                                                        const double* __restrict__ row,
+                                                        const double* __restrict__ col,
+                                                        double* __restrict__ rays) {
+    const int64_t n = n_views * h * w;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t view = i / (h * w);
+        const int64_t pix = i - view * h * w;
+        const int64_t a = pix / w, b = pix - a * w;
+        const double* f = frame + 9 * view;          // look, right, up
+        double p, q;                                 // coefficients of right and up
+        if (circ == 2) {                             // r, cos, sin are float32 tensors on the host:
+            const float r = (float)row[view * h + a];  // their product is rounded to float32
+            p = (double)(r * (float)col[view * 2 * w + b]);
+            q = (double)(r * (float)col[view * 2 * w + w + b]);
+        } else if (circ) {
+            const double r = row[view * h + a];
+            p = r * col[view * 2 * w + b];           // r_i * cos_j
+            q = r * col[view * 2 * w + w + b];       // r_i * sin_j
+        } else {
+            p = row[view * h + a];
+            q = col[view * w + b];
+        }
+        double d[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double s = f[c] + f[3 + c] * p;
+            d[c] = s + f[6 + c] * q;
+        }
+        const double nrm = __builtin_sqrt(__builtin_fma(d[2], d[2], __builtin_fma(d[1], d[1], d[0] * d[0])));
+        double* o = rays + 3 * i;
+        o[0] = d[0] / nrm;
+        o[1] = d[1] / nrm;
+        o[2] = d[2] / nrm;
+    }
+}
+
+}  // namespace sphrt
+
+using namespace sphrt;
+
+extern "C" int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ,
+                               const double* frame, const double* row, const double* col,
+                               double* rays, void* stream) {
+    if (n_views < 0 || h < 0 || w < 0) return fail("bad detector shape");
+    if (!frame || !row || !col || !rays) return fail("null pointer");
+    const int64_t n = n_views * h * w;
+    if (n == 0) return 0;
+    const int64_t blocks = (n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536;
+    hipLaunchKernelGGL(cone_rays_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       n_views, h, w, circ, frame, row, col, rays);
+    return check_launch("cone_rays_kernel");
+}

@@ -31,6 +31,18 @@ namespace sphrt {
 enum { MODE_COUNT = 0, MODE_FILL = 1, MODE_INTEGRATE = 2 };
 constexpr int kNone = 0x7fffffff;  // "no update" in the forward-fill scans
 constexpr int kWavesPerBlock = 4;
+
+// Diagnostic build only (-DSPHRT_TRACE_STAMPS, tools/trace_phases.py): s_memtime cycles per trace
+// phase summed over all hit rays (0 solve+push, 1 sort, 2 tie check, 3 fill/lengths, 4 emit).
+#ifdef SPHRT_TRACE_STAMPS
+__device__ unsigned long long g_trace_cycles[8];
+#define TRACE_T(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define TRACE_ADD(i, a, b) \
+    do { if (lane == 0) atomicAdd(&g_trace_cycles[i], (unsigned long long)((b) - (a))); } while (0)
+#else
+#define TRACE_T(var) do {} while (0)
+#define TRACE_ADD(i, a, b) do {} while (0)
+#endif
 constexpr size_t kLdsBytes = 160 * 1024;        // LDS per CU; one workgroup may take all of it
 
 __device__ __forceinline__ void wave_sync() {
@@ -264,6 +276,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
                           const int sa, const int64_t ray, uint64_t* keys, uint32_t* pays,
                           const int lane, const TraceOut<T>& o) {
     // ---- 1. crossings -> LDS list (finite, t >= 0), min finite negative distance ----------
+    TRACE_T(ts0);
     int base = 0;
     double tneg = kInf;
     auto note = [&](double t) {
@@ -290,7 +303,10 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         note(ti);
         note(to);
         push(v && keep(ti), ti, j, ri);
-        push(v && keep(to), to, nbr + j, ro);
+        // a double root (tangent sphere, the e = pi/2 "cone") writing the same region twice at
+        // the same distance changes nothing in the forward fill: keep one entry, so the group is
+        // no exact tie (the tie analysis below only runs for real ties)
+        push(v && keep(to) && !(to == ti && ro == ri), to, nbr + j, ro);
     }
     const int ce0 = 2 * nbr;
     for (int j0 = 0; j0 < nbe; j0 += 64) {
@@ -302,7 +318,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         note(ta);
         note(tb);
         push(v && keep(ta), ta, ce0 + j, ra);
-        push(v && keep(tb), tb, ce0 + nbe + j, rb);
+        push(v && keep(tb) && !(tb == ta && rb == ra), tb, ce0 + nbe + j, rb);
     }
     const int ca0 = 2 * nbr + 2 * nbe;
     for (int j0 = 0; j0 < nba; j0 += 64) {
@@ -320,11 +336,15 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     wave_sync();
 
     // ---- 2. sort by (distance, candidate) ------------------------------------------------
+    TRACE_T(ts1);
+    TRACE_ADD(0, ts0, ts1);
     if (F <= 64) sort_regs<1>(keys, pays, F, lane);
     else if (F <= 128) sort_regs<2>(keys, pays, F, lane);
     else if (F <= 256) sort_regs<4>(keys, pays, F, lane);
     else sort_lds(keys, pays, F, lane);
 
+    TRACE_T(ts2);
+    TRACE_ADD(1, ts1, ts2);
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe, start_c = G.K - 1;
     const int start_vals[3] = {sr, se, sa};
     if (ambiguous_ties(keys, pays, F, lane, r_lim, e_lim, start_c, start_vals)) {
@@ -337,6 +357,8 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     }
 
     // ---- 3. forward fill, lengths, compaction ----------------------------------------------
+    TRACE_T(ts3);
+    TRACE_ADD(2, ts2, ts3);
     const bool start_ok = sr >= 0 && sr < G.nr && se >= 0 && se < G.ne && sa >= 0 && sa < G.na;
     // every distance behind the start is integrated in the start voxel (raytracer.py:126,140)
     const int head = (start_ok && tneg < 0.0) ? 1 : 0;
@@ -394,6 +416,8 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     }
 
     // ---- 4. emit ---------------------------------------------------------------------------
+    TRACE_T(ts4);
+    TRACE_ADD(3, ts3, ts4);
     if (MODE == MODE_COUNT) {
         if (lane == 0) o.counts[ray] = head + nseg;
     } else if (MODE == MODE_FILL) {
@@ -424,6 +448,14 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         }
     }
     wave_sync();
+    TRACE_T(ts5);
+    TRACE_ADD(4, ts4, ts5);
+#ifdef SPHRT_TRACE_STAMPS
+    if (lane == 0) {
+        atomicAdd(&g_trace_cycles[5], 1ull);
+        atomicAdd(&g_trace_cycles[6], (unsigned long long)F);
+    }
+#endif
 }
 
 // Screen one ray per lane: a ray yields a segment only if it reaches the outer sphere or starts
@@ -663,6 +695,17 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
 }  // namespace sphrt
 
 using namespace sphrt;
+
+#ifdef SPHRT_TRACE_STAMPS
+extern "C" int sphrt_diag_trace_cycles(unsigned long long* host, int reset) {
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_trace_cycles), z, sizeof(z)) == hipSuccess ? 0 : 1;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace_cycles), 8 * sizeof(unsigned long long), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" size_t sphrt_trace_workspace_bytes(const sphrt_plan* plan, int64_t n) {
     if (!plan || n < 0) return 0;

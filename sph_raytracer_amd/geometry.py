@@ -214,6 +214,14 @@ class ViewGeomCollection(ViewGeom):
     def ray_starts(self):
         return tr.concat([g.ray_starts[None, ...] for g in self.geoms])
 
+    def _ray_spec(self):
+        """Stacked generator inputs when every view is a cone detector of one kind, else None."""
+        specs = [g._ray_spec() if hasattr(g, '_ray_spec') else None for g in self.geoms]
+        if not specs or any(sp is None for sp in specs) or len({sp[0] for sp in specs}) != 1:
+            return None
+        return (specs[0][0], tr.stack([sp[1] for sp in specs]), tr.stack([sp[2] for sp in specs]),
+                tr.stack([sp[3] for sp in specs]))
+
     @property
     def pos(self):
         if not all(hasattr(g, 'pos') for g in self.geoms):
@@ -257,6 +265,16 @@ class ConeRectGeom(ViewGeom):
              + right[None, None, :] * col
              + self.updir[None, None, :] * row).reshape((*self.shape, 3))
         return _unit_rows(d)
+
+    def _ray_spec(self):
+        """Inputs of the on-device generator (sphrt_rays_cone) that reproduce ``rays`` bit for
+        bit: (circ, frame = [lookdir, right, updir], per-row values, per-column values), from
+        the same torch calls as ``rays``."""
+        right = tr.cross(self.lookdir, self.updir, dim=-1)
+        ulim, vlim = self._span(0), self._span(1)
+        row = tr.linspace(-ulim, ulim, self.shape[0])
+        col = tr.linspace(-vlim, vlim, self.shape[1])
+        return 0, tr.concat([self.lookdir, right, self.updir]), row, col
 
     @property
     def ray_starts(self):
@@ -303,6 +321,15 @@ class ConeCircGeom(ConeRectGeom):
              + rad * tr.cos(ang) * right[None, None, :]
              + rad * tr.sin(ang) * self.updir[None, None, :])
         return _unit_rows(d)
+
+    def _ray_spec(self):
+        right = tr.cross(self.lookdir, self.updir, dim=-1)
+        ang = self.theta[None, :, None]
+        cos, sin = tr.cos(ang).reshape(-1), tr.sin(ang).reshape(-1)
+        # r * cos(theta) is formed in the tensors' own precision (float32 by default)
+        single = self.r.dtype == tr.float32 and cos.dtype == tr.float32
+        return (2 if single else 1, tr.concat([self.lookdir, right, self.updir]), self.r,
+                tr.concat([cos, sin]))
 
     @property
     def _wireframe(self):

@@ -132,6 +132,32 @@ def _broadcast_pair(xs, rays):
     return shape[:-1], xs, rays
 
 
+def _device_rays(geom, dev):
+    """Cone-detector ray directions generated on the device (sphrt_rays_cone), bit-identical to
+    ``geom.rays``; None for other geometries (their rays are copied from the host)."""
+    spec = geom._ray_spec() if hasattr(geom, '_ray_spec') else None
+    if spec is None:
+        return None
+    circ, frame, row, col = (spec[0],) + tuple(t.to(tr.float64).contiguous() for t in spec[1:])
+    shape = tuple(geom.shape)
+    n_views = frame.shape[0] if frame.dim() == 2 else 1
+    h, w = shape[-2], shape[-1]
+    if n_views * h * w != math.prod(shape) or row.shape[-1] != h:
+        return None
+    lib = _lib.load()
+    frame_d, row_d, col_d = (t.to(dev) for t in (frame, row, col))
+    rays = tr.empty(shape + (3,), dtype=tr.float64, device=dev)
+    _lib.check(lib.sphrt_rays_cone(n_views, h, w, int(circ), _lib.ptr(frame_d), _lib.ptr(row_d),
+                                   _lib.ptr(col_d), _lib.ptr(rays), _lib.stream_of(dev)),
+               'sphrt_rays_cone')
+    return rays
+
+
+def _geom_rays(geom, dev):
+    rays = _device_rays(geom, dev)
+    return geom.rays if rays is None else rays
+
+
 class _RayBatch:
     """Device copies of the unique starts / directions + the broadcast descriptor."""
 
@@ -271,7 +297,7 @@ def line_integrals(grid, geom, density):
     segment CSR — the memory-capped / cold path (one kernel, O(output) memory)."""
     dev = _lib.require_gpu()
     plan = _Plan(grid, dev)
-    batch = _RayBatch(grid, geom.ray_starts, geom.rays, dev)
+    batch = _RayBatch(grid, geom.ray_starts, _geom_rays(geom, dev), dev)
     density = tr.as_tensor(density)
     n_chan, div, out_shape = _layout_for(grid, batch.shape, density.shape)
     cdt = density.dtype if density.dtype in (tr.float32, tr.float64) else tr.float32
@@ -346,7 +372,7 @@ class Operator:
         self._cdev = dev
         lib = _lib.load()
         self._plan = _Plan(self.grid, dev)
-        batch = _RayBatch(self.grid, self.geom.ray_starts, self.geom.rays, dev)
+        batch = _RayBatch(self.grid, self.geom.ray_starts, _geom_rays(self.geom, dev), dev)
         self._ray_shape = batch.shape
         n = batch.n
         stream = _lib.stream_of(dev)

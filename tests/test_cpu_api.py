@@ -101,6 +101,23 @@ def test_viewgeom():
     assert g.shape == (4, 4)
 
 
+def test_ray_spec_availability():
+    """Cone detectors (and collections of one kind) expose the on-device generator's inputs;
+    arbitrary ViewGeoms and mixed collections keep host rays."""
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom, ViewGeom
+    rect = ConeRectGeom((4, 5), pos=(3, 0, 1))
+    circ = ConeCircGeom((4, 5), pos=(3, 0, 1))
+    circ_, frame, row, col = rect._ray_spec()
+    assert circ_ == 0 and frame.shape == (9,) and row.shape == (4,) and col.shape == (5,)
+    circ_, frame, row, col = circ._ray_spec()
+    assert circ_ == 2 and row.shape == (4,) and col.shape == (10,)   # float32 r, theta
+    coll = rect + ConeRectGeom((4, 5), pos=(0, 3, 1))
+    assert coll._ray_spec()[1].shape == (2, 9)
+    assert (rect + circ)._ray_spec() is None
+    rays = tr.rand((4, 5, 3))
+    assert not hasattr(ViewGeom(rays=rays, ray_starts=tr.zeros(3)), '_ray_spec')
+
+
 def test_model_instantiation():
     """test_model.py:7-15."""
     from sph_raytracer_amd import SphericalGrid

@@ -143,3 +143,26 @@ def test_gpu_sqrt_div_correctly_rounded(gpu):
     d = x[0, 2]
     ref = np.sqrt(R * R - d * d)
     assert np.array_equal(t.numpy()[0, len(R):], ref)
+
+
+def test_device_rays_bit_identical(gpu):
+    """On-device cone-beam rays (sphrt_rays_cone) equal the torch CPU rays bit
+    for bit: ConeRect / ConeCirc (lin and log radial spacing), orbit collections, one-pixel axes,
+    explicit look/up directions."""
+    import torch as tr
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom
+    from sph_raytracer_amd.raytracer import _device_rays
+    th = tr.linspace(0, 2 * tr.pi, 7)
+    cases = [
+        ConeRectGeom((50, 100), pos=(5, 0, 0), fov=(45, 45)),
+        ConeRectGeom((1, 5), pos=(3, 1, 2), fov=(10, 30)),
+        ConeRectGeom((4, 1), pos=(3, 1, 2)),
+        ConeRectGeom((6, 7), (1, 0, 0), (-1, 0, 0), (0, 1, 0), fov=(23, 45)),
+        sum(ConeRectGeom((50, 100), pos=(5 * tr.cos(a), 5 * tr.sin(a), 1), fov=(45, 45)) for a in th),
+        sum(ConeCircGeom((30, 24), pos=(5 * tr.cos(a), 5 * tr.sin(a), 1), fov=(0, 45)) for a in th),
+        ConeCircGeom((9, 13), pos=(2, 3, 4), fov=(5, 40), spacing='log'),
+    ]
+    for g in cases:
+        got = _device_rays(g, gpu)
+        assert got is not None
+        assert tr.equal(got.cpu(), g.rays), type(g).__name__
