@@ -381,6 +381,76 @@ __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restri
     }
 }
 
+// The same tables from a bitmap of the volume's granules in LDS instead of a sort, when the
+// bitmap fits (n_cols/4 bits; 128^3 voxels = 64 KiB): set one bit per segment, prefix-popcount
+// the words, and a granule's rank is the number of set bits below it.  O(segments + words) per
+// workgroup, a handful of barriers.  Identical output to the sort (ascending distinct granules).
+template <bool FILL>
+__global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
+    int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
+    int32_t* __restrict__ tab, int64_t tab_stride, int n_words,
+    unsigned long long* stats) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char bm_lds[];
+    uint32_t* bm = reinterpret_cast<uint32_t*>(bm_lds);     // n_words bitmap words
+    int32_t* pre = reinterpret_cast<int32_t*>(bm + n_words);  // set bits before each word
+    __shared__ ScanShared sh;
+    int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
+    const int64_t s0 = m[2], s1 = m[3];
+    if (FILL && m[5] < 0) return;
+    const int tid = threadIdx.x;
+    const int64_t n = s1 - s0;
+    if (n > kLocalMax) {
+        if (!FILL && tid == 0) {
+            m[5] = -1;
+            atomicAdd(stats, 1ull);
+        }
+        return;
+    }
+    for (int w = tid; w < n_words; w += kThreads) bm[w] = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += kThreads) {
+        const uint32_t g = ((uint32_t)vox[s0 + i] & ~kHead) >> 2;
+        atomicOr(&bm[g >> 5], 1u << (g & 31));
+    }
+    __syncthreads();
+    // thread t owns words [t*per, (t+1)*per)
+    const int per = (n_words + kThreads - 1) / kThreads;
+    const int w0 = min(tid * per, n_words), w1 = min(w0 + per, n_words);
+    int cnt = 0;
+    for (int w = w0; w < w1; ++w) cnt += __builtin_popcount(bm[w]);
+    int n_tab;
+    int run = block_excl_count(cnt, n_tab, sh);
+    if (!FILL) {
+        if (tid == 0) {
+            if (n_tab > kMaxGran) {
+                m[5] = -1;
+                atomicAdd(stats, 1ull);
+            } else {
+                m[5] = n_tab;
+                atomicMax(stats + 1, (unsigned long long)n_tab);
+            }
+        }
+        return;
+    }
+    int32_t* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
+    for (int w = w0; w < w1; ++w) {
+        pre[w] = run;
+        uint32_t bits = bm[w];
+        while (bits) {
+            const int b = __builtin_ctz(bits);
+            bits &= bits - 1;
+            tab_b[run++] = w * 32 + b;
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += kThreads) {
+        const uint32_t x = (uint32_t)vox[s0 + i];
+        const uint32_t v = x & ~kHead, g = v >> 2;
+        const int rank = pre[g >> 5] + __builtin_popcount(bm[g >> 5] & ((1u << (g & 31)) - 1u));
+        loc[s0 + i] = (uint16_t)((4 * rank + (int)(v & 3)) | ((x & kHead) ? 0x8000 : 0));
+    }
+}
+
 // LDS image of the staged granules (capacity `cap` granules = the table stride).  float: granule
 // j at dens[4j .. 4j+3].  double (32-byte granules, two 16-byte DMA halves): voxels 0-1 of
 // granule j at dens[2j ..], voxels 2-3 at dens[2*cap + 2j ..].
@@ -829,6 +899,12 @@ extern "C" int sphrt_diag_fwd_stamps(unsigned long long* host, int64_t n) {
 }
 #endif
 
+// bitmap words for a volume of n_cols voxels, or 0 when the bitmap does not fit in LDS
+static int table_bitmap_words(int64_t n_cols) {
+    const int64_t words = ((n_cols + 3) / 4 + 31) / 32;
+    return n_cols > 0 && words * 8 <= 150 * 1024 ? (int)words : 0;
+}
+
 extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_t* stats,
                                      void* stream) {
     if (!c || !c->vox || !blocks || !stats) return fail("incomplete CSR for the granule tables");
@@ -837,6 +913,12 @@ extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_
     if (hipMemsetAsync(stats, 0, 2 * sizeof(int64_t), st) != hipSuccess)
         return fail("hipMemsetAsync failed");
     if (c->n_segments == 0) return 0;
+    if (const int words = table_bitmap_words(c->n_cols)) {
+        hipLaunchKernelGGL(local_table_bitmap_kernel<false>, dim3((unsigned)c->n_blocks),
+                           dim3(kThreads), (size_t)words * 8, st, blocks, c->vox, nullptr, nullptr,
+                           0, words, (unsigned long long*)stats);
+        return check_launch("local_table_bitmap_kernel<count>");
+    }
     hipLaunchKernelGGL(local_table_kernel<false>, dim3((unsigned)c->n_blocks), dim3(kThreads), 0,
                        st, blocks, c->vox, nullptr, nullptr, 0, (unsigned long long*)stats);
     return check_launch("local_table_kernel<count>");
@@ -848,6 +930,12 @@ extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, u
     if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
     if (tab_stride < 1 || tab_stride > kMaxGran) return fail("bad granule table stride");
     if (c->n_segments == 0) return 0;
+    if (const int words = table_bitmap_words(c->n_cols)) {
+        hipLaunchKernelGGL(local_table_bitmap_kernel<true>, dim3((unsigned)c->n_blocks),
+                           dim3(kThreads), (size_t)words * 8, (hipStream_t)stream,
+                           (int64_t*)blocks, c->vox, loc, tab, tab_stride, words, nullptr);
+        return check_launch("local_table_bitmap_kernel<fill>");
+    }
     hipLaunchKernelGGL(local_table_kernel<true>, dim3((unsigned)c->n_blocks), dim3(kThreads), 0,
                        (hipStream_t)stream, (int64_t*)blocks, c->vox, loc, tab, tab_stride,
                        nullptr);
