@@ -22,6 +22,8 @@
 // tie groups and defers the ray to exact_kernel, which rebuilds all K candidates in the
 // reference's concatenation order, runs the emulated introsort (introsort.hpp) and walks the
 // sorted list exactly like trace_indices.  Deferred rays are rare; the list lives in workspace.
+#include <climits>
+
 #include "common.hpp"
 #include "introsort.hpp"
 #include "solve.hpp"
@@ -63,14 +65,25 @@ __device__ __forceinline__ double wave_sum(double v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return v;
 }
-// inclusive scan with op(a, b) = (b != none) ? b : a  — "last update wins" forward fill
-__device__ __forceinline__ int scan_last(int v, int lane) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        int u = __shfl_up(v, off);
-        if (lane >= off && v == kNone) v = u;
-    }
+// Wave inclusive scans on DPP lane moves: row_shr 1, 2, 4, 8 inside rows of 16, then
+// row_bcast 15 (rows 1, 3) and row_bcast 31 (rows 2, 3); lanes without a source read `id`.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ int dpp_or(int x, int id) {
+    return __builtin_amdgcn_update_dpp(id, x, CTRL, ROWS, 0xf, false);
+}
+template <typename Op>
+__device__ __forceinline__ int wave_scan(int v, int id, Op op) {
+    v = op(dpp_or<0x111>(v, id), v);
+    v = op(dpp_or<0x112>(v, id), v);
+    v = op(dpp_or<0x114>(v, id), v);
+    v = op(dpp_or<0x118>(v, id), v);
+    v = op(dpp_or<0x142, 0xa>(v, id), v);
+    v = op(dpp_or<0x143, 0xc>(v, id), v);
     return v;
+}
+// inclusive scan with op(a, b) = (b != none) ? b : a  — "last update wins" forward fill
+__device__ __forceinline__ int scan_last(int v, int /*lane*/) {
+    return wave_scan(v, kNone, [](int a, int b) { return b != kNone ? b : a; });
 }
 
 // ---- sorting of (key = distance bits, pay = candidate<<16 | region+2) pairs ---------------
@@ -78,28 +91,61 @@ __device__ __forceinline__ bool pair_less(uint64_t ka, uint32_t pa, uint64_t kb,
     return ka < kb || (ka == kb && pa < pb);
 }
 
+// ---- lane exchanges without the LDS crossbar ------------------------------------------------
+// xlane<X>(x): the value x holds in lane (lane ^ X), X a compile-time constant: DPP quad
+// permutes and row (half-)mirrors inside 16 lanes, row shifts for xor 4 / 8, a swizzle for
+// xor 16 / 31 inside 32 lanes, the gfx950 32-lane swap for xor 32.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+template <int X>
+__device__ __forceinline__ uint32_t xlane(uint32_t x, int lane) {
+    if constexpr (X == 1) return dpp_mov<0xB1>(x);                 // quad_perm [1,0,3,2]
+    else if constexpr (X == 2) return dpp_mov<0x4E>(x);            // quad_perm [2,3,0,1]
+    else if constexpr (X == 3) return dpp_mov<0x1B>(x);            // quad_perm [3,2,1,0]
+    else if constexpr (X == 7) return dpp_mov<0x141>(x);           // row_half_mirror
+    else if constexpr (X == 15) return dpp_mov<0x140>(x);          // row_mirror
+    else if constexpr (X == 4 || X == 8) {                         // row_shl / row_shr by X
+        const uint32_t up = dpp_mov<0x100 + X>(x), dn = dpp_mov<0x110 + X>(x);
+        return (lane & X) ? dn : up;
+    } else if constexpr (X == 16 || X == 31) {
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (X << 10) | 0x1F);
+    } else if constexpr (X == 32) {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return lane < 32 ? (uint32_t)r[1] : (uint32_t)r[0];
+    } else if constexpr (X == 63) {
+        return xlane<32>(xlane<31>(x, lane), lane);
+    } else {
+        return (uint32_t)__shfl_xor((int)x, X);
+    }
+}
+template <int X>
+__device__ __forceinline__ uint64_t xlane64(uint64_t x, int lane) {
+    return (uint64_t)xlane<X>((uint32_t)x, lane) | ((uint64_t)xlane<X>((uint32_t)(x >> 32), lane) << 32);
+}
+
 // One compare-exchange layer of the ascending-only ("flip") bitonic network over 64*M elements,
-// element e = i*64 + lane; partner = e ^ mask.  `mask` is a compile-time constant after unroll.
-template <int M>
-__device__ __forceinline__ void cas_layer(uint64_t (&k)[M], uint32_t (&p)[M], int mask,
-                                          int lane) {
+// element e = i*64 + lane; partner = e ^ MASK.
+template <int M, int MASK>
+__device__ __forceinline__ void cas_layer(uint64_t (&k)[M], uint32_t (&p)[M], int lane) {
+    constexpr int LM = MASK & 63;
     uint64_t nk[M];
     uint32_t np[M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-        const int pi = i ^ (mask >> 6);
-        const int pl = lane ^ (mask & 63);
+        const int pi = i ^ (MASK >> 6);
         uint64_t ok;
         uint32_t op;
-        if ((mask & 63) == 0) {
+        if constexpr (LM == 0) {
             ok = k[pi];
             op = p[pi];
         } else {
-            ok = __shfl(k[pi], pl);
-            op = __shfl(p[pi], pl);
+            ok = xlane64<LM>(k[pi], lane);
+            op = xlane<LM>(p[pi], lane);
         }
         const int e = i * 64 + lane;
-        const int pe = pi * 64 + pl;
+        const int pe = pi * 64 + (lane ^ LM);
         bool take = (e < pe) ? pair_less(ok, op, k[i], p[i]) : pair_less(k[i], p[i], ok, op);
         nk[i] = take ? ok : k[i];
         np[i] = take ? op : p[i];
@@ -108,6 +154,23 @@ __device__ __forceinline__ void cas_layer(uint64_t (&k)[M], uint32_t (&p)[M], in
     for (int i = 0; i < M; ++i) {
         k[i] = nk[i];
         p[i] = np[i];
+    }
+}
+
+// half-cleaner layers J, J/2, ..., 1 and the stages KK, 2KK, ... P of the network
+template <int M, int J>
+__device__ __forceinline__ void half_cleaners(uint64_t (&k)[M], uint32_t (&p)[M], int lane) {
+    if constexpr (J > 0) {
+        cas_layer<M, J>(k, p, lane);
+        half_cleaners<M, J / 2>(k, p, lane);
+    }
+}
+template <int M, int KK>
+__device__ __forceinline__ void sort_stages(uint64_t (&k)[M], uint32_t (&p)[M], int lane) {
+    if constexpr (KK <= 64 * M) {
+        cas_layer<M, KK - 1>(k, p, lane);   // flip: mirror partner inside the KK-block
+        half_cleaners<M, KK / 4>(k, p, lane);
+        sort_stages<M, KK * 2>(k, p, lane);
     }
 }
 
@@ -122,13 +185,7 @@ __device__ void sort_regs(uint64_t* keys, uint32_t* pays, int F, int lane) {
         k[i] = r ? keys[e] : ~0ull;
         p[i] = r ? pays[e] : ~0u;
     }
-    constexpr int P = 64 * M;
-#pragma unroll
-    for (int kk = 2; kk <= P; kk <<= 1) {
-        cas_layer<M>(k, p, kk - 1, lane);  // flip: mirror partner inside the 2-block
-#pragma unroll
-        for (int j = kk >> 2; j > 0; j >>= 1) cas_layer<M>(k, p, j, lane);
-    }
+    sort_stages<M, 2>(k, p, lane);
     wave_sync();
 #pragma unroll
     for (int i = 0; i < M; ++i) {
@@ -198,13 +255,8 @@ __device__ __forceinline__ int update_mask(uint32_t pay, int r_lim, int e_lim, i
     return cand < e_lim ? 2 : 4;
 }
 
-__device__ __forceinline__ int scan_max(int v, int lane) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        int u = __shfl_up(v, off);
-        if (lane >= off) v = max(v, u);
-    }
-    return v;
+__device__ __forceinline__ int scan_max(int v, int /*lane*/) {
+    return wave_scan(v, INT_MIN, [](int a, int b) { return max(a, b); });
 }
 
 // value a candidate writes into region row `row` (0 r, 1 e, 2 a); start entry: the start voxel
@@ -398,9 +450,9 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         if (ur == kNone) ur = cr;
         if (ue == kNone) ue = cE;
         if (ua == kNone) ua = cA;
-        cr = __shfl(ur, 63);
-        cE = __shfl(ue, 63);
-        cA = __shfl(ua, 63);
+        cr = __builtin_amdgcn_readlane(ur, 63);
+        cE = __builtin_amdgcn_readlane(ue, 63);
+        cA = __builtin_amdgcn_readlane(ua, 63);
         const double t = __longlong_as_double((long long)k);
         const double len = tn - t;
         const bool ok = real && len > 0.0 && __builtin_isfinite(len) && ur >= 0 && ur < G.nr &&
