@@ -392,7 +392,9 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     TRACE_ADD(0, ts0, ts1);
     if (F <= 64) sort_regs<1>(keys, pays, F, lane);
     else if (F <= 128) sort_regs<2>(keys, pays, F, lane);
+#if !defined(SPHRT_TRACE_NO_M4)
     else if (F <= 256) sort_regs<4>(keys, pays, F, lane);
+#endif
     else sort_lds(keys, pays, F, lane);
 
     TRACE_T(ts2);
@@ -544,7 +546,10 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
 // Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
 // image looks like.  Every lane evaluates the (wave-uniform) ray set-up itself.
 template <int MODE, typename T>
-__global__ __launch_bounds__(256, 4) void trace_kernel(GridDev G, RaysDev R, TraceOut<T> o,
+#ifndef SPHRT_TRACE_MIN_BLOCKS
+#define SPHRT_TRACE_MIN_BLOCKS 4
+#endif
+__global__ __launch_bounds__(256, SPHRT_TRACE_MIN_BLOCKS) void trace_kernel(GridDev G, RaysDev R, TraceOut<T> o,
                                                     int cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
