@@ -127,13 +127,15 @@ int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const doubl
  *             rays empty_ray[empty_lo .. empty_hi),
  *   tab     — (optional) per block b, its n_tab distinct 4-voxel granules (voxel >> 2) ascending
  *             at tab[b*tab_stride ..) (n_blocks * tab_stride entries),
- *   loc     — (optional) per segment, 4 * (rank of its granule in the block's table) +
- *             (voxel & 3), with the row-head flag in bit 15 (SPHRT_LOC_HEAD).
+ *   loc     — (optional) per segment, 16 * (rank of its granule in the block's table + 1) +
+ *             4 * (voxel & 3): the voxel's byte offset in the forward's float LDS image, whose
+ *             granule 0 is zero; the row-head flag in bit 15 (SPHRT_LOC_HEAD).
  * sphrt_csr_index() fills vox heads, row_ray, empty_ray and blocks from row_ptr (n_tab = -1);
  * n_blocks = sphrt_csr_blocks(n_segments).  sphrt_csr_local_count/_fill then build tab and loc
- * (uint16, n_segments entries) for every block of at most 4096 segments and 2048 granules; with
+ * (uint16, n_segments entries) for every block of at most 4096 segments and 2046 granules; with
  * loc/tab/n_cols/tab_stride set, a static forward on a 16-byte-aligned density stages each
- * block's granules in LDS (4 * tab_stride elements, up to 48 KB) instead of gathering per segment.
+ * block's granules in LDS (4 * (tab_stride + 1) elements, up to 48 KB) instead of gathering per
+ * segment.
  * Per-segment arrays (vox, len, len32, loc) are read in aligned 8-entry chunks: allocate
  * them to round_up(n_segments, 8) entries (the entries past n_segments are never used).  `len32` is
  * the float32 copy of `len` used by the float32 forward (sphrt_f64_to_f32). */

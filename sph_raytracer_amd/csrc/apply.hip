@@ -20,13 +20,24 @@ namespace sphrt {
 
 constexpr uint32_t kHead = 0x80000000u;
 constexpr int kThreads = 256;
+#ifndef SPHRT_FWD_MINB64
+#define SPHRT_FWD_MINB64 5   // resident float64 forward workgroups per CU the registers aim for
+#endif
+#ifndef SPHRT_FWD_EMIT
+#define SPHRT_FWD_EMIT 2   // row-close emission: 2 selects, 1 rank walk, 0 per-slot window tests
+#endif
+// 64-bit min/max as plain selects (HIP's min<int64_t>/max<int64_t> went through double
+// conversions on VALU even for uniform operands).
+__host__ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
+__host__ __device__ __forceinline__ int64_t imax64(int64_t a, int64_t b) { return a > b ? a : b; }
 constexpr int kPer = 8;                         // segments per thread per pass
 constexpr int kPass = kThreads * kPer;          // 2048 segments per pass
 constexpr int64_t kSegPerBlock = 1792;          // row starts per workgroup (leaves room for the
                                                 // last row's overhang inside one pass)
 constexpr int kBlockFields = 6;                 // empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab
 constexpr int kLocalMax = 4096;                 // segments per workgroup with a granule table
-constexpr int kMaxGran = 2048;                  // granules per table (sphrt_csr_local)
+constexpr int kMaxGran = 2046;                  // granules per table (sphrt_csr_local): loc's
+                                                // 15-bit byte offsets reach 16*(2046+1)+12
 constexpr int kGranEarly = 3;                   // table chunks of 256 fetched before the record
 
 // Diagnostic build only (-DSPHRT_FWD_STAMPS, tools/fwd_timeline.py): s_memrealtime (100 MHz)
@@ -82,8 +93,8 @@ __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
     // this block's share of the empty-ray list (split evenly, independent of the segments)
     const int64_t n_empty = n - row_pre[n];
     const int64_t e_chunk = (n_empty + nblocks - 1) / nblocks;
-    m[0] = min<int64_t>(b * e_chunk, n_empty);
-    m[1] = min<int64_t>((b + 1) * e_chunk, n_empty);
+    m[0] = imin64(b * e_chunk, n_empty);
+    m[1] = imin64((b + 1) * e_chunk, n_empty);
     m[2] = row_ptr[lo];
     m[3] = row_ptr[hi];
     m[4] = row_pre[lo];
@@ -99,10 +110,11 @@ struct ScanShared {
 
 // Wave-level inclusive scans on DPP lane moves (no LDS crossbar, no lane-index registers):
 // row_shr 1, 2, 4, 8 within each row of 16 lanes, then row_bcast 15 (rows 1, 3) and row_bcast 31
-// (rows 2, 3).  Lanes without a source read the identity (`old` = 0).
+// (rows 2, 3).  Lanes without a source read the identity: bound_ctrl zero for the full-row moves
+// (no `old` register to clear), `old` = 0 for the row_bcast ones (rows outside ROWS keep it).
 template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ int dpp0(int x) {
-    return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWS, 0xf, false);
+    return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWS, 0xf, ROWS == 0xf);
 }
 template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ double dpp0(double x) {
@@ -184,9 +196,9 @@ __device__ __forceinline__ double block_excl_segsum(bool has, double tail, bool&
 // passed: no trailing barrier.  `lds_barrier` waits for LDS traffic only, so global loads issued
 // before it (row prefetches, per-segment gathers) stay in flight across it.
 struct FwdShared {
-    int cnt[2][4];
-    int has[2][4];
-    double sum[2][4];
+    alignas(16) int cnt[2][4];
+    alignas(16) int has[2][4];
+    alignas(16) double sum[2][4];
 };
 
 __device__ __forceinline__ void lds_barrier() {
@@ -195,21 +207,23 @@ __device__ __forceinline__ void lds_barrier() {
 
 template <bool kDrain>   // kDrain: a full barrier (also retires LDS-DMA granule loads)
 __device__ __forceinline__ int block_excl_count1(int v, int& total, int (&cnt)[4]) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int inc = wave_incl_sum(v);
     if (lane == 63) cnt[wid] = inc;
     if (kDrain) __syncthreads();
     else lds_barrier();
-    int base = 0;
-    for (int w = 0; w < wid; ++w) base += cnt[w];
-    total = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+    const int4 c = *reinterpret_cast<const int4*>(cnt);     // one LDS read, no per-wave loop
+    total = c.x + c.y + c.z + c.w;
+    const int base = (wid > 0 ? c.x : 0) + (wid > 1 ? c.y : 0) + (wid > 2 ? c.z : 0);
     return base + inc - v;
 }
 
 __device__ __forceinline__ double block_excl_segsum1(bool has, double tail, bool& tot_has,
                                                      double& tot_sum, int (&hs)[4],
                                                      double (&sm)[4]) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int h = has ? 1 : 0;
     double s = tail;
     seg_step<kShr1>(h, s);
@@ -225,14 +239,18 @@ __device__ __forceinline__ double block_excl_segsum1(bool has, double tail, bool
         sm[wid] = s;
     }
     lds_barrier();
-    double cs = 0.0;
-    for (int w = 0; w < wid; ++w) cs = hs[w] ? sm[w] : cs + sm[w];
-    tot_has = false;
-    tot_sum = 0.0;
-    for (int w = 0; w < 4; ++w) {
-        tot_sum = hs[w] ? sm[w] : tot_sum + sm[w];
-        tot_has = tot_has || hs[w];
-    }
+    const int4 hv = *reinterpret_cast<const int4*>(hs);   // vector LDS reads, no per-wave loop
+    const double2 s01 = *reinterpret_cast<const double2*>(sm);
+    const double2 s23 = *reinterpret_cast<const double2*>(sm + 2);
+    const int hw[4] = {hv.x, hv.y, hv.z, hv.w};
+    const double sw[4] = {s01.x, s01.y, s23.x, s23.y};
+    double t[4];                                   // segmented prefix through wave w
+    t[0] = sw[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) t[w] = hw[w] ? sw[w] : t[w - 1] + sw[w];
+    const double cs = wid == 0 ? 0.0 : wid == 1 ? t[0] : wid == 2 ? t[1] : t[2];
+    tot_sum = t[3];
+    tot_has = (hv.x | hv.y | hv.z | hv.w) != 0;
     return eh ? es : cs + es;
 }
 
@@ -287,6 +305,13 @@ __device__ __forceinline__ void load8(const int32_t* __restrict__ vox, const L* 
     }
 }
 
+// loc entry of a segment whose voxel v sits in granule `rank` of its workgroup's table: the
+// byte offset of the voxel in the forward's float LDS image (granule 0 of which is a zero granule
+// for masked slots, so table granule r sits at 16*(r+1)), and the row-head flag in bit 15.
+__device__ __forceinline__ uint16_t loc_code(int rank, uint32_t v, bool head) {
+    return (uint16_t)((16 * (rank + 1) + 4 * (int)(v & 3u)) | (head ? 0x8000 : 0));
+}
+
 // ---- per-workgroup granule table ----------------------------------------------------------
 // Per-segment density gathers are the forward's bottleneck: every segment is one divergent 4-byte
 // lane access, and the load path's per-lane rate, not bytes, bounds the kernel (C2: ~7 of 13 us).
@@ -308,7 +333,7 @@ __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restri
     int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
     const int64_t s0 = m[2], s1 = m[3];
     if (FILL && m[5] < 0) return;
-    const int n = (int)min<int64_t>(s1 - s0, (int64_t)kLocalMax + 1);
+    const int n = (int)imin64(s1 - s0, (int64_t)kLocalMax + 1);
     const int tid = threadIdx.x;
     if (n > kLocalMax) {
         if (tid == 0) {
@@ -376,8 +401,7 @@ __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restri
             tab[(int64_t)blockIdx.x * tab_stride + rank] = (int32_t)gran(k);
         }
         const int pos = (int)((k >> 1) & 0xfff);
-        const int slot = 4 * rank + (int)((k >> 13) & 3);
-        loc[s0 + pos] = (uint16_t)(slot | ((k & 1) ? 0x8000 : 0));
+        loc[s0 + pos] = loc_code(rank, (uint32_t)(k >> 13), (k & 1) != 0);
     }
 }
 
@@ -447,34 +471,41 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
         const uint32_t x = (uint32_t)vox[s0 + i];
         const uint32_t v = x & ~kHead, g = v >> 2;
         const int rank = pre[g >> 5] + __builtin_popcount(bm[g >> 5] & ((1u << (g & 31)) - 1u));
-        loc[s0 + i] = (uint16_t)((4 * rank + (int)(v & 3)) | ((x & kHead) ? 0x8000 : 0));
+        loc[s0 + i] = loc_code(rank, v, (x & kHead) != 0);
     }
 }
 
-// LDS image of the staged granules (capacity `cap` granules = the table stride).  float: granule
-// j at dens[4j .. 4j+3].  double (32-byte granules, two 16-byte DMA halves): voxels 0-1 of
-// granule j at dens[2j ..], voxels 2-3 at dens[2*cap + 2j ..].
+// LDS image of a workgroup's granule table: granule 0 is zero (the read of every masked slot),
+// table granule r at granules r+1; float 16 B and double 32 B per granule, contiguous, so a
+// segment's loc offset x (bits 0-14) is its voxel's byte offset for float and half of it for
+// double.  Each 16-byte LDS-DMA lane carries a whole float granule or half a double one: DMA
+// round r of wave w covers table entries gran_entry(r, w, lane) (64/G granules, G lanes each).
 template <typename T>
-__device__ __forceinline__ int dens_index(uint32_t slot, int cap) {
-    if constexpr (sizeof(T) == 4) return (int)slot;
-    else return (int)(((slot & 2u) ? 2 * cap : 0) + ((slot >> 2) << 1) + (slot & 1u));
+constexpr int kGranLanes = (int)sizeof(T) / 4;        // 16-byte DMA lanes per granule
+template <typename T>   // early rounds: kGranEarly chunks of 256 granules
+constexpr int kEarlyRounds = kGranEarly * kGranLanes<T>;
+
+template <typename T>
+__device__ __forceinline__ int gran_entry0(int r, int w) {    // first entry of round r (uniform)
+    constexpr int G = kGranLanes<T>;
+    return (r / G) * kThreads + w * 64 + (r % G) * (64 / G);
 }
 
-// One granule by LDS-DMA: float, 16 B at dens[4*j0 + 4*lane]; double, two 16-B halves.  `off`
-// is the granule's byte offset in the channel (32-bit: volumes under 4 GiB per channel).
 template <typename T>
-__device__ __forceinline__ void stage_one(const T* __restrict__ rho, uint32_t off, int j0, int cap,
+__device__ __forceinline__ T lds_at(const T* dens, uint32_t x) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(dens) + x * (sizeof(T) / 4));
+}
+
+// One DMA lane: granule g (its index in the channel; the byte offset is 32-bit: volumes under
+// 4 GiB per channel), into the round whose first table entry is e0.
+template <typename T>
+__device__ __forceinline__ void stage_one(const T* __restrict__ rho, int32_t g, int e0, int lane,
                                           T* dens) {
-    const char* src = reinterpret_cast<const char*>(rho) + off;
-    if constexpr (sizeof(T) == 4) {
-        __builtin_amdgcn_global_load_lds((const void*)src,
-            (__attribute__((address_space(3))) void*)(dens + 4 * j0), 16, 0, 0);
-    } else {
-        __builtin_amdgcn_global_load_lds((const void*)src,
-            (__attribute__((address_space(3))) void*)(dens + 2 * j0), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(src + 16),
-            (__attribute__((address_space(3))) void*)(dens + 2 * cap + 2 * j0), 16, 0, 0);
-    }
+    constexpr int G = kGranLanes<T>;
+    const char* src = reinterpret_cast<const char*>(rho) + (uint32_t)g * (16u * G) +
+                      16 * (lane % G);
+    __builtin_amdgcn_global_load_lds((const void*)src,
+        (__attribute__((address_space(3))) void*)(dens + 4 * (e0 + 1)), 16, 0, 0);
 }
 
 // The volume's last granule, if partial (voxel count not a multiple of 4), can only be the
@@ -482,81 +513,57 @@ __device__ __forceinline__ void stage_one(const T* __restrict__ rho, uint32_t of
 template <typename T>
 __device__ __forceinline__ void stage_partial_tail(const T* __restrict__ rho,
                                                    const int32_t* __restrict__ tab_b, int n_tab,
-                                                   int64_t n_cols, int cap, T* dens) {
+                                                   int64_t n_cols, T* dens) {
     if ((n_cols & 3) != 0 && n_tab > 0 && (int)threadIdx.x == (n_tab - 1) % kThreads) {
         const int j = n_tab - 1;
         const int64_t v0 = 4 * (int64_t)tab_b[j];
         if (v0 + 4 > n_cols)
-            for (int i = 0; i < 4; ++i)
-                dens[dens_index<T>(4 * j + i, cap)] = v0 + i < n_cols ? rho[v0 + i] : (T)0;
+            for (int i = 0; i < 4; ++i) dens[4 * (j + 1) + i] = v0 + i < n_cols ? rho[v0 + i] : (T)0;
     }
 }
 
-// Chunks [q0, ..) of the table, read from memory one 256-chunk per round.
+// DMA rounds [r0, ..) of the table, entries read from memory one round at a time.
 template <typename T>
 __device__ __forceinline__ void stage_granules_late(const T* __restrict__ rho,
-                                                    const int32_t* __restrict__ tab_b, int q0,
-                                                    int n_tab, int64_t n_cols, int cap, T* dens) {
+                                                    const int32_t* __restrict__ tab_b, int r0,
+                                                    int n_tab, int32_t g_full, T* dens) {
+    constexpr int G = kGranLanes<T>;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t g_full = n_cols >> 2;
-    constexpr int kShift = sizeof(T) == 4 ? 4 : 5;
-    for (int q = q0; q * kThreads < n_tab; ++q) {
-        const int j0 = q * kThreads + w * 64;
-        if (j0 + lane < n_tab) {
-            const int32_t g = tab_b[j0 + lane];
-            if (g < g_full) stage_one<T>(rho, (uint32_t)g << kShift, j0, cap, dens);
+    for (int r = r0; (r / G) * kThreads < n_tab; ++r) {
+        const int e0 = gran_entry0<T>(r, w);
+        const int e = e0 + lane / G;
+        if (e < n_tab) {
+            const int32_t g = tab_b[e];
+            if (g < g_full) stage_one<T>(rho, g, e0, lane, dens);
         }
     }
 }
 
-// Granules [0, kGranEarly*256) come from the table entries fetched early (ti); any beyond that
-// (large tables) are fetched here, one 256-chunk per round.  When the volume's voxel count is
-// not a multiple of 4 its last granule is partial: only the table's last entry can be, it is
-// skipped by the DMA (no read past the volume) and copied lane by lane at the end.
+// Rounds [0, kEarlyRounds) come from the table entries fetched early (ti); any beyond that
+// (large tables) are fetched here.  When the volume's voxel count is not a multiple of 4 its
+// last granule is partial: only the table's last entry can be, it is skipped by the DMA (no read
+// past the volume) and copied lane by lane at the end.  Writes the zero granule.
 template <typename T>
-__device__ __forceinline__ void stage_granules(const T* __restrict__ rho, const int32_t (&ti)[kGranEarly],
+__device__ __forceinline__ void stage_granules(const T* __restrict__ rho,
+                                               const int32_t (&ti)[kEarlyRounds<T>],
                                                const int32_t* __restrict__ tab_b, int n_tab,
-                                               int64_t n_cols, int cap, T* dens) {
+                                               int32_t g_full, int64_t n_cols, T* dens) {
+    constexpr int G = kGranLanes<T>;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t g_full = n_cols >> 2;        // granules below this one are whole
-    constexpr int kShift = sizeof(T) == 4 ? 4 : 5;
+    if (threadIdx.x < 4) dens[threadIdx.x] = (T)0;
     // every early table entry is consumed before the first DMA goes out (one wait, not one per
     // DMA: the wait-count model serialises VMEM results read after an LDS-DMA)
-    static_assert(kGranEarly == 3, "the register pin below names every early entry");
-    asm volatile("" ::"v"(ti[0]), "v"(ti[1]), "v"(ti[2]));   // one wait for all of them, here
 #pragma unroll
-    for (int q = 0; q < kGranEarly; ++q) {
-        const int j0 = q * kThreads + w * 64;   // this wave's 64 granules of round q (uniform)
-        if (j0 + lane < n_tab && ti[q] < g_full)
-            stage_one<T>(rho, (uint32_t)ti[q] << kShift, j0, cap, dens);
+    for (int r = 0; r < kEarlyRounds<T>; ++r) asm volatile("" ::"v"(ti[r]));
+#pragma unroll
+    for (int r = 0; r < kEarlyRounds<T>; ++r) {
+        const int e0 = gran_entry0<T>(r, w);
+        if (e0 + lane / G < n_tab && ti[r] < g_full) stage_one<T>(rho, ti[r], e0, lane, dens);
     }
-    stage_granules_late<T>(rho, tab_b, kGranEarly, n_tab, n_cols, cap, dens);
-    stage_partial_tail<T>(rho, tab_b, n_tab, n_cols, cap, dens);
-}
-
-template <typename L>
-__device__ __forceinline__ void load8_loc(const uint16_t* __restrict__ loc,
-                                          const L* __restrict__ len, int p0, int s0, int s1,
-                                          uint32_t (&v)[kPer], L (&l)[kPer]) {
-    if (p0 < s1) {                            // 16 bytes of slots, 8 lengths
-        const uint4 a = *reinterpret_cast<const uint4*>(loc + p0);
-        const uint32_t w[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const uint32_t x = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-            v[k] = (x & 0x7fffu) | ((x & 0x8000u) << 16);
-        }
-        load_len8(len, p0, l);
-        if (p0 < s0 || p0 + kPer > s1) mask8(p0, s0, s1, v, l);
-    } else {
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            v[k] = 0u;
-            l[k] = (L)0;
-        }
-    }
+    stage_granules_late<T>(rho, tab_b, kEarlyRounds<T>, n_tab, g_full, dens);
+    stage_partial_tail<T>(rho, tab_b, n_tab, n_cols, dens);
 }
 
 // The first pass's loads, issued before anything is known about the workgroup and decoded
@@ -589,22 +596,48 @@ __device__ __forceinline__ void raw_load(const int32_t* __restrict__ vox,
     }
 }
 
+// Bits [first, end) of a chunk (chunk-relative segment window).
+__device__ __forceinline__ uint32_t window_bits(int first, int end) {
+    const int a = max(first, 0), b = min(end, kPer);
+    return a < b ? ((1u << b) - 1u) & ~((1u << a) - 1u) : 0u;
+}
+
+// A chunk's segments: table mode, v[k] = LDS byte offset of the voxel (loc bits 0-14); otherwise
+// the vox word.  Returns the row heads of the chunk (bit k = segment k).
 template <typename L, bool LOCAL>
-__device__ __forceinline__ void decode(const RawChunk<L, LOCAL>& r, uint32_t (&v)[kPer],
-                                       L (&l)[kPer]) {
+__device__ __forceinline__ uint32_t decode(const RawChunk<L, LOCAL>& r, uint32_t (&v)[kPer],
+                                           L (&l)[kPer]) {
+    uint32_t hmask = 0;
     if constexpr (LOCAL) {
         const uint32_t w[4] = {r.ix[0].x, r.ix[0].y, r.ix[0].z, r.ix[0].w};
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const uint32_t x = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-            v[k] = (x & 0x7fffu) | ((x & 0x8000u) << 16);
-        }
+        for (int k = 0; k < kPer; ++k) v[k] = (w[k >> 1] >> (16 * (k & 1))) & 0x7ffcu;
+        // bit 15 of half-word k -> bit k: even k to bits 0,2,4,6, odd k to 16,18,20,22, folded
+        const uint32_t h = ((w[0] >> 15) & 0x10001u) | ((w[1] >> 13) & 0x40004u) |
+                           ((w[2] >> 11) & 0x100010u) | ((w[3] >> 9) & 0x400040u);
+        hmask = (h | (h >> 15)) & 0xffu;
     } else {
         v[0] = r.ix[0].x; v[1] = r.ix[0].y; v[2] = r.ix[0].z; v[3] = r.ix[0].w;
         v[4] = r.ix[1].x; v[5] = r.ix[1].y; v[6] = r.ix[1].z; v[7] = r.ix[1].w;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) hmask |= (v[k] >> 31) << k;
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) l[k] = r.l[k];
+    return hmask;
+}
+
+// Load, decode and window one chunk [p0, p0 + kPer) of a pass (pass-relative window [lo, hi)):
+// masked slots read the zero granule / voxel 0 with length 0 and carry no head.
+template <typename L, bool LOCAL>
+__device__ __forceinline__ uint32_t window_chunk(const RawChunk<L, LOCAL>& r, int p0, int lo,
+                                                 int hi, uint32_t (&v)[kPer], L (&l)[kPer]) {
+    uint32_t hmask = decode<L, LOCAL>(r, v, l);
+    if (p0 < lo || p0 + kPer > hi) {                // edge chunks only
+        mask8(p0, lo, hi, v, l);
+        hmask &= window_bits(lo - p0, hi - p0);
+    }
+    return hmask;
 }
 
 // ---- forward ------------------------------------------------------------------------------
@@ -623,7 +656,7 @@ enum FwdMode { kFwdTable = 0, kFwdGather = 1, kFwdDynamic = 2 };
 // Resident workgroups per CU the register allocation aims for: 6 (<= 80 VGPRs) lets a C2-sized
 // launch (~1500 workgroups) be resident at once; float64 stops at 5 (no spills).
 template <typename T, int MODE>
-constexpr int fwd_min_blocks() { return sizeof(T) == 8 ? 5 : 6; }
+constexpr int fwd_min_blocks() { return sizeof(T) == 8 ? SPHRT_FWD_MINB64 : 6; }
 
 template <typename T>
 using AccumOf = typename std::conditional<sizeof(T) == 4, float, double>::type;
@@ -650,17 +683,18 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
     // so its first pass is [b*kSegPerBlock, +kPass)) and the granule table (fixed stride).
     FWD_STAMP(0);
     const int64_t base0 = (int64_t)blockIdx.x * kSegPerBlock;
-    const int n_here = (int)min<int64_t>(n_seg - base0, (int64_t)kPass + 1);
+    const int n_here = (int)imin64(n_seg - base0, (int64_t)kPass + 1);
     RawChunk<L, local> raw;
     raw_load<L, local>(vox + base0, loc + base0, len + base0, o, n_here, raw);
     // table chunks beyond the stride read the next workgroup's entries (tab is padded by
     // kGranEarly*kThreads entries); they are never staged (j >= n_tab)
     const int32_t* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
-    const int cap = (int)tab_stride;
-    int32_t ti[kGranEarly];
+    int32_t ti[kEarlyRounds<T>];
     if (local) {
+        const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
-        for (int q = 0; q < kGranEarly; ++q) ti[q] = tab_b[tid + q * kThreads];
+        for (int r = 0; r < kEarlyRounds<T>; ++r)
+            ti[r] = tab_b[gran_entry0<T>(r, w) + (tid & 63) / kGranLanes<T>];
     }
     __builtin_amdgcn_sched_barrier(0);
     const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
@@ -688,42 +722,43 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
         zero_empty();
         return;
     }
-    if (local) stage_granules<T>(density, ti, tab_b, (int)n_tab, n_cols, cap, dens);
+    const int32_t g_full = (int32_t)imin64(n_cols >> 2, INT32_MAX);   // whole granules
+    if (local) stage_granules<T>(density, ti, tab_b, (int)n_tab, g_full, n_cols, dens);
     // pass-relative segment window [lo, hi) of this workgroup (32-bit lane arithmetic)
     auto window = [&](int64_t base, int& lo, int& hi) {
-        lo = (int)max<int64_t>(s0 - base, -1);
-        hi = (int)min<int64_t>(s1 - base, (int64_t)kPass + 1);
+        lo = (int)imax64(s0 - base, -1);
+        hi = (int)imin64(s1 - base, (int64_t)kPass + 1);
     };
     uint32_t v[kPer];
     L l[kPer];
-    decode<L, local>(raw, v, l);
+    uint32_t hmask;
     {
         int lo, hi;
         window(base0, lo, hi);
-        mask8(o, lo, hi, v, l);
+        hmask = window_chunk<L, local>(raw, o, lo, hi, v, l);
     }
     int64_t rbase = 0;                            // rows started in earlier passes
     FWD_STAMP(1);
+#pragma clang loop unroll(disable)   // (also no peeling: one copy of the pass body)
     for (int64_t c = 0; c < nc; ++c) {
         const T* rho = density + c * cs;
         T* oc = out + c * ocs;
         if (local && c > 0) {
-            stage_granules_late<T>(rho, tab_b, 0, (int)n_tab, n_cols, cap, dens);
-            stage_partial_tail<T>(rho, tab_b, (int)n_tab, n_cols, cap, dens);
+            stage_granules_late<T>(rho, tab_b, 0, (int)n_tab, g_full, dens);
+            stage_partial_tail<T>(rho, tab_b, (int)n_tab, n_cols, dens);
         }
         FWD_STAMP(2);
         double carry = 0.0;                 // open run entering the pass
         rbase = 0;
+#pragma clang loop unroll(disable)
         for (int64_t base = base0; base < s1; base += kPass) {
             int lo, hi;
             window(base, lo, hi);
             if (base != base0 || c != 0) {
-                if (local) load8_loc(loc + base, len + base, o, lo, hi, v, l);
-                else load8(vox + base, len + base, o, lo, hi, v, l);
+                RawChunk<L, local> rc;
+                raw_load<L, local>(vox + base, loc + base, len + base, o, hi, rc);
+                hmask = window_chunk<L, local>(rc, o, lo, hi, v, l);
             }
-            uint32_t hmask = 0;                 // row heads of this chunk, bit k = segment k
-#pragma unroll
-            for (int k = 0; k < kPer; ++k) hmask |= (v[k] >> 31) << k;
             const int hcount = __builtin_popcount(hmask);
             T rv[kPer];
             if (MODE == kFwdGather) {       // per-segment gathers go out before any scan
@@ -739,15 +774,24 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             // rows this thread closes: the run open at its start (row hb-1) and its first own row
             // (row hb) are fetched now, under the segmented scan; further ones (rare) at the store
             const int32_t* rows = row_ray + k0 + rbase + hb;
+#if SPHRT_FWD_EMIT
+            // unconditional loads (clamped into row_ray's n_rays entries): no branch, so nothing
+            // waits for them before the first store
+            const int64_t ri = k0 + rbase + hb;
+            const int32_t r_prev = row_ray[imax64(ri - 1, 0)];
+            const int32_t r_first = row_ray[imin64(ri, n_rays - 1)];
+            const int32_t r_second = row_ray[imin64(ri + 1, n_rays - 1)];
+#else
             const int32_t r_prev = hb > 0 || base != base0 ? rows[-1] : 0;
             const int32_t r_first = hcount > 0 ? rows[0] : 0;
+#endif
             auto row_of = [&](int i) -> int64_t {     // ray of the row after i own heads
                 return i < 0 ? r_prev : i == 0 ? r_first : rows[i];
             };
             if (local) {
 #pragma unroll
                 for (int k = 0; k < kPer; ++k)
-                    rv[k] = l[k] != (L)0 ? dens[dens_index<T>(v[k] & ~kHead, cap)] : (T)0;
+                    rv[k] = lds_at<T>(dens, v[k]);   // masked slots: the zero granule
             }
             if (MODE == kFwdDynamic) {      // time slice of each segment's ray
                 int rank = 0;
@@ -768,12 +812,36 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             A p[kPer];
 #pragma unroll
             for (int k = 0; k < kPer; ++k) p[k] = (A)rv[k] * (A)l[k];
+#if SPHRT_FWD_EMIT == 2
+            // Row closes: at every head except the workgroup's first segment, and at position kPer
+            // in the thread holding the workgroup's last segment when this pass reaches it (masked
+            // slots carry no head and zero length, so no per-slot window test is needed).  With
+            // h1 < h2 < h3 the first three heads of the chunk (kPer when missing), the closes at
+            // h1, h2 and h3 store qa (run0 + the chunk's part before h1: the run open at the chunk
+            // start, in double), v1 and v2 (the runs [h1,h2), [h2,h3)) to rows hb-1, hb and hb+1;
+            // closes past h3 (chunks of 3+ heads) take a second walk.  One walk gives the runs and
+            // the thread's tail (its last run, the scan's input).
+            const uint32_t hm0 = hmask | (1u << kPer);
+            const uint32_t hm1 = hm0 & (hm0 - 1), hm2 = hm1 & (hm1 - 1);
+            const int h1 = __builtin_ctz(hm0);
+            const int h2 = __builtin_ctz(hm1 | (1u << kPer));
+            const int h3 = __builtin_ctz(hm2 | (1u << kPer));
+            A tail = (A)0, qa = (A)0, v1 = (A)0, v2 = (A)0;
+#pragma unroll
+            for (int k = 0; k <= kPer; ++k) {
+                qa = k == h1 ? tail : qa;
+                v1 = k == h2 ? tail : v1;
+                v2 = k == h3 ? tail : v2;
+                if (k < kPer) tail = ((hmask >> k) & 1 ? (A)0 : tail) + p[k];
+            }
+#else
             A tail = (A)0;
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 if ((hmask >> k) & 1) tail = (A)0;
                 tail += p[k];
             }
+#endif
             bool tot_has;
             double tot_sum;
             const double ex = block_excl_segsum1(hmask != 0, (double)tail, tot_has, tot_sum,
@@ -783,6 +851,61 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             // the run open at this thread's start: the segmented prefix of the earlier threads,
             // plus the carry of earlier passes when no earlier thread of this pass saw a head
             const double run0 = hb > 0 ? ex : carry + ex;
+#if SPHRT_FWD_EMIT == 2
+            uint32_t cmask = hmask;
+            {
+                const int first = lo - o, end = hi - o;
+                if (base == base0 && first >= 0 && first < kPer) cmask &= ~(1u << first);
+                if (base + kPass >= s1 && end > 0 && end <= kPer) cmask |= 1u << kPer;
+            }
+            if ((cmask >> h1) & 1) oc[r_prev] = (T)(run0 + (double)qa);
+            if (h2 != h1 && ((cmask >> h2) & 1)) oc[r_first] = (T)v1;
+            if (h3 != h2 && ((cmask >> h3) & 1)) oc[r_second] = (T)v2;
+            if (hcount > 2) {                         // rare: closes of the fourth and later runs
+                A q = (A)0;
+                int rank = 0;
+#pragma unroll
+                for (int k = 0; k <= kPer; ++k) {
+                    if (k > h3 && ((cmask >> k) & 1)) oc[rows[rank - 1]] = (T)q;
+                    if (k < kPer) {
+                        const bool h = (hmask >> k) & 1;
+                        rank += h;
+                        q = (h ? (A)0 : q) + p[k];
+                    }
+                }
+            }
+#elif SPHRT_FWD_EMIT == 1
+            // Row closes, as a bit mask over chunk positions 0..kPer: every head except the
+            // workgroup's first segment, and position kPer in the thread holding the workgroup's
+            // last segment when this pass reaches it (masked slots carry no head and zero length,
+            // so no per-slot window test is needed).  The close at the first head (or at kPer when
+            // the chunk has none) ends the run open at the chunk start: run0 + its own part, in
+            // double, stored once after the loop; every later close stores the thread-local run.
+            uint32_t cmask = hmask;
+            {
+                const int first = lo - o, end = hi - o;
+                if (base == base0 && first >= 0 && first < kPer) cmask &= ~(1u << first);
+                if (base + kPass >= s1 && end > 0 && end <= kPer) cmask |= 1u << kPer;
+            }
+            const int fo = __builtin_ctz(hmask | (1u << kPer));
+            A q = (A)0, qa = (A)0;
+            int rank = 0;                             // own heads passed
+#pragma unroll
+            for (int k = 0; k <= kPer; ++k) {
+                if (k == fo) {
+                    qa = q;
+                } else if ((cmask >> k) & 1) {        // rank >= 1: rows hb, hb+1 prefetched
+                    const int64_t ray = rank == 1 ? r_first : rank == 2 ? r_second : rows[rank - 1];
+                    oc[ray] = (T)q;
+                }
+                if (k < kPer) {
+                    const bool h = (hmask >> k) & 1;
+                    rank += h;
+                    q = (h ? (A)0 : q) + p[k];
+                }
+            }
+            if ((cmask >> fo) & 1) oc[r_prev] = (T)(run0 + (double)qa);
+#else
             A lr = (A)0;                              // this thread's part of the current run
             bool open0 = true;                        // the current run started before this thread
             int seen = -1;                            // own heads passed so far, minus one
@@ -801,6 +924,7 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
                 lr += p[k];
                 if (k == end - 1 && closes) oc[row_of(seen)] = value();   // the last row
             }
+#endif
             carry = tot_has ? tot_sum : carry + tot_sum;
             rbase += pass_heads;
         }
@@ -827,8 +951,8 @@ __global__ __launch_bounds__(kThreads) void adjoint_kernel(
     for (int64_t base = a0; base < s1; base += kPass) {
         uint32_t v[kPer];
         double l[kPer];
-        load8(vox + base, len + base, tid * kPer, (int)max<int64_t>(s0 - base, -1),
-              (int)min<int64_t>(s1 - base, (int64_t)kPass + 1), v, l);
+        load8(vox + base, len + base, tid * kPer, (int)imax64(s0 - base, -1),
+              (int)imin64(s1 - base, (int64_t)kPass + 1), v, l);
         int hcount = 0;
 #pragma unroll
         for (int k = 0; k < kPer; ++k) hcount += (v[k] & kHead) ? 1 : 0;
@@ -928,7 +1052,8 @@ extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, u
                                     int32_t* tab, int64_t tab_stride, void* stream) {
     if (!c || !c->vox || !blocks || !loc || !tab) return fail("incomplete CSR for the granule tables");
     if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
-    if (tab_stride < 1 || tab_stride > kMaxGran) return fail("bad granule table stride");
+    if (tab_stride < 1 || tab_stride > (kMaxGran + 63) / 64 * 64)
+        return fail("bad granule table stride");
     if (c->n_segments == 0) return 0;
     if (const int words = table_bitmap_words(c->n_cols)) {
         hipLaunchKernelGGL(local_table_bitmap_kernel<true>, dim3((unsigned)c->n_blocks),
@@ -959,7 +1084,7 @@ template <typename T>
 static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int64_t chan_stride,
                        int64_t div) {
     if (!c->loc || !c->tab || c->n_cols <= 0 || div > 0) return false;
-    if (c->tab_stride < 1 || (size_t)c->tab_stride * 4 * sizeof(T) > kTableLdsMax) return false;
+    if (c->tab_stride < 1 || (size_t)(c->tab_stride + 1) * 4 * sizeof(T) > kTableLdsMax) return false;
     if ((uintptr_t)density % (4 * sizeof(T)) != 0) return false;
     if (n_chan > 1 && chan_stride % 4 != 0) return false;
     return true;
@@ -976,7 +1101,7 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
     if (div > 0) {
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic>), grid, block, 0, st, SPHRT_FWD_ARGS, 0);
     } else if (use_tables(c, density, n_chan, chan_stride, div)) {
-        const size_t lds = (size_t)c->tab_stride * 4 * sizeof(T);
+        const size_t lds = (size_t)(c->tab_stride + 1) * 4 * sizeof(T);   // + zero granule
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable>), grid, block, lds, st, SPHRT_FWD_ARGS, 0);
         if (c->n_fallback > 0) {
             if (int e = check_launch("forward_kernel<table>")) return e;

@@ -116,7 +116,9 @@ def test_granule_tables(c2, gpu):
     s0, s1, n_tab = blocks[:, 2], blocks[:, 3], blocks[:, 5]
     assert (n_tab >= 0).all() and (n_tab <= s1 - s0).all() and csr['desc'].n_fallback == 0
     owner = np.repeat(np.arange(len(blocks)), s1 - s0)
-    slot = (loc & 0x7fff).astype(np.int64)
+    off = (loc & 0x7fff).astype(np.int64)   # byte offset in the float LDS image (zero granule first)
+    assert (off % 4 == 0).all() and (off >= 16).all()
+    slot = off // 4 - 4
     assert (slot // 4 < n_tab[owner]).all()
     v = (vox & 0x7fffffff).astype(np.int64)
     stride = csr['desc'].tab_stride
