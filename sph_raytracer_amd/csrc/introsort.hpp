@@ -19,96 +19,128 @@ struct Cand {
     uint32_t pad;
 };
 
-__device__ __forceinline__ bool cless(const Cand& a, const Cand& b) { return a.t < b.t; }
-__device__ __forceinline__ void cswap(Cand* v, int i, int j) {
-    Cand x = v[i];
-    v[i] = v[j];
-    v[j] = x;
+// The sort runs on any list with get/set of one element and operator< on the distance: an array
+// of Cand (one lane per list, workspace) or the distance / payload arrays of a wave's LDS list.
+struct CandList {
+    using E = Cand;
+    Cand* v;
+    __device__ E get(int i) const { return v[i]; }
+    __device__ void set(int i, const E& e) const { v[i] = e; }
+};
+struct SoaList {
+    struct E {
+        double t;
+        uint32_t pay;
+    };
+    double* t;
+    uint32_t* pay;
+    __device__ E get(int i) const { return E{t[i], pay[i]}; }
+    __device__ void set(int i, const E& e) const {
+        t[i] = e.t;
+        pay[i] = e.pay;
+    }
+};
+
+template <class E>
+__device__ __forceinline__ bool eless(const E& a, const E& b) { return a.t < b.t; }
+template <class V>
+__device__ __forceinline__ bool cless(const V& v, int a, int b) { return eless(v.get(a), v.get(b)); }
+template <class V>
+__device__ __forceinline__ void cswap(const V& v, int i, int j) {
+    const auto x = v.get(i);
+    v.set(i, v.get(j));
+    v.set(j, x);
 }
 
-__device__ inline void move_median_to_first(Cand* v, int res, int a, int b, int c) {
-    if (cless(v[a], v[b])) {
-        if (cless(v[b], v[c])) cswap(v, res, b);
-        else if (cless(v[a], v[c])) cswap(v, res, c);
+template <class V>
+__device__ inline void move_median_to_first(const V& v, int res, int a, int b, int c) {
+    if (cless(v, a, b)) {
+        if (cless(v, b, c)) cswap(v, res, b);
+        else if (cless(v, a, c)) cswap(v, res, c);
         else cswap(v, res, a);
-    } else if (cless(v[a], v[c])) {
+    } else if (cless(v, a, c)) {
         cswap(v, res, a);
-    } else if (cless(v[b], v[c])) {
+    } else if (cless(v, b, c)) {
         cswap(v, res, c);
     } else {
         cswap(v, res, b);
     }
 }
 
-__device__ inline int unguarded_partition(Cand* v, int first, int last, int piv) {
+template <class V>
+__device__ inline int unguarded_partition(const V& v, int first, int last, int piv) {
     while (true) {
-        while (cless(v[first], v[piv])) ++first;
+        while (cless(v, first, piv)) ++first;
         --last;
-        while (cless(v[piv], v[last])) --last;
+        while (cless(v, piv, last)) --last;
         if (!(first < last)) return first;
         cswap(v, first, last);
         ++first;
     }
 }
 
-__device__ inline void adjust_heap(Cand* v, int first, int hole, int len, Cand value) {
+template <class V, class E>
+__device__ inline void adjust_heap(const V& v, int first, int hole, int len, E value) {
     const int top = hole;
     int child = hole;
     while (child < (len - 1) / 2) {
         child = 2 * (child + 1);
-        if (cless(v[first + child], v[first + child - 1])) child--;
-        v[first + hole] = v[first + child];
+        if (cless(v, first + child, first + child - 1)) child--;
+        v.set(first + hole, v.get(first + child));
         hole = child;
     }
     if ((len & 1) == 0 && child == (len - 2) / 2) {
         child = 2 * (child + 1);
-        v[first + hole] = v[first + child - 1];
+        v.set(first + hole, v.get(first + child - 1));
         hole = child - 1;
     }
     int parent = (hole - 1) / 2;
-    while (hole > top && cless(v[first + parent], value)) {
-        v[first + hole] = v[first + parent];
+    while (hole > top && eless(v.get(first + parent), value)) {
+        v.set(first + hole, v.get(first + parent));
         hole = parent;
         parent = (hole - 1) / 2;
     }
-    v[first + hole] = value;
+    v.set(first + hole, value);
 }
 
 // std::__partial_sort(first, last, last) = make_heap + sort_heap
-__device__ inline void heap_sort(Cand* v, int first, int last) {
+template <class V>
+__device__ inline void heap_sort(const V& v, int first, int last) {
     const int len = last - first;
     if (len >= 2) {
         for (int parent = (len - 2) / 2;; --parent) {
-            adjust_heap(v, first, parent, len, v[first + parent]);
+            adjust_heap(v, first, parent, len, v.get(first + parent));
             if (parent == 0) break;
         }
     }
     while (last - first > 1) {
         --last;
-        Cand value = v[last];
-        v[last] = v[first];
+        const auto value = v.get(last);
+        v.set(last, v.get(first));
         adjust_heap(v, first, 0, last - first, value);
     }
 }
 
-__device__ inline void unguarded_linear_insert(Cand* v, int last) {
-    Cand val = v[last];
+template <class V>
+__device__ inline void unguarded_linear_insert(const V& v, int last) {
+    const auto val = v.get(last);
     int next = last - 1;
-    while (cless(val, v[next])) {
-        v[last] = v[next];
+    while (eless(val, v.get(next))) {
+        v.set(last, v.get(next));
         last = next;
         --next;
     }
-    v[last] = val;
+    v.set(last, val);
 }
 
-__device__ inline void insertion_sort(Cand* v, int first, int last) {
+template <class V>
+__device__ inline void insertion_sort(const V& v, int first, int last) {
     if (first == last) return;
     for (int i = first + 1; i != last; ++i) {
-        if (cless(v[i], v[first])) {
-            Cand val = v[i];
-            for (int k = i; k > first; --k) v[k] = v[k - 1];
-            v[first] = val;
+        if (cless(v, i, first)) {
+            const auto val = v.get(i);
+            for (int k = i; k > first; --k) v.set(k, v.get(k - 1));
+            v.set(first, val);
         } else {
             unguarded_linear_insert(v, i);
         }
@@ -117,7 +149,8 @@ __device__ inline void insertion_sort(Cand* v, int first, int last) {
 
 constexpr int kIntroThreshold = 16;
 
-__device__ inline void introsort(Cand* v, int n) {
+template <class V>
+__device__ inline void introsort(const V& v, int n) {
     if (n <= 1) return;
     const int lg = 31 - __builtin_clz((unsigned)n);
     // __introsort_loop recurses on [cut, last) and iterates on [first, cut); the two ranges are

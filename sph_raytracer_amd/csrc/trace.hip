@@ -21,7 +21,7 @@
 // boundary (e.g. an orbit view at azimuth 0 with a boundary at 0).  The wave path detects such
 // tie groups and defers the ray to exact_kernel, which rebuilds all K candidates in the
 // reference's concatenation order, runs the emulated introsort (introsort.hpp) and walks the
-// sorted list exactly like trace_indices.  Deferred rays are rare; the list lives in workspace.
+// sorted list exactly like trace_indices, one wave per deferred ray with its list in LDS.
 #include <climits>
 
 #include "common.hpp"
@@ -37,7 +37,7 @@ constexpr int kWavesPerBlock = 4;
 // Diagnostic build only (-DSPHRT_TRACE_STAMPS, tools/trace_phases.py): s_memtime cycles per trace
 // phase summed over all hit rays (0 solve+push, 1 sort, 2 tie check, 3 fill/lengths, 4 emit).
 #ifdef SPHRT_TRACE_STAMPS
-__device__ unsigned long long g_trace_cycles[8];
+__device__ unsigned long long g_trace_cycles[16];   // 8..12: exact_wave_kernel
 #define TRACE_T(var) const uint64_t var = __builtin_amdgcn_s_memtime()
 #define TRACE_ADD(i, a, b) \
     do { if (lane == 0) atomicAdd(&g_trace_cycles[i], (unsigned long long)((b) - (a))); } while (0)
@@ -611,101 +611,367 @@ __global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int fa
     }
 }
 
-// ---- exact path for deferred rays: one lane per ray, the reference algorithm verbatim --------
+// ---- exact path for deferred rays: one wave per ray, the reference algorithm verbatim -----
+// Candidates in the reference's concatenation order (raytracer.py:92, 117-122), solved by the
+// lanes in parallel.  Returns through `put(c, t, region)`.
+template <class Put>
+__device__ __forceinline__ void exact_candidates(const GridDev& G, const RayGeo& g, int lane,
+                                                 Put put) {
+    const int nbr = G.nbr, nbe = G.nbe, nba = G.nba;
+    const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe;
+    for (int j = lane; j < nbr; j += 64) {
+        double ti, to;
+        int ri, ro, ni, no;
+        sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
+        put(j, ti, ri);
+        put(nbr + j, to, ro);
+    }
+    for (int j = lane; j < nbe; j += 64) {
+        double ta, tb;
+        int ra, rb, na_, nb_;
+        cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
+        put(r_lim + j, ta, ra);
+        put(r_lim + nbe + j, tb, rb);
+    }
+    for (int j = lane; j < nba; j += 64) {
+        double t;
+        int r, ng;
+        plane_solve(G, g, j, t, r, ng);
+        put(e_lim + j, t, r);
+    }
+    if (lane == 0) put(G.K - 1, 0.0, 0);
+}
+
+// Forward fill + diff + masking over the sorted list (raytracer.py:126, 140-173), one lane.
+template <int MODE, typename T, class V>
+__device__ void exact_walk(const GridDev& G, const TraceOut<T>& o, int64_t ray, const int* s,
+                           const V& v) {
+    const int K = G.K, r_lim = 2 * G.nbr, e_lim = 2 * G.nbr + 2 * G.nbe;
+    int64_t c_lo = 0, c_hi = o.n_chan;
+    if (MODE == MODE_INTEGRATE && o.ray_chan_div > 0) {
+        c_lo = ray / o.ray_chan_div;
+        c_hi = c_lo + 1;
+    }
+    if (MODE != MODE_INTEGRATE) c_hi = c_lo + 1;
+    for (int64_t c = c_lo; c < c_hi; ++c) {
+        int cr = s[0], ce = s[1], ca = s[2];
+        int64_t nseg = 0;
+        double acc = 0.0;
+        const int64_t base = MODE == MODE_FILL ? o.row_ptr[ray] : 0;
+        auto cur = v.get(0);
+        for (int k = 0; k < K; ++k) {
+            const double t = cur.t;
+            const uint32_t p = cur.pay;
+            if (!(t < 0.0)) {
+                const int cand = (int)(p >> 16);
+                const int reg = (int)(p & 0xffffu) - 2;
+                if (cand == K - 1) { cr = s[0]; ce = s[1]; ca = s[2]; }
+                else if (cand < r_lim) cr = reg;
+                else if (cand < e_lim) { if (reg != -2) ce = reg; }
+                else if (reg != -2) ca = reg;
+            }
+            if (k + 1 < K) cur = v.get(k + 1);
+            const double tn = k + 1 < K ? cur.t : kInf;
+            const double len = tn - t;
+            if (!(len > 0.0) || !__builtin_isfinite(len)) continue;
+            if (cr < 0 || cr >= G.nr || ce < 0 || ce >= G.ne || ca < 0 || ca >= G.na) continue;
+            const int vx = (cr * G.ne + ce) * G.na + ca;
+            if (MODE == MODE_FILL) {
+                o.vox[base + nseg] = vx;
+                o.len[base + nseg] = len;
+            } else if (MODE == MODE_INTEGRATE) {
+                acc += (double)o.density[c * o.chan_stride + vx] * len;
+            }
+            ++nseg;
+        }
+        if (MODE == MODE_COUNT) o.counts[ray] = (int32_t)nseg;
+        if (MODE == MODE_INTEGRATE) {
+            const int64_t oc = o.ray_chan_div > 0 ? 0 : c;
+            o.out[oc * o.out_chan_stride + ray] = (T)acc;
+        }
+    }
+}
+
+// The same walk, wave-parallel over 64-entry chunks of the sorted list (ts, ps): "last update
+// wins" scans for the three region rows, differences, and in-order compaction of the non-zero
+// in-grid segments into (seg_vox, seg_len) (LDS, K entries), then count / copy / integrate.
+template <int MODE, typename T>
+__device__ void exact_walk_wave(const GridDev& G, const TraceOut<T>& o, int64_t ray, const int* s,
+                                const double* ts, const uint32_t* ps, int32_t* seg_vox,
+                                double* seg_len, int lane) {
+    const int K = G.K, r_lim = 2 * G.nbr, e_lim = 2 * G.nbr + 2 * G.nbe;
+    int cr = s[0], ce = s[1], ca = s[2];
+    int nseg = 0;
+    for (int c0 = 0; c0 < K; c0 += 64) {
+        const int k = c0 + lane;
+        const bool real = k < K;
+        const double t = real ? ts[k] : kInf;
+        const double tn = k + 1 < K ? ts[k + 1] : kInf;
+        const uint32_t p = real ? ps[k] : 0u;
+        int ur = kNone, ue = kNone, ua = kNone;
+        if (real && !(t < 0.0)) {
+            const int cand = (int)(p >> 16);
+            const int reg = (int)(p & 0xffffu) - 2;
+            if (cand == K - 1) {
+                ur = s[0]; ue = s[1]; ua = s[2];
+            } else if (cand < r_lim) {
+                ur = reg;
+            } else if (cand < e_lim) {
+                if (reg != -2) ue = reg;
+            } else if (reg != -2) {
+                ua = reg;
+            }
+        }
+        ur = scan_last(ur, lane);
+        ue = scan_last(ue, lane);
+        ua = scan_last(ua, lane);
+        if (ur == kNone) ur = cr;
+        if (ue == kNone) ue = ce;
+        if (ua == kNone) ua = ca;
+        cr = __builtin_amdgcn_readlane(ur, 63);
+        ce = __builtin_amdgcn_readlane(ue, 63);
+        ca = __builtin_amdgcn_readlane(ua, 63);
+        const double len = tn - t;
+        const bool ok = real && len > 0.0 && __builtin_isfinite(len) && ur >= 0 && ur < G.nr &&
+                        ue >= 0 && ue < G.ne && ua >= 0 && ua < G.na;
+        const uint64_t m = __ballot(ok);
+        if (MODE != MODE_COUNT && ok) {
+            const int pos = nseg + __popcll(m & lanemask_lt(lane));
+            seg_len[pos] = len;
+            seg_vox[pos] = (ur * G.ne + ue) * G.na + ua;
+        }
+        nseg += __popcll(m);
+    }
+    wave_sync();
+    if (MODE == MODE_COUNT) {
+        if (lane == 0) o.counts[ray] = nseg;
+    } else if (MODE == MODE_FILL) {
+        const int64_t r0 = o.row_ptr[ray];
+        for (int q = lane; q < nseg; q += 64) {
+            o.vox[r0 + q] = seg_vox[q];
+            o.len[r0 + q] = seg_len[q];
+        }
+    } else {
+        int64_t c_lo = 0, c_hi = o.n_chan;
+        if (o.ray_chan_div > 0) {
+            c_lo = ray / o.ray_chan_div;
+            c_hi = c_lo + 1;
+        }
+        for (int64_t c = c_lo; c < c_hi; ++c) {
+            const T* rho = o.density + c * o.chan_stride;
+            double acc = 0.0;
+            for (int q = lane; q < nseg; q += 64) acc += (double)rho[seg_vox[q]] * seg_len[q];
+            acc = wave_sum(acc);
+            const int64_t oc = (o.ray_chan_div > 0) ? 0 : c;
+            if (lane == 0) o.out[oc * o.out_chan_stride + ray] = (T)acc;
+        }
+    }
+}
+
+// Large K (the wave list does not fit kExactLdsMax): lane 0 sorts the ray's list serially in the
+// wave's slice of workspace.
 template <int MODE, typename T>
 __global__ __launch_bounds__(64) void exact_kernel(GridDev G, RaysDev R, TraceOut<T> o,
                                                    Cand* scratch) {
-    const int64_t lanes = (int64_t)gridDim.x * blockDim.x;
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    Cand* v = scratch + gid * G.K;
+    const int lane = threadIdx.x;
+    const CandList v{scratch + (int64_t)blockIdx.x * G.K};
     const int64_t count = (int64_t)*o.n_deferred;
-    const int nbr = G.nbr, nbe = G.nbe, nba = G.nba, K = G.K;
-    const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe;
-    for (int64_t q = gid; q < count; q += lanes) {
+    for (int64_t q = blockIdx.x; q < count; q += gridDim.x) {
         const int64_t ray = o.deferred[q];
         double x[3], d[3];
         int s[3];
         load_ray(R, ray, x, d, s);
         const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
-        auto put = [&](int c, double t, int reg) {
-            v[c].t = t;
-            v[c].pay = ((uint32_t)c << 16) | (uint32_t)(reg + 2);
-        };
-        // candidates in the reference's concatenation order (raytracer.py:92, 117-122)
-        for (int j = 0; j < nbr; ++j) {
-            double ti, to;
-            int ri, ro, ni, no;
-            sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
-            put(j, ti, ri);
-            put(nbr + j, to, ro);
+        exact_candidates(G, g, lane, [&](int c, double t, int reg) {
+            v.set(c, Cand{t, ((uint32_t)c << 16) | (uint32_t)(reg + 2), 0u});
+        });
+        __syncthreads();
+        if (lane == 0) {
+            introsort(v, G.K);
+            exact_walk<MODE, T>(G, o, ray, s, v);
         }
-        for (int j = 0; j < nbe; ++j) {
-            double ta, tb;
-            int ra, rb, na_, nb_;
-            cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
-            put(r_lim + j, ta, ra);
-            put(r_lim + nbe + j, tb, rb);
-        }
-        for (int j = 0; j < nba; ++j) {
-            double t;
-            int r, ng;
-            plane_solve(G, g, j, t, r, ng);
-            put(e_lim + j, t, r);
-        }
-        put(K - 1, 0.0, 0);
-        introsort(v, K);
-        // forward fill + diff + masking (raytracer.py:126, 140-173)
-        int64_t c_lo = 0, c_hi = o.n_chan;
-        if (MODE == MODE_INTEGRATE && o.ray_chan_div > 0) {
-            c_lo = ray / o.ray_chan_div;
-            c_hi = c_lo + 1;
-        }
-        if (MODE != MODE_INTEGRATE) c_hi = c_lo + 1;
-        for (int64_t c = c_lo; c < c_hi; ++c) {
-            int cr = s[0], ce = s[1], ca = s[2];
-            int64_t nseg = 0;
-            double acc = 0.0;
-            const int64_t base = MODE == MODE_FILL ? o.row_ptr[ray] : 0;
-            for (int k = 0; k < K; ++k) {
-                const double t = v[k].t;
-                const uint32_t p = v[k].pay;
-                if (!(t < 0.0)) {
-                    const int cand = (int)(p >> 16);
-                    const int reg = (int)(p & 0xffffu) - 2;
-                    if (cand == K - 1) { cr = s[0]; ce = s[1]; ca = s[2]; }
-                    else if (cand < r_lim) cr = reg;
-                    else if (cand < e_lim) { if (reg != -2) ce = reg; }
-                    else if (reg != -2) ca = reg;
-                }
-                const double tn = k + 1 < K ? v[k + 1].t : kInf;
-                const double len = tn - t;
-                if (!(len > 0.0) || !__builtin_isfinite(len)) continue;
-                if (cr < 0 || cr >= G.nr || ce < 0 || ce >= G.ne || ca < 0 || ca >= G.na) continue;
-                const int vx = (cr * G.ne + ce) * G.na + ca;
-                if (MODE == MODE_FILL) {
-                    o.vox[base + nseg] = vx;
-                    o.len[base + nseg] = len;
-                } else if (MODE == MODE_INTEGRATE) {
-                    acc += (double)o.density[c * o.chan_stride + vx] * len;
-                }
-                ++nseg;
+        __syncthreads();
+    }
+}
+
+// The emulated introsort, wave-parallel (the list in LDS).  Same result as introsort():
+//  * partition: with piv = v[first] after the median-of-three, the left scan's stops are the
+//    positions i in (first, last) with !(v[i] < piv), ascending (L[0], L[1], ...), the right
+//    scan's the positions j in [first, last) with !(piv < v[j]), descending (R[0], ...).  Swap k
+//    exchanges L[k] and R[k] as long as L[k] < R[k]; with k* the first k where that fails
+//    (k* = #{left stops i of rank a : #right stops after i > a}), the cut is min(L[k*], R[k*-1])
+//    (L[k*] = +inf when there is none; L[0] when k* = 0).  Positions between the pointers are
+//    untouched until they cross, so the stop lists of the unswapped array decide everything.
+//  * the final insertion sort never moves an element past an equal one, and after the partition
+//    phase no element is smaller than one in an earlier leaf: it is a stable sort of each leaf
+//    (range of <= 16 left by the loop; heap-sorted ranges are already sorted), computed as ranks.
+//  Rays with a NaN distance (none expected: the solvers map NaN to +inf) take the serial sort.
+constexpr size_t kExactWaveEntryBytes = 2 * 8 + 5 * 4;   // per candidate, see the layout below
+constexpr int kExactStack = 64;                         // partition stack (depth <= 2 log2 K)
+constexpr size_t kExactWaveLdsMax = 64 * 1024;
+__host__ __device__ constexpr size_t exact_wave_lds(int K) {
+    return (size_t)K * kExactWaveEntryBytes + 3 * kExactStack * sizeof(int);
+}
+
+template <int MODE, typename T>
+__global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char xw_lds[];
+    const int K = G.K;
+    double* tk = reinterpret_cast<double*>(xw_lds);   // list (distance), current order
+    double* ts = tk + K;                              // sorted list
+    uint32_t* pk = reinterpret_cast<uint32_t*>(ts + K);
+    uint32_t* ps = pk + K;
+    int32_t* lpos = reinterpret_cast<int32_t*>(ps + K);   // left stops by rank
+    int32_t* rpos = lpos + K;                              // right stops by rank
+    uint32_t* leaf = reinterpret_cast<uint32_t*>(rpos + K);   // leaf range lo | hi << 16
+    // the partition stack in LDS (uniform; a private array would live in scratch memory, one
+    // global round trip per push or pop)
+    int* st_first = reinterpret_cast<int*>(leaf + K);
+    int* st_last = st_first + kExactStack;
+    int* st_depth = st_last + kExactStack;
+    const SoaList v{tk, pk};
+    const int lane = threadIdx.x;
+    const uint64_t below = lanemask_lt(lane);
+    const int64_t count = (int64_t)*o.n_deferred;
+    for (int64_t q = blockIdx.x; q < count; q += gridDim.x) {
+        const int64_t ray = o.deferred[q];
+        double x[3], d[3];
+        int s[3];
+        load_ray(R, ray, x, d, s);
+        TRACE_T(x0);
+        const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
+        exact_candidates(G, g, lane, [&](int c, double t, int reg) {
+            tk[c] = t;
+            pk[c] = ((uint32_t)c << 16) | (uint32_t)(reg + 2);
+        });
+        bool nan = false;
+        for (int p = lane; p < K; p += 64) leaf[p] = (uint32_t)p | ((uint32_t)(p + 1) << 16);
+        wave_sync();
+        for (int p = lane; p < K; p += 64) nan |= __builtin_isnan(tk[p]);
+        if (__ballot(nan) != 0) {
+            if (lane == 0) {
+                introsort(v, K);
+                exact_walk<MODE, T>(G, o, ray, s, v);
             }
-            if (MODE == MODE_COUNT) o.counts[ray] = (int32_t)nseg;
-            if (MODE == MODE_INTEGRATE) {
-                const int64_t oc = o.ray_chan_div > 0 ? 0 : c;
-                o.out[oc * o.out_chan_stride + ray] = (T)acc;
+            wave_sync();
+            continue;
+        }
+        TRACE_T(x1);
+        TRACE_ADD(8, 0, 1);
+        TRACE_ADD(9, x0, x1);
+        // ---- partition phase (uniform control flow) ----
+        int sp = 0;
+        int first = 0, last = K, depth = 2 * (31 - __builtin_clz((unsigned)max(K, 1)));
+        bool have = K > 1;
+        while (have) {
+            while (last - first > kIntroThreshold) {
+                if (depth == 0) {                      // rare: the reference's heapsort
+                    if (lane == 0) heap_sort(v, first, last);
+                    wave_sync();
+                    first = last;                      // sorted: no leaf
+                    break;
+                }
+                --depth;
+                const int mid = first + (last - first) / 2;
+                if (lane == 0) move_median_to_first(v, first, first + 1, mid, last - 1);
+                wave_sync();
+                const double piv = tk[first];
+                // stop counts
+                int n_l = 0, n_r = 0;
+                for (int c0 = first; c0 < last; c0 += 64) {
+                    const int p = c0 + lane;
+                    const bool in = p < last;
+                    const double t = in ? tk[p] : 0.0;
+                    n_l += __builtin_popcountll(__ballot(in && p > first && !(t < piv)));
+                    n_r += __builtin_popcountll(__ballot(in && !(piv < t)));
+                }
+                // ranks, stop lists and k*
+                int a0 = 0, r0 = 0, ks = 0;
+                for (int c0 = first; c0 < last; c0 += 64) {
+                    const int p = c0 + lane;
+                    const bool in = p < last;
+                    const double t = in ? tk[p] : 0.0;
+                    const bool is_l = in && p > first && !(t < piv);
+                    const bool is_r = in && !(piv < t);
+                    const uint64_t bl = __ballot(is_l), br = __ballot(is_r);
+                    const int a = a0 + __builtin_popcountll(bl & below);   // left rank
+                    const int rb = r0 + __builtin_popcountll(br & below);  // right stops before p
+                    if (is_l) lpos[a] = p;
+                    if (is_r) rpos[n_r - 1 - rb] = p;
+                    const int after = n_r - rb - (is_r ? 1 : 0);          // right stops after p
+                    ks += __builtin_popcountll(__ballot(is_l && after > a));
+                    a0 += __builtin_popcountll(bl);
+                    r0 += __builtin_popcountll(br);
+                }
+                wave_sync();
+                int cut;
+                if (ks < n_l) cut = ks > 0 ? min(lpos[ks], rpos[ks - 1]) : lpos[0];
+                else cut = rpos[ks - 1];
+                for (int k = lane; k < ks; k += 64) {
+                    const int i = lpos[k], j = rpos[k];
+                    const double ti = tk[i], tj = tk[j];
+                    const uint32_t pi = pk[i], pj = pk[j];
+                    tk[i] = tj; pk[i] = pj;
+                    tk[j] = ti; pk[j] = pi;
+                }
+                if (lane == 0) {
+                    st_first[sp] = cut;
+                    st_last[sp] = last;
+                    st_depth[sp] = depth;
+                }
+                ++sp;
+                last = cut;
+                wave_sync();
+            }
+            if (last - first > 1) {                    // a leaf: its range, for the final ranks
+                const uint32_t code = (uint32_t)first | ((uint32_t)last << 16);
+                for (int p = first + lane; p < last; p += 64) leaf[p] = code;
+            }
+            have = sp > 0;
+            if (have) {
+                --sp;
+                first = st_first[sp];
+                last = st_last[sp];
+                depth = st_depth[sp];
             }
         }
+        wave_sync();
+        TRACE_T(x2);
+        TRACE_ADD(10, x1, x2);
+        // ---- final insertion sort = stable sort inside each leaf, as ranks ----
+        for (int p = lane; p < K; p += 64) {
+            const uint32_t code = leaf[p];
+            const int lo = (int)(code & 0xffffu), hi = (int)(code >> 16);
+            const double t = tk[p];
+            int r = lo;
+            for (int j = lo; j < hi; ++j) {
+                const double u = tk[j];
+                r += (u < t || (u == t && j < p)) ? 1 : 0;
+            }
+            ts[r] = t;
+            ps[r] = pk[p];
+        }
+        wave_sync();
+        TRACE_T(x3);
+        TRACE_ADD(11, x2, x3);
+        // (the pre-sort list and the left-stop list are free now: compacted segments go there)
+        exact_walk_wave<MODE, T>(G, o, ray, s, ts, ps, lpos, tk, lane);
+        wave_sync();
+        TRACE_T(x4);
+        TRACE_ADD(12, x3, x4);
     }
 }
 
 // ---- host launchers ----------------------------------------------------------------------
 static int trace_cap(const GridDev& G) { return ((G.K + 63) / 64) * 64; }
-constexpr int kExactBlocks = 64;     // 4096 lanes for the (rare) deferred rays
+constexpr int kExactBlocks = 4096;   // one wave per deferred ray, 16 per CU
 constexpr size_t kWsHead = 256;      // deferred counter, padded
 
-static size_t exact_scratch_bytes(const GridDev& G) {
-    return (size_t)kExactBlocks * 64 * G.K * sizeof(Cand);
+static bool exact_in_lds(const GridDev& G) {
+    return exact_wave_lds(G.K) <= kExactWaveLdsMax;
+}
+static size_t exact_scratch_bytes(const GridDev& G) {   // lists of large-K grids, one per wave
+    return exact_in_lds(G) ? 0 : (size_t)kExactBlocks * G.K * sizeof(Cand);
 }
 static size_t hits_bytes(int64_t n) { return (((size_t)n * sizeof(int32_t) + 255) / 256) * 256; }
 static size_t workspace_bytes(const GridDev& G, int64_t n) {
@@ -744,8 +1010,12 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,
                        R, o, cap);
     if (int e = check_launch("trace_kernel")) return e;
-    hipLaunchKernelGGL((exact_kernel<MODE, T>), dim3(kExactBlocks), dim3(64), 0, st, G, R, o,
-                       scratch);
+    if (exact_in_lds(G))
+        hipLaunchKernelGGL((exact_wave_kernel<MODE, T>), dim3(kExactBlocks), dim3(64),
+                           exact_wave_lds(G.K), st, G, R, o);
+    else
+        hipLaunchKernelGGL((exact_kernel<MODE, T>), dim3(kExactBlocks), dim3(64), 0, st, G, R, o,
+                           scratch);
     return check_launch("exact_kernel");
 }
 
@@ -756,10 +1026,10 @@ using namespace sphrt;
 #ifdef SPHRT_TRACE_STAMPS
 extern "C" int sphrt_diag_trace_cycles(unsigned long long* host, int reset) {
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[16] = {};
         return hipMemcpyToSymbol(HIP_SYMBOL(g_trace_cycles), z, sizeof(z)) == hipSuccess ? 0 : 1;
     }
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace_cycles), 8 * sizeof(unsigned long long), 0,
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace_cycles), 16 * sizeof(unsigned long long), 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 #endif

@@ -257,3 +257,52 @@ def test_gd_retrieval_decreases_loss(gpu):
     fid = list(losses.values())[0]
     assert fid[-1] < 0.2 * fid[0]
     assert y.shape == meas.shape
+
+
+def _deferred_count(grid, geom, gpu):
+    """Rays the wave trace defers to the exact (emulated introsort) path: the trace workspace's
+    counter after a count pass (trace.hip launch_trace)."""
+    from sph_raytracer_amd import _lib, raytracer as rt
+    lib = _lib.load()
+    plan = rt._Plan(grid, gpu)
+    batch = rt._RayBatch(grid, geom.ray_starts, rt._geom_rays(geom, gpu), gpu)
+    counts = tr.empty(max(batch.n, 1), dtype=tr.int32, device=gpu)
+    tws = rt._workspace(lib, plan, batch.n, gpu)
+    _lib.check(lib.sphrt_trace_count(plan.handle, batch.desc, _lib.ptr(counts), _lib.ptr(tws),
+                                     tws.numel(), _lib.stream_of(gpu)), 'sphrt_trace_count')
+    return int(tws[:8].view(tr.int64).item())
+
+
+@pytest.mark.parametrize('shape,a_full', [((64, 64, 64), False), ((17, 9, 30), False),
+                                          ((12, 20, 7), True), ((40, 3, 100), True)])
+def test_exact_tie_rays_vs_oracle(shape, a_full, gpu):
+    """Rays that hit exact ties (through the origin: every cone and half-plane crossed at one
+    distance; starts on the a = 0 half-plane) take the exact path, whose emulated introsort
+    decides the voxel after each tie group.  Compared with the IEEE-sqrt C oracle under the
+    parity contract (golden_cases.compare_segments: voxel sequences exact, lengths 1e-12)."""
+    from oracle import oracle
+    from sph_raytracer_amd import ConeCircGeom, Operator, SphericalGrid, ViewGeom
+    from sph_raytracer_amd.raytracer import find_starts
+    size_a = (0, 2 * tr.pi) if a_full else (-tr.pi, tr.pi)
+    grid = SphericalGrid(shape=shape, size_a=size_a)
+    geoms = [ConeCircGeom(shape=(6, 16), pos=(5 * tr.cos(th), 5 * tr.sin(th), 1), fov=(0, 40))
+             for th in tr.linspace(0, 2 * tr.pi, 7)]
+    rng = np.random.default_rng(3)
+    pos = tr.from_numpy(rng.normal(size=(40, 3)) * 2.0)
+    geoms.append(ViewGeom(pos[:, None, :], -pos[:, None, :]))           # aimed at the origin
+    xs_in = tr.from_numpy(np.c_[rng.uniform(0.1, 0.9, 30), np.zeros(30), rng.uniform(-.5, .5, 30)])
+    geoms.append(ViewGeom(xs_in[:, None, :], tr.from_numpy(rng.normal(size=(30, 1, 3)))))
+    for gm in geoms:
+        op = Operator(grid, gm, device=gpu)
+        oracle.use_mkl_sqrt(False)
+        g = oracle.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy())
+        xs = np.broadcast_to(gm.ray_starts.numpy(), gm.rays.shape).reshape(-1, 3).copy()
+        d = gm.rays.numpy().reshape(-1, 3).copy()
+        ptr, vox, seg = oracle.trace_segments(g, xs, d, find_starts(grid, tr.from_numpy(xs)).numpy())
+        got = tuple(t.cpu().numpy() for t in op.segments())
+        msg = gc.compare_segments((ptr, vox, seg), got, 5.1, f'{shape} {type(gm).__name__}')
+        assert msg is None, msg
+    # the geometry really exercises the exact path (rays through the origin, starts on a = 0)
+    deferred = [_deferred_count(grid, gm, gpu) for gm in geoms]
+    print('deferred rays per view:', deferred)
+    assert sum(deferred) > 0
