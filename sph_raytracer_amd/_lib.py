@@ -105,6 +105,30 @@ def load():
     return lib
 
 
+_fast = None
+FAST_PATH = os.path.join(_HERE, 'lib', '_sphrt_fast.so')
+
+
+def load_fast():
+    """The CPython steady-state entry (csrc/fastpath.cpp), or None when it was not built (then
+    Operator.__call__ binds through ctypes only: same kernels, more host time per call)."""
+    global _fast
+    if _fast is None:
+        _fast = False
+        if os.path.exists(FAST_PATH) and os.environ.get('SPHRT_NO_FASTPATH') != '1':
+            import importlib.util
+            spec = importlib.util.spec_from_file_location('_sphrt_fast', FAST_PATH)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            _fast = mod
+    return _fast or None
+
+
+def address(fn):
+    """Address of a ctypes-bound C function (for the fast path's bindings)."""
+    return ctypes.cast(fn, ctypes.c_void_p).value
+
+
 def check(status, what):
     if status != 0:
         msg = load().sphrt_last_error().decode(errors='replace')

@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, 'csrc')
 OUT = os.path.join(HERE, 'lib', 'libsphrt.so')
+FAST_OUT = os.path.join(HERE, 'lib', '_sphrt_fast.so')   # CPython entry for steady-state calls
 SOURCES = ['api.hip', 'trace.hip', 'apply.hip', 'transpose.hip', 'rays.hip']
 HEADERS = ['common.hpp', 'solve.hpp', 'introsort.hpp']
 ARCH = os.environ.get('SPHRT_ARCH', 'gfx950')
@@ -43,8 +44,39 @@ def _stale(out):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def fast_command(out=FAST_OUT):
+    """g++ for csrc/fastpath.cpp: host code against torch's C++ / CPython API (torch headers of the
+    interpreter that builds it), linked to the torch libraries it is loaded next to."""
+    import sysconfig
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    return ['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-D__HIP_PLATFORM_AMD__=1',
+            '-DUSE_ROCM=1', '-I', os.path.join(tdir, 'include'),
+            '-I', os.path.join(tdir, 'include', 'torch', 'csrc', 'api', 'include'),
+            '-I', '/opt/rocm/include', '-I', sysconfig.get_paths()['include'],
+            os.path.join(CSRC, 'fastpath.cpp'), '-L', os.path.join(tdir, 'lib'),
+            '-ltorch_python', '-ltorch', '-ltorch_cpu', '-lc10', '-lc10_hip',
+            f'-Wl,-rpath,{os.path.join(tdir, "lib")}', '-o', out]
+
+
+def build_fast(force=False, verbose=False):
+    src = os.path.join(CSRC, 'fastpath.cpp')
+    if not force and os.path.exists(FAST_OUT) and \
+            os.path.getmtime(FAST_OUT) >= max(os.path.getmtime(src), os.path.getmtime(__file__)):
+        return FAST_OUT
+    cmd = fast_command(FAST_OUT + '.tmp')
+    if verbose:
+        print(' '.join(cmd))
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f'g++ (fastpath.cpp) failed ({res.returncode}):\n{res.stderr[-4000:]}')
+    os.replace(FAST_OUT + '.tmp', FAST_OUT)
+    return FAST_OUT
+
+
 def build(force=False, verbose=False):
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    build_fast(force, verbose)
     if not force and not _stale(OUT):
         return OUT
     cmd = command()

@@ -358,6 +358,7 @@ class Operator:
             raise NotImplementedError('invalid=True (keep invalid segments) is not supported')
         self._csr = None
         self._fast = {}     # (shape, dtype, device) -> bound forward launch (steady-state calls)
+        self._fastc = None  # the same bindings inside the CPython entry (csrc/fastpath.cpp)
         # 'transpose': deterministic voxel-major adjoint (default); 'atomic': float64 atomics
         # (used anyway when views are paired with time slices)
         self.adjoint_mode = 'transpose'
@@ -421,6 +422,12 @@ class Operator:
     def __call__(self, density):
         """Line integrals of ``density`` along every ray: (C..., *geom.shape) for a static grid,
         (T, H, W) for a dynamic one (raytracer.py:692-713).  Differentiable in ``density``."""
+        fc = self._fastc
+        if fc is not None:
+            # steady state in one C call (bound shapes/dtypes, contiguous, on the GPU, no grad)
+            out = self._fastfn(fc, density)
+            if out is not None:
+                return out
         if self._csr is None:
             raise RuntimeError('Operator was built with _compute=False')
         if type(density) is tr.Tensor and not (density.requires_grad and tr.is_grad_enabled()):
@@ -493,6 +500,14 @@ class Operator:
             self._fast[(density.shape, density.dtype, density.device)] = (
                 fn, ctypes.byref(self._csr['desc']), n_chan, math.prod(self.grid.shape[-3:]), div,
                 n, alloc, tuple(out_shape))
+            fast = _lib.load_fast()
+            if fast is not None:
+                if self._fastc is None:
+                    self._fastfn = fast.forward
+                    self._fastc = fast.new(_lib.address(lib.sphrt_last_error))
+                fast.add(self._fastc, tuple(density.shape), cdt == tr.float64, dev.index,
+                         _lib.address(fn), ctypes.addressof(self._csr['desc']), n_chan,
+                         math.prod(self.grid.shape[-3:]), div, n, tuple(out_shape))
         out = out.view(out_shape)
         if out.device != density.device or cdt != in_dtype:
             out = out.to(device=density.device, dtype=in_dtype)

@@ -245,3 +245,19 @@ def test_library_builds_and_exports_header():
     lib = _lib.load()
     assert lib.sphrt_version().startswith(b'sph_raytracer_amd')
     assert lib.sphrt_scan_workspace_bytes(10_000) > 0
+
+
+def test_fastpath_entry_builds_and_declines_foreign_inputs():
+    """csrc/fastpath.cpp (the CPython entry for steady-state Operator calls) builds against the
+    installed torch, loads, and returns None for anything it has no binding for (CPU tensors,
+    non-tensors), so Operator.__call__ falls back to its general path."""
+    import torch
+    from sph_raytracer_amd import _lib, build
+    build.build()
+    fast = _lib.load_fast()
+    assert fast is not None
+    b = fast.new(_lib.address(_lib.load().sphrt_last_error))
+    assert fast.forward(b, torch.zeros(4)) is None
+    assert fast.forward(b, [1.0]) is None
+    with pytest.raises(ValueError):
+        fast.add(b, (2, 2), False, 0, 0, 0, 1, 4, 0, 4, (4,))

@@ -306,3 +306,27 @@ def test_exact_tie_rays_vs_oracle(shape, a_full, gpu):
     deferred = [_deferred_count(grid, gm, gpu) for gm in geoms]
     print('deferred rays per view:', deferred)
     assert sum(deferred) > 0
+
+
+def test_fast_path_matches_general_path(c2, gpu):
+    """Steady-state calls go through the CPython entry (csrc/fastpath.cpp) once a shape is bound:
+    bitwise the same result as the general path, fresh output tensors, and inputs it does not
+    serve (grad, non-contiguous, other shapes) still take the general path."""
+    grid, geom, op = c2
+    assert op._fastc is not None or op._fast == {}
+    for dt in (tr.float32, tr.float64):
+        x = tr.rand(grid.shape, dtype=dt, device=gpu)
+        y0 = op(x)                       # binds
+        y1 = op(x)                       # fast path
+        y2 = op(x)
+        assert op._fastc is not None
+        assert y1.shape == y0.shape == tuple(geom.shape) and y1.dtype == dt
+        assert tr.equal(y0, y1) and tr.equal(y1, y2) and y1.data_ptr() != y2.data_ptr()
+        xg = x.clone().requires_grad_(True)
+        yg = op(xg)
+        assert yg.requires_grad and tr.equal(yg.detach(), y0)
+        xt = x.transpose(0, 2).contiguous().transpose(0, 2)     # same values, not contiguous
+        assert tr.equal(op(xt), y0)
+        x2 = tr.stack([x, 2 * x])
+        y3 = op(x2)
+        assert y3.shape == (2,) + tuple(geom.shape) and tr.equal(y3[0], y0)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Host-side cost of a steady-state Operator call (C2): op(x) issue rate vs the bare C launch."""
+"""Host-side cost of a steady-state Operator call (C2): op(x) issue rate (CPython fast path, and
+the ctypes-only path) vs the bare C launch."""
 import os
 import sys
 import time
@@ -38,8 +39,13 @@ def main():
     desc = op._csr['desc']
     st = torch.cuda.current_stream(dev).cuda_stream
     n_vox = x.numel()
+    fc = op._fastc
+    op_ct = Operator(grid, geom, device=dev)      # the same call through ctypes only
+    op_ct(x)
+    op_ct._fastc = None
     for name, fn in [
         ('op(x)', lambda: op(x)),
+        ('op(x) ctypes', lambda: op_ct(x)),
         ('torch.empty', lambda: torch.empty(n, device=dev)),
         ('current_stream', lambda: torch.cuda.current_stream(dev).cuda_stream),
         ('bare C launch', lambda: lib.sphrt_forward_f32(desc, x.data_ptr(), 1, n_vox, 0,
