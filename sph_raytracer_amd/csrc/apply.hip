@@ -23,6 +23,9 @@ constexpr int kThreads = 256;
 #ifndef SPHRT_FWD_MINB64
 #define SPHRT_FWD_MINB64 5   // resident float64 forward workgroups per CU the registers aim for
 #endif
+#ifndef SPHRT_FWD_MINB32
+#define SPHRT_FWD_MINB32 6   // the same for float32
+#endif
 #ifndef SPHRT_FWD_EMIT
 #define SPHRT_FWD_EMIT 2   // row-close emission: 2 selects, 1 rank walk, 0 per-slot window tests
 #endif
@@ -577,23 +580,18 @@ struct RawChunk {
 template <typename L, bool LOCAL>
 __device__ __forceinline__ void raw_load(const int32_t* __restrict__ vox,
                                          const uint16_t* __restrict__ loc,
-                                         const L* __restrict__ len, int p0, int s1,
+                                         const L* __restrict__ len, int64_t a,
                                          RawChunk<L, LOCAL>& r) {
-    if (p0 < s1) {
-        if constexpr (LOCAL) {
-            r.ix[0] = *reinterpret_cast<const uint4*>(loc + p0);
-        } else {
-            const uint4* vp = reinterpret_cast<const uint4*>(vox + p0);
-            r.ix[0] = vp[0];
-            r.ix[1] = vp[1];
-        }
-        load_len8(len, p0, r.l);
+    // unconditional (the caller clamps `a` into the arrays; chunks outside the window are masked
+    // by window_chunk): no branch, so no copy of a load result that would wait for it early
+    if constexpr (LOCAL) {
+        r.ix[0] = *reinterpret_cast<const uint4*>(loc + a);
     } else {
-        r.ix[0] = make_uint4(0, 0, 0, 0);
-        if constexpr (!LOCAL) r.ix[1] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) r.l[k] = (L)0;
+        const uint4* vp = reinterpret_cast<const uint4*>(vox + a);
+        r.ix[0] = vp[0];
+        r.ix[1] = vp[1];
     }
+    load_len8(len + a, 0, r.l);
 }
 
 // Bits [first, end) of a chunk (chunk-relative segment window).
@@ -602,16 +600,26 @@ __device__ __forceinline__ uint32_t window_bits(int first, int end) {
     return a < b ? ((1u << b) - 1u) & ~((1u << a) - 1u) : 0u;
 }
 
-// A chunk's segments: table mode, v[k] = LDS byte offset of the voxel (loc bits 0-14); otherwise
-// the vox word.  Returns the row heads of the chunk (bit k = segment k).
+// A chunk's segment columns: table mode keeps the loc half-words packed two per register (head
+// bits cleared; slot k = LDS byte offset of its voxel, vslot()), otherwise the vox words.
+template <bool LOCAL>
+constexpr int kVW = LOCAL ? kPer / 2 : kPer;
+
+template <bool LOCAL>
+__device__ __forceinline__ uint32_t vslot(const uint32_t (&v)[kVW<LOCAL>], int k) {
+    if constexpr (LOCAL) return (v[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+    else return v[k];
+}
+
+// Decode a raw chunk; returns the row heads of the chunk (bit k = segment k).
 template <typename L, bool LOCAL>
-__device__ __forceinline__ uint32_t decode(const RawChunk<L, LOCAL>& r, uint32_t (&v)[kPer],
+__device__ __forceinline__ uint32_t decode(const RawChunk<L, LOCAL>& r, uint32_t (&v)[kVW<LOCAL>],
                                            L (&l)[kPer]) {
     uint32_t hmask = 0;
     if constexpr (LOCAL) {
         const uint32_t w[4] = {r.ix[0].x, r.ix[0].y, r.ix[0].z, r.ix[0].w};
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) v[k] = (w[k >> 1] >> (16 * (k & 1))) & 0x7ffcu;
+        for (int j = 0; j < 4; ++j) v[j] = w[j] & 0x7ffc7ffcu;
         // bit 15 of half-word k -> bit k: even k to bits 0,2,4,6, odd k to 16,18,20,22, folded
         const uint32_t h = ((w[0] >> 15) & 0x10001u) | ((w[1] >> 13) & 0x40004u) |
                            ((w[2] >> 11) & 0x100010u) | ((w[3] >> 9) & 0x400040u);
@@ -631,11 +639,18 @@ __device__ __forceinline__ uint32_t decode(const RawChunk<L, LOCAL>& r, uint32_t
 // masked slots read the zero granule / voxel 0 with length 0 and carry no head.
 template <typename L, bool LOCAL>
 __device__ __forceinline__ uint32_t window_chunk(const RawChunk<L, LOCAL>& r, int p0, int lo,
-                                                 int hi, uint32_t (&v)[kPer], L (&l)[kPer]) {
+                                                 int hi, uint32_t (&v)[kVW<LOCAL>], L (&l)[kPer]) {
     uint32_t hmask = decode<L, LOCAL>(r, v, l);
     if (p0 < lo || p0 + kPer > hi) {                // edge chunks only
-        mask8(p0, lo, hi, v, l);
-        hmask &= window_bits(lo - p0, hi - p0);
+        const int first = lo - p0, end = hi - p0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+            if (k < first || k >= end) {
+                if constexpr (LOCAL) v[k >> 1] &= ~(0xffffu << (16 * (k & 1)));
+                else v[k] = 0u;
+                l[k] = (L)0;
+            }
+        hmask &= window_bits(first, end);
     }
     return hmask;
 }
@@ -656,7 +671,7 @@ enum FwdMode { kFwdTable = 0, kFwdGather = 1, kFwdDynamic = 2 };
 // Resident workgroups per CU the register allocation aims for: 6 (<= 80 VGPRs) lets a C2-sized
 // launch (~1500 workgroups) be resident at once; float64 stops at 5 (no spills).
 template <typename T, int MODE>
-constexpr int fwd_min_blocks() { return sizeof(T) == 8 ? SPHRT_FWD_MINB64 : 6; }
+constexpr int fwd_min_blocks() { return sizeof(T) == 8 ? SPHRT_FWD_MINB64 : SPHRT_FWD_MINB32; }
 
 template <typename T>
 using AccumOf = typename std::conditional<sizeof(T) == 4, float, double>::type;
@@ -683,9 +698,9 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
     // so its first pass is [b*kSegPerBlock, +kPass)) and the granule table (fixed stride).
     FWD_STAMP(0);
     const int64_t base0 = (int64_t)blockIdx.x * kSegPerBlock;
-    const int n_here = (int)imin64(n_seg - base0, (int64_t)kPass + 1);
+    const int64_t last_chunk = imax64((n_seg + kPer - 1) / kPer, 1) - 1;   // clamp for loads
     RawChunk<L, local> raw;
-    raw_load<L, local>(vox + base0, loc + base0, len + base0, o, n_here, raw);
+    raw_load<L, local>(vox, loc, len, imin64(base0 + o, last_chunk * kPer), raw);
     // table chunks beyond the stride read the next workgroup's entries (tab is padded by
     // kGranEarly*kThreads entries); they are never staged (j >= n_tab)
     const int32_t* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
@@ -729,7 +744,7 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
         lo = (int)imax64(s0 - base, -1);
         hi = (int)imin64(s1 - base, (int64_t)kPass + 1);
     };
-    uint32_t v[kPer];
+    uint32_t v[kVW<local>];
     L l[kPer];
     uint32_t hmask;
     {
@@ -756,15 +771,15 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             window(base, lo, hi);
             if (base != base0 || c != 0) {
                 RawChunk<L, local> rc;
-                raw_load<L, local>(vox + base, loc + base, len + base, o, hi, rc);
+                raw_load<L, local>(vox, loc, len, imin64(base + o, last_chunk * kPer), rc);
                 hmask = window_chunk<L, local>(rc, o, lo, hi, v, l);
             }
             const int hcount = __builtin_popcount(hmask);
             T rv[kPer];
-            if (MODE == kFwdGather) {       // per-segment gathers go out before any scan
+            if constexpr (MODE == kFwdGather) {   // per-segment gathers go out before any scan
 #pragma unroll
                 for (int k = 0; k < kPer; ++k)
-                    rv[k] = l[k] != (L)0 ? rho[v[k] & ~kHead] : (T)0;
+                    rv[k] = l[k] != (L)0 ? rho[vslot<local>(v, k) & ~kHead] : (T)0;
             }
             int pass_heads;
             // (table mode: the full barrier also retires the granule LDS-DMA)
@@ -788,12 +803,12 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             auto row_of = [&](int i) -> int64_t {     // ray of the row after i own heads
                 return i < 0 ? r_prev : i == 0 ? r_first : rows[i];
             };
-            if (local) {
+            if constexpr (local) {
 #pragma unroll
                 for (int k = 0; k < kPer; ++k)
-                    rv[k] = lds_at<T>(dens, v[k]);   // masked slots: the zero granule
+                    rv[k] = lds_at<T>(dens, vslot<local>(v, k));   // masked: the zero granule
             }
-            if (MODE == kFwdDynamic) {      // time slice of each segment's ray
+            if constexpr (MODE == kFwdDynamic) {   // time slice of each segment's ray
                 int rank = 0;
 #pragma unroll
                 for (int k = 0; k < kPer; ++k) {
@@ -801,7 +816,7 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
                     T x = (T)0;
                     if (l[k] != (L)0) {
                         const int64_t ray = row_of(rank - 1);
-                        x = density[(ray / div) * cs + (v[k] & ~kHead)];
+                        x = density[(ray / div) * cs + (vslot<local>(v, k) & ~kHead)];
                     }
                     rv[k] = x;
                 }
