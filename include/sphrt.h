@@ -153,11 +153,12 @@ typedef struct sphrt_csr {
     const int64_t *blocks;
     int64_t n_blocks;
     const uint16_t *loc;   /* NULL: per-segment gathers through vox */
-    const int32_t *tab;
+    const void *tab;       /* int32 entries, or uint16 when tab_bytes == 2 */
     int64_t n_cols;        /* column ids (vox & ~head) are < n_cols: voxels, or rays if transposed */
     int64_t n_fallback;    /* blocks without a granule table (n_tab = -1), from sphrt_csr_local */
     const int32_t *empty_ray;  /* the rays without segments, ascending (n_rays - rows entries) */
     int64_t tab_stride;    /* granule-table entries per block (>= the largest n_tab) */
+    int64_t tab_bytes;     /* 2: uint16 table entries (n_cols <= 2^18), else int32 */
 } sphrt_csr;
 
 int64_t sphrt_csr_blocks(int64_t n_segments);
@@ -170,7 +171,7 @@ int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_
  * csr->n_fallback, picks tab_stride >= the second (csr->tab_stride; tab holds n_blocks *
  * tab_stride entries) and runs _fill. */
 int sphrt_csr_local_count(const sphrt_csr *csr, int64_t *blocks, int64_t *stats, void *stream);
-int sphrt_csr_local_fill(const sphrt_csr *csr, const int64_t *blocks, uint16_t *loc, int32_t *tab,
+int sphrt_csr_local_fill(const sphrt_csr *csr, const int64_t *blocks, uint16_t *loc, void *tab,
                          int64_t tab_stride, void *stream);
 
 /* ---- forward line integral on the CSR (replaces Operator.__call__, raytracer.py:692-713) -- */

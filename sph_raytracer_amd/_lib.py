@@ -38,7 +38,8 @@ class CSR(ctypes.Structure):
     _fields_ = [('n_rays', c_i64), ('n_segments', c_i64), ('row_ptr', c_vp), ('vox', c_vp),
                 ('len', c_vp), ('len32', c_vp), ('row_ray', c_vp), ('blocks', c_vp),
                 ('n_blocks', c_i64), ('loc', c_vp), ('tab', c_vp), ('n_cols', c_i64),
-                ('n_fallback', c_i64), ('empty_ray', c_vp), ('tab_stride', c_i64)]
+                ('n_fallback', c_i64), ('empty_ray', c_vp), ('tab_stride', c_i64),
+                ('tab_bytes', c_i64)]
 
 
 ROW_HEAD = 0x80000000

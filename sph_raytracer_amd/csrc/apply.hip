@@ -324,11 +324,11 @@ __device__ __forceinline__ uint16_t loc_code(int rank, uint32_t v, bool head) {
 // the granules into LDS with 16-byte LDS-DMA loads (one lane per granule, ~3x fewer lane accesses
 // than segments) and the segments read LDS.  n_tab = -1 marks a workgroup left on the
 // per-segment gather (more than kLocalMax segments or kMaxGran granules).
-template <bool FILL>
+template <bool FILL, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restrict__ blocks,
                                                                const int32_t* __restrict__ vox,
                                                                uint16_t* __restrict__ loc,
-                                                               int32_t* __restrict__ tab,
+                                                               TabT* __restrict__ tab,
                                                                int64_t tab_stride,
                                                                unsigned long long* stats) {
     __shared__ uint64_t key[kLocalMax];
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restri
         const uint64_t k = key[i];
         if (i == 0 || gran(k) != gran(key[i - 1])) {
             ++rank;
-            tab[(int64_t)blockIdx.x * tab_stride + rank] = (int32_t)gran(k);
+            tab[(int64_t)blockIdx.x * tab_stride + rank] = (TabT)gran(k);
         }
         const int pos = (int)((k >> 1) & 0xfff);
         loc[s0 + pos] = loc_code(rank, (uint32_t)(k >> 13), (k & 1) != 0);
@@ -412,10 +412,10 @@ __global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restri
 // bitmap fits (n_cols/4 bits; 128^3 voxels = 64 KiB): set one bit per segment, prefix-popcount
 // the words, and a granule's rank is the number of set bits below it.  O(segments + words) per
 // workgroup, a handful of barriers.  Identical output to the sort (ascending distinct granules).
-template <bool FILL>
+template <bool FILL, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
-    int32_t* __restrict__ tab, int64_t tab_stride, int n_words,
+    TabT* __restrict__ tab, int64_t tab_stride, int n_words,
     unsigned long long* stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char bm_lds[];
     uint32_t* bm = reinterpret_cast<uint32_t*>(bm_lds);     // n_words bitmap words
@@ -459,14 +459,14 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
         }
         return;
     }
-    int32_t* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
+    TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
     for (int w = w0; w < w1; ++w) {
         pre[w] = run;
         uint32_t bits = bm[w];
         while (bits) {
             const int b = __builtin_ctz(bits);
             bits &= bits - 1;
-            tab_b[run++] = w * 32 + b;
+            tab_b[run++] = (TabT)(w * 32 + b);
         }
     }
     __syncthreads();
@@ -513,9 +513,9 @@ __device__ __forceinline__ void stage_one(const T* __restrict__ rho, int32_t g, 
 
 // The volume's last granule, if partial (voxel count not a multiple of 4), can only be the
 // table's last entry: the DMA skips it (no read past the volume) and one lane copies it here.
-template <typename T>
+template <typename T, typename TabT>
 __device__ __forceinline__ void stage_partial_tail(const T* __restrict__ rho,
-                                                   const int32_t* __restrict__ tab_b, int n_tab,
+                                                   const TabT* __restrict__ tab_b, int n_tab,
                                                    int64_t n_cols, T* dens) {
     if ((n_cols & 3) != 0 && n_tab > 0 && (int)threadIdx.x == (n_tab - 1) % kThreads) {
         const int j = n_tab - 1;
@@ -526,9 +526,9 @@ __device__ __forceinline__ void stage_partial_tail(const T* __restrict__ rho,
 }
 
 // DMA rounds [r0, ..) of the table, entries read from memory one round at a time.
-template <typename T>
+template <typename T, typename TabT>
 __device__ __forceinline__ void stage_granules_late(const T* __restrict__ rho,
-                                                    const int32_t* __restrict__ tab_b, int r0,
+                                                    const TabT* __restrict__ tab_b, int r0,
                                                     int n_tab, int32_t g_full, T* dens) {
     constexpr int G = kGranLanes<T>;
     const int lane = threadIdx.x & 63;
@@ -537,7 +537,7 @@ __device__ __forceinline__ void stage_granules_late(const T* __restrict__ rho,
         const int e0 = gran_entry0<T>(r, w);
         const int e = e0 + lane / G;
         if (e < n_tab) {
-            const int32_t g = tab_b[e];
+            const int32_t g = (int32_t)tab_b[e];
             if (g < g_full) stage_one<T>(rho, g, e0, lane, dens);
         }
     }
@@ -547,10 +547,10 @@ __device__ __forceinline__ void stage_granules_late(const T* __restrict__ rho,
 // (large tables) are fetched here.  When the volume's voxel count is not a multiple of 4 its
 // last granule is partial: only the table's last entry can be, it is skipped by the DMA (no read
 // past the volume) and copied lane by lane at the end.  Writes the zero granule.
-template <typename T>
+template <typename T, typename TabT>
 __device__ __forceinline__ void stage_granules(const T* __restrict__ rho,
                                                const int32_t (&ti)[kEarlyRounds<T>],
-                                               const int32_t* __restrict__ tab_b, int n_tab,
+                                               const TabT* __restrict__ tab_b, int n_tab,
                                                int32_t g_full, int64_t n_cols, T* dens) {
     constexpr int G = kGranLanes<T>;
     const int lane = threadIdx.x & 63;
@@ -565,8 +565,8 @@ __device__ __forceinline__ void stage_granules(const T* __restrict__ rho,
         const int e0 = gran_entry0<T>(r, w);
         if (e0 + lane / G < n_tab && ti[r] < g_full) stage_one<T>(rho, ti[r], e0, lane, dens);
     }
-    stage_granules_late<T>(rho, tab_b, kEarlyRounds<T>, n_tab, g_full, dens);
-    stage_partial_tail<T>(rho, tab_b, n_tab, n_cols, dens);
+    stage_granules_late<T, TabT>(rho, tab_b, kEarlyRounds<T>, n_tab, g_full, dens);
+    stage_partial_tail<T, TabT>(rho, tab_b, n_tab, n_cols, dens);
 }
 
 // The first pass's loads, issued before anything is known about the workgroup and decoded
@@ -676,10 +676,10 @@ constexpr int fwd_min_blocks() { return sizeof(T) == 8 ? SPHRT_FWD_MINB64 : SPHR
 template <typename T>
 using AccumOf = typename std::conditional<sizeof(T) == 4, float, double>::type;
 
-template <typename T, typename L, int MODE>
+template <typename T, typename L, int MODE, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward_kernel(
     const int64_t* __restrict__ blocks, const int32_t* __restrict__ vox,
-    const uint16_t* __restrict__ loc, const int32_t* __restrict__ tab, const L* __restrict__ len,
+    const uint16_t* __restrict__ loc, const TabT* __restrict__ tab, const L* __restrict__ len,
     const int32_t* __restrict__ row_ray, const int32_t* __restrict__ empty_ray,
     const T* __restrict__ density, int64_t n_chan, int64_t cs, int64_t div, T* __restrict__ out,
     int64_t ocs, int64_t n_rays, int64_t n_seg, int64_t n_cols, int64_t tab_stride,
@@ -703,13 +703,13 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
     raw_load<L, local>(vox, loc, len, imin64(base0 + o, last_chunk * kPer), raw);
     // table chunks beyond the stride read the next workgroup's entries (tab is padded by
     // kGranEarly*kThreads entries); they are never staged (j >= n_tab)
-    const int32_t* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
+    const TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
     int32_t ti[kEarlyRounds<T>];
     if (local) {
         const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
         for (int r = 0; r < kEarlyRounds<T>; ++r)
-            ti[r] = tab_b[gran_entry0<T>(r, w) + (tid & 63) / kGranLanes<T>];
+            ti[r] = (int32_t)tab_b[gran_entry0<T>(r, w) + (tid & 63) / kGranLanes<T>];
     }
     __builtin_amdgcn_sched_barrier(0);
     const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
@@ -738,7 +738,7 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
         return;
     }
     const int32_t g_full = (int32_t)imin64(n_cols >> 2, INT32_MAX);   // whole granules
-    if (local) stage_granules<T>(density, ti, tab_b, (int)n_tab, g_full, n_cols, dens);
+    if (local) stage_granules<T, TabT>(density, ti, tab_b, (int)n_tab, g_full, n_cols, dens);
     // pass-relative segment window [lo, hi) of this workgroup (32-bit lane arithmetic)
     auto window = [&](int64_t base, int& lo, int& hi) {
         lo = (int)imax64(s0 - base, -1);
@@ -759,8 +759,8 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
         const T* rho = density + c * cs;
         T* oc = out + c * ocs;
         if (local && c > 0) {
-            stage_granules_late<T>(rho, tab_b, 0, (int)n_tab, g_full, dens);
-            stage_partial_tail<T>(rho, tab_b, (int)n_tab, n_cols, dens);
+            stage_granules_late<T, TabT>(rho, tab_b, 0, (int)n_tab, g_full, dens);
+            stage_partial_tail<T, TabT>(rho, tab_b, (int)n_tab, n_cols, dens);
         }
         FWD_STAMP(2);
         double carry = 0.0;                 // open run entering the pass
@@ -1053,32 +1053,45 @@ extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_
         return fail("hipMemsetAsync failed");
     if (c->n_segments == 0) return 0;
     if (const int words = table_bitmap_words(c->n_cols)) {
-        hipLaunchKernelGGL(local_table_bitmap_kernel<false>, dim3((unsigned)c->n_blocks),
+        hipLaunchKernelGGL((local_table_bitmap_kernel<false, int32_t>), dim3((unsigned)c->n_blocks),
                            dim3(kThreads), (size_t)words * 8, st, blocks, c->vox, nullptr, nullptr,
                            0, words, (unsigned long long*)stats);
         return check_launch("local_table_bitmap_kernel<count>");
     }
-    hipLaunchKernelGGL(local_table_kernel<false>, dim3((unsigned)c->n_blocks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((local_table_kernel<false, int32_t>), dim3((unsigned)c->n_blocks), dim3(kThreads), 0,
                        st, blocks, c->vox, nullptr, nullptr, 0, (unsigned long long*)stats);
     return check_launch("local_table_kernel<count>");
 }
 
 extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, uint16_t* loc,
-                                    int32_t* tab, int64_t tab_stride, void* stream) {
+                                    void* tab, int64_t tab_stride, void* stream) {
     if (!c || !c->vox || !blocks || !loc || !tab) return fail("incomplete CSR for the granule tables");
     if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
     if (tab_stride < 1 || tab_stride > (kMaxGran + 63) / 64 * 64)
         return fail("bad granule table stride");
+    const bool u16 = c->tab_bytes == 2;
+    if (u16 && (c->n_cols + 3) / 4 > 65536) return fail("16-bit granule tables need <= 2^18 columns");
     if (c->n_segments == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
     if (const int words = table_bitmap_words(c->n_cols)) {
-        hipLaunchKernelGGL(local_table_bitmap_kernel<true>, dim3((unsigned)c->n_blocks),
-                           dim3(kThreads), (size_t)words * 8, (hipStream_t)stream,
-                           (int64_t*)blocks, c->vox, loc, tab, tab_stride, words, nullptr);
+        if (u16)
+            hipLaunchKernelGGL((local_table_bitmap_kernel<true, uint16_t>), dim3((unsigned)c->n_blocks),
+                               dim3(kThreads), (size_t)words * 8, st, (int64_t*)blocks, c->vox, loc,
+                               (uint16_t*)tab, tab_stride, words, nullptr);
+        else
+            hipLaunchKernelGGL((local_table_bitmap_kernel<true, int32_t>), dim3((unsigned)c->n_blocks),
+                               dim3(kThreads), (size_t)words * 8, st, (int64_t*)blocks, c->vox, loc,
+                               (int32_t*)tab, tab_stride, words, nullptr);
         return check_launch("local_table_bitmap_kernel<fill>");
     }
-    hipLaunchKernelGGL(local_table_kernel<true>, dim3((unsigned)c->n_blocks), dim3(kThreads), 0,
-                       (hipStream_t)stream, (int64_t*)blocks, c->vox, loc, tab, tab_stride,
-                       nullptr);
+    if (u16)
+        hipLaunchKernelGGL((local_table_kernel<true, uint16_t>), dim3((unsigned)c->n_blocks),
+                           dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (uint16_t*)tab,
+                           tab_stride, nullptr);
+    else
+        hipLaunchKernelGGL((local_table_kernel<true, int32_t>), dim3((unsigned)c->n_blocks),
+                           dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (int32_t*)tab,
+                           tab_stride, nullptr);
     return check_launch("local_table_kernel<fill>");
 }
 
@@ -1110,20 +1123,28 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
                           int64_t chan_stride, int64_t div, T* out, int64_t ocs, void* stream) {
     const dim3 grid((unsigned)c->n_blocks), block(kThreads);
     hipStream_t st = (hipStream_t)stream;
-#define SPHRT_FWD_ARGS c->blocks, c->vox, c->loc, c->tab, len, c->row_ray, c->empty_ray, density, \
-                       n_chan, chan_stride, div, out, ocs, c->n_rays, c->n_segments, c->n_cols, \
-                       c->tab_stride
+#define SPHRT_FWD_ARGS(TabT) c->blocks, c->vox, c->loc, (const TabT*)c->tab, len, c->row_ray,  \
+                       c->empty_ray, density, n_chan, chan_stride, div, out, ocs, c->n_rays,    \
+                       c->n_segments, c->n_cols, c->tab_stride
     if (div > 0) {
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic>), grid, block, 0, st, SPHRT_FWD_ARGS, 0);
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic>), grid, block, 0, st,
+                           SPHRT_FWD_ARGS(int32_t), 0);
     } else if (use_tables(c, density, n_chan, chan_stride, div)) {
         const size_t lds = (size_t)(c->tab_stride + 1) * 4 * sizeof(T);   // + zero granule
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable>), grid, block, lds, st, SPHRT_FWD_ARGS, 0);
+        if (c->tab_bytes == 2)
+            hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, uint16_t>), grid, block, lds, st,
+                               SPHRT_FWD_ARGS(uint16_t), 0);
+        else
+            hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, int32_t>), grid, block, lds, st,
+                               SPHRT_FWD_ARGS(int32_t), 0);
         if (c->n_fallback > 0) {
             if (int e = check_launch("forward_kernel<table>")) return e;
-            hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather>), grid, block, 0, st, SPHRT_FWD_ARGS, 1);
+            hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather>), grid, block, 0, st,
+                               SPHRT_FWD_ARGS(int32_t), 1);
         }
     } else {
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather>), grid, block, 0, st, SPHRT_FWD_ARGS, 0);
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather>), grid, block, 0, st,
+                           SPHRT_FWD_ARGS(int32_t), 0);
     }
 #undef SPHRT_FWD_ARGS
     return check_launch(sizeof(T) == 4 ? "forward_kernel<f32>" : "forward_kernel<f64>");

@@ -278,7 +278,11 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
     n_fallback, max_tab = stats.tolist()
     stride = max(64, (max_tab + 63) // 64 * 64)
     loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
-    tab = tr.empty(nblocks * stride + 3 * 256, dtype=tr.int32, device=dev)   # + early-fetch pad
+    # 16-bit entries when every granule index fits (<= 2^18 columns): half the table bytes the
+    # forward streams
+    desc.tab_bytes = 2 if (desc.n_cols + 3) // 4 <= 65536 else 4
+    tab = tr.empty(nblocks * stride + 3 * 256, dtype=tr.int16 if desc.tab_bytes == 2 else tr.int32,
+                   device=dev)   # + early-fetch pad
     _lib.check(lib.sphrt_csr_local_fill(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(tab),
                                         stride, stream), 'sphrt_csr_local_fill')
     desc.n_fallback, desc.tab_stride = n_fallback, stride

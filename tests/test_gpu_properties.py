@@ -113,6 +113,8 @@ def test_granule_tables(c2, gpu):
     vox = csr['vox'].cpu().numpy().view(np.uint32)[:csr['total']]
     loc = csr['loc'].cpu().numpy().view(np.uint16)[:csr['total']]
     tab = csr['tab'].cpu().numpy()
+    assert csr['desc'].tab_bytes == 2 and tab.dtype == np.int16   # 50^3 voxels: 16-bit entries
+    tab = tab.view(np.uint16).astype(np.int64)
     s0, s1, n_tab = blocks[:, 2], blocks[:, 3], blocks[:, 5]
     assert (n_tab >= 0).all() and (n_tab <= s1 - s0).all() and csr['desc'].n_fallback == 0
     owner = np.repeat(np.arange(len(blocks)), s1 - s0)
