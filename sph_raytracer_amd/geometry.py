@@ -215,12 +215,38 @@ class ViewGeomCollection(ViewGeom):
         return tr.concat([g.ray_starts[None, ...] for g in self.geoms])
 
     def _ray_spec(self):
-        """Stacked generator inputs when every view is a cone detector of one kind, else None."""
+        """Stacked generator inputs when every view is a cone detector of one kind, else None.
+
+        Orbits of identical detectors (one type, shape, fov and radial samples) take one batched
+        pass: the frames' cross products in one call, the per-axis samples once (the same torch
+        calls as each view's own spec, so the same bits; tests/test_cpu_api.py)."""
+        fast = self._ray_spec_batched()
+        if fast is not None:
+            return fast
         specs = [g._ray_spec() if hasattr(g, '_ray_spec') else None for g in self.geoms]
         if not specs or any(sp is None for sp in specs) or len({sp[0] for sp in specs}) != 1:
             return None
         return (specs[0][0], tr.stack([sp[1] for sp in specs]), tr.stack([sp[2] for sp in specs]),
                 tr.stack([sp[3] for sp in specs]))
+
+    def _ray_spec_batched(self):
+        gs = self.geoms
+        kind = type(gs[0]) if gs else None
+        if kind not in (ConeRectGeom, ConeCircGeom) or any(type(g) is not kind for g in gs):
+            return None
+        g0 = gs[0]
+        key = (tuple(g0.shape), g0.fov.tolist())
+        if any((tuple(g.shape), g.fov.tolist()) != key for g in gs):
+            return None
+        if kind is ConeCircGeom and any(not (tr.equal(g.r, g0.r) and tr.equal(g.theta, g0.theta))
+                                        for g in gs):
+            return None
+        look = tr.stack([g.lookdir for g in gs])
+        up = tr.stack([g.updir for g in gs])
+        frame = tr.concat([look, tr.cross(look, up, dim=-1), up], dim=-1)
+        circ, _, row, col = g0._ray_spec()
+        n = len(gs)
+        return (circ, frame, row.expand(n, *row.shape), col.expand(n, *col.shape))
 
     @property
     def pos(self):

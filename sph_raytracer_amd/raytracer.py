@@ -145,7 +145,9 @@ def _device_rays(geom, dev):
     if n_views * h * w != math.prod(shape) or row.shape[-1] != h:
         return None
     lib = _lib.load()
-    frame_d, row_d, col_d = (t.to(dev) for t in (frame, row, col))
+    # one host-to-device copy for the three inputs
+    packed = tr.concat([frame.reshape(-1), row.reshape(-1), col.reshape(-1)]).to(dev)
+    frame_d, row_d, col_d = packed.split([frame.numel(), row.numel(), col.numel()])
     rays = tr.empty(shape + (3,), dtype=tr.float64, device=dev)
     _lib.check(lib.sphrt_rays_cone(n_views, h, w, int(circ), _lib.ptr(frame_d), _lib.ptr(row_d),
                                    _lib.ptr(col_d), _lib.ptr(rays), _lib.stream_of(dev)),
@@ -173,9 +175,12 @@ class _RayBatch:
         if grid is not None:
             starts = find_starts(grid, xs_u)                   # (3, ...) on the host
             st[..., :3] = starts.moveaxis(0, -1).to(tr.int32)
-        self.xs = xs_u.to(device)
+        # starts and start voxels in one host-to-device copy
+        xb, sb = xs_u.reshape(-1).view(tr.uint8), st.reshape(-1).view(tr.uint8)
+        packed = tr.concat([xb, sb]).to(device)
+        self.xs = packed[:xb.numel()].view(tr.float64).view(xs_u.shape)
+        self.start = packed[xb.numel():].view(tr.int32).view(st.shape)
         self.rays = rays.detach().contiguous().to(device)
-        self.start = st.to(device)
         full = rshape + (3,)
         xs_str = self.xs.expand(full).stride()
         ry_str = self.rays.expand(full).stride()

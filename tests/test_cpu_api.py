@@ -261,3 +261,27 @@ def test_fastpath_entry_builds_and_declines_foreign_inputs():
     assert fast.forward(b, [1.0]) is None
     with pytest.raises(ValueError):
         fast.add(b, (2, 2), False, 0, 0, 0, 1, 4, 0, 4, (4,))
+
+
+def test_batched_orbit_spec_matches_per_view():
+    """ViewGeomCollection._ray_spec batches uniform orbits (one cross product call, the per-axis
+    samples once): bitwise the stack of the views' own specs, for rectangular and circular
+    detectors with arbitrary frames; non-uniform collections take the per-view path."""
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom
+    g = tr.Generator().manual_seed(5)
+    for kind, kw in ((ConeRectGeom, dict(fov=(30, 50))), (ConeCircGeom, dict(fov=(2, 40)))):
+        views = []
+        for i in range(40):
+            pos = tr.randn(3, generator=g, dtype=tr.float64) * 4
+            look = -pos + 0.3 * tr.randn(3, generator=g, dtype=tr.float64) if i % 2 else None
+            views.append(kind((7, 9), pos=pos, lookdir=look, **kw))
+        coll = sum(views)
+        fast = coll._ray_spec()
+        assert coll._ray_spec_batched() is not None
+        specs = [v._ray_spec() for v in views]
+        assert fast[0] == specs[0][0]
+        for i in (1, 2, 3):
+            ref = tr.stack([sp[i] for sp in specs])
+            assert fast[i].shape == ref.shape and tr.equal(fast[i].contiguous(), ref), (kind, i)
+    mixed = ConeRectGeom((7, 9), pos=(3, 0, 1), fov=(30, 30)) + ConeRectGeom((7, 9), pos=(0, 3, 1))
+    assert mixed._ray_spec_batched() is None and mixed._ray_spec()[1].shape == (2, 9)
