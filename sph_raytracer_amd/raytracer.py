@@ -489,7 +489,9 @@ class Operator:
         es = d.element_size()
         table = (c.loc and div == 0 and 0 < c.tab_stride and (c.tab_stride + 1) * 4 * es <= 48 * 1024
                  and d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0))
-        return f'forward_kernel<{t}, {0 if table else (2 if div else 1)}>'
+        if table:
+            return f'forward_kernel<{t}, 0, {"unsigned short" if c.tab_bytes == 2 else "int"}>'
+        return f'forward_kernel<{t}, {2 if div else 1}, int>'
 
     def _apply_forward(self, density):
         dev = self._cdev

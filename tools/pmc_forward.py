@@ -28,6 +28,18 @@ PASSES = [
 ]
 
 
+def kernel_name(config):
+    """The f32 forward instantiation for a config, from a child process (this driver never
+    touches the GPU itself)."""
+    code = ('import sys, torch; sys.path.insert(0, %r); sys.path.insert(0, %r); import bench; '
+            'from sph_raytracer_amd import Operator; cfg = bench.CONFIGS[%r]; '
+            'g, v = bench.build_geometry(cfg, 0, 1); op = Operator(g, v, device=torch.device("cuda", 0)); '
+            'x = torch.rand(cfg[0], device="cuda"); print(op._forward_kernel_name(x))'
+            % (ROOT, os.path.join(ROOT, 'tools'), config))
+    out = subprocess.run([sys.executable, '-c', code], check=True, capture_output=True, text=True)
+    return out.stdout.strip().splitlines()[-1]
+
+
 def run_pass(counters, workdir, config, reps, kernel):
     d = os.path.join(workdir, '_'.join(c.lower() for c in counters[:2]))
     shutil.rmtree(d, ignore_errors=True)
@@ -55,9 +67,12 @@ def main():
     ap.add_argument('--out', required=True)
     ap.add_argument('--config', default='c2')
     ap.add_argument('--reps', type=int, default=10)
-    ap.add_argument('--kernel', default='forward_kernel<float, float, 0>')
+    ap.add_argument('--kernel', default=None,
+                    help='kernel name substring (default: the instantiation the f32 forward runs)')
     ap.add_argument('--workdir', default=os.path.join(ROOT, 'gpurun_out', 'pmc'))
     args = ap.parse_args()
+    if args.kernel is None:
+        args.kernel = kernel_name(args.config)
     per_launch, dispatches, raw = {}, {}, []
     for counters in PASSES:
         v, n, files = run_pass(counters, args.workdir, args.config, args.reps, args.kernel)
