@@ -229,6 +229,16 @@ __device__ void sort_lds(uint64_t* keys, uint32_t* pays, int F, int lane) {
     }
 }
 
+// A screened hit ray as the trace kernel reads it: start, direction, start voxel, ray id (one
+// 64-byte record, read with scalar loads by the wave that traces it: no broadcast index
+// arithmetic and no RaysDev in the trace kernel's registers).
+struct HitRay {
+    double x[3];
+    double d[3];
+    int32_t s[3];
+    int32_t ray;
+};
+
 template <typename T>
 struct TraceOut {
     int32_t* counts;          // COUNT
@@ -242,7 +252,7 @@ struct TraceOut {
     unsigned long long* n_deferred;  // workspace: deferred-ray counter
     int64_t* deferred;               // workspace: deferred ray ids
     unsigned* n_hits;                // workspace: screened hit-ray counter
-    int32_t* hits;                   // workspace: hit ray ids
+    HitRay* hits;                    // workspace: hit rays
 };
 
 // region rows a candidate updates: bit0 r, bit1 e, bit2 a (start entry: all)
@@ -540,7 +550,14 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
     unsigned base = 0;
     if (lane == __builtin_ctzll(m)) base = atomicAdd(o.n_hits, (unsigned)__popcll(m));
     base = __shfl(base, __builtin_ctzll(m));
-    if (hit) o.hits[base + __popcll(m & lanemask_lt(lane))] = (int32_t)ray;
+    if (hit) {
+        HitRay h;
+        h.x[0] = x[0]; h.x[1] = x[1]; h.x[2] = x[2];
+        h.d[0] = d[0]; h.d[1] = d[1]; h.d[2] = d[2];
+        h.s[0] = s[0]; h.s[1] = s[1]; h.s[2] = s[2];
+        h.ray = (int32_t)ray;
+        o.hits[base + __popcll(m & lanemask_lt(lane))] = h;
+    }
 }
 
 // Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
@@ -549,8 +566,8 @@ template <int MODE, typename T>
 #ifndef SPHRT_TRACE_MIN_BLOCKS
 #define SPHRT_TRACE_MIN_BLOCKS 4
 #endif
-__global__ __launch_bounds__(256, SPHRT_TRACE_MIN_BLOCKS) void trace_kernel(GridDev G, RaysDev R, TraceOut<T> o,
-                                                    int cap) {
+__global__ __launch_bounds__(256, SPHRT_TRACE_MIN_BLOCKS) void trace_kernel(GridDev G, TraceOut<T> o,
+                                                                            int cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
@@ -562,12 +579,9 @@ __global__ __launch_bounds__(256, SPHRT_TRACE_MIN_BLOCKS) void trace_kernel(Grid
     const int64_t n_hits = (int64_t)*o.n_hits;
     for (int64_t h = (int64_t)blockIdx.x * waves + wid; h < n_hits;
          h += (int64_t)gridDim.x * waves) {
-        const int64_t ray = o.hits[h];
-        double x[3], d[3];
-        int s[3];
-        load_ray(R, ray, x, d, s);
-        const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
-        trace_one<MODE, T>(G, g, s[0], s[1], s[2], ray, keys, pays, lane, o);
+        const HitRay& hr = o.hits[__builtin_amdgcn_readfirstlane((int)h)];   // uniform record
+        const RayGeo g = make_ray(hr.x[0], hr.x[1], hr.x[2], hr.d[0], hr.d[1], hr.d[2]);
+        trace_one<MODE, T>(G, g, hr.s[0], hr.s[1], hr.s[2], hr.ray, keys, pays, lane, o);
     }
 }
 
@@ -973,7 +987,7 @@ static bool exact_in_lds(const GridDev& G) {
 static size_t exact_scratch_bytes(const GridDev& G) {   // lists of large-K grids, one per wave
     return exact_in_lds(G) ? 0 : (size_t)kExactBlocks * G.K * sizeof(Cand);
 }
-static size_t hits_bytes(int64_t n) { return (((size_t)n * sizeof(int32_t) + 255) / 256) * 256; }
+static size_t hits_bytes(int64_t n) { return (((size_t)n * sizeof(HitRay) + 255) / 256) * 256; }
 static size_t workspace_bytes(const GridDev& G, int64_t n) {
     return kWsHead + (((size_t)n * sizeof(int64_t) + 255) / 256) * 256 + hits_bytes(n) +
            exact_scratch_bytes(G);
@@ -999,7 +1013,7 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     o.n_deferred = (unsigned long long*)ws;
     o.n_hits = (unsigned*)(ws + 64);
     o.deferred = (int64_t*)(ws + kWsHead);
-    o.hits = (int32_t*)(ws + kWsHead + (((size_t)R.n * sizeof(int64_t) + 255) / 256) * 256);
+    o.hits = (HitRay*)(ws + kWsHead + (((size_t)R.n * sizeof(int64_t) + 255) / 256) * 256);
     Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
     if (hipMemsetAsync(ws, 0, kWsHead, st) != hipSuccess) return fail("memset failed");
     hipLaunchKernelGGL((screen_kernel<MODE, T>), dim3((unsigned)((R.n + 255) / 256)), dim3(256), 0,
@@ -1008,7 +1022,7 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
     const int64_t grid = 2048 * kWavesPerBlock / waves;
     hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,
-                       R, o, cap);
+                       o, cap);
     if (int e = check_launch("trace_kernel")) return e;
     if (exact_in_lds(G))
         hipLaunchKernelGGL((exact_wave_kernel<MODE, T>), dim3(kExactBlocks), dim3(64),
