@@ -196,11 +196,7 @@ extern "C" int sphrt_plan_create(const sphrt_grid_desc* gd, int device, sphrt_pl
     G.plane_par_tol = gd->plane_par_tol;
     G.r_outer = gd->r_b[gd->nr];
     double* d = (double*)dmem;
-    G.r_b = d;
-    G.c2_e = d + nbr;
-    G.cos_a = d + nbr + nbe;
-    G.sin_a = d + nbr + nbe + nba;
-    G.e_flags = (const uint8_t*)(d + nd);
+    G.r_b = d;   // the rest of the block follows it (GridDev accessors)
     *out = p;
     return 0;
 }

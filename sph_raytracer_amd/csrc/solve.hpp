@@ -24,11 +24,16 @@ struct GridDev {
     double close_tol;      // isclose() threshold (raytracer.py:246)
     double plane_par_tol;  // a_torch parallel threshold (raytracer.py:521)
     double r_outer;        // r_b[nr]
-    const double* r_b;     // nbr
-    const double* c2_e;    // nbe   cos(e_b)**2
-    const uint8_t* e_flags;// nbe   bit0: cos(e_b) >= 0, bit1: shadow test exempt (e_b ~ pi/2)
-    const double* cos_a;   // nba
-    const double* sin_a;   // nba
+    // One table block: r_b (nbr) | cos(e_b)**2 (nbe) | cos(a_b) (nba) | sin(a_b) (nba) as doubles,
+    // then e_flags (nbe bytes; bit0: cos(e_b) >= 0, bit1: shadow test exempt, e_b ~ pi/2).  One
+    // pointer instead of five: the trace kernel's arguments stay in fewer SGPRs.
+    const double* r_b;
+    __device__ __forceinline__ const double* c2_e() const { return r_b + nbr; }
+    __device__ __forceinline__ const double* cos_a() const { return r_b + nbr + nbe; }
+    __device__ __forceinline__ const double* sin_a() const { return r_b + nbr + nbe + nba; }
+    __device__ __forceinline__ const uint8_t* e_flags() const {
+        return reinterpret_cast<const uint8_t*>(r_b + nbr + nbe + 2 * nba);
+    }
 };
 
 // Everything a crossing solve needs about one ray.
@@ -126,7 +131,7 @@ __device__ __forceinline__ void cone_root(const GridDev& G, const RayGeo& g, int
     neg = prod > 0.0 ? 1 : 0;
     int r = j - neg;
     if (__builtin_fabs(prod) < G.close_tol) r = -2;
-    uint8_t f = G.e_flags[j];
+    uint8_t f = G.e_flags()[j];
     bool cone_up = (f & 1) != 0;
     bool exempt = (f & 2) != 0;
     if (((p2 >= 0.0) != cone_up) && !exempt) t = kInf;   // opposite (shadow) nappe
@@ -139,7 +144,7 @@ __device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeo& g, in
                                            double& ta, int& rega, double& tb, int& regb,
                                            int& nega, int& negb) {
     const double th = G.close_tol;
-    double c2 = G.c2_e[j];
+    double c2 = G.c2_e()[j];
     double aa = g.w2 * g.w2 - c2;
     double bb = 2.0 * (g.w2 * g.x2 - g.wx * c2);
     double cc = g.x2 * g.x2 - g.nx2 * c2;
@@ -166,7 +171,7 @@ __device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeo& g, in
 // ---- azimuth half-planes (a_torch, raytracer.py:505-550) ------------------------------------
 __device__ __forceinline__ void plane_solve(const GridDev& G, const RayGeo& g, int j,
                                             double& t, int& reg, int& neg) {
-    double ca = G.cos_a[j], sa = G.sin_a[j];
+    double ca = G.cos_a()[j], sa = G.sin_a()[j];
     double msa = -sa;
     // einsum '...bc,...jc->...b' against plane normal (-sin, cos, 0): fused chain
     double num = __builtin_fma(0.0, g.x2, __builtin_fma(ca, g.x1, msa * g.x0));

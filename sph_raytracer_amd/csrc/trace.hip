@@ -146,7 +146,10 @@ __device__ __forceinline__ void cas_layer(uint64_t (&k)[M], uint32_t (&p)[M], in
         }
         const int e = i * 64 + lane;
         const int pe = pi * 64 + (lane ^ LM);
-        bool take = (e < pe) ? pair_less(ok, op, k[i], p[i]) : pair_less(k[i], p[i], ok, op);
+        // (key, payload) pairs are distinct (the candidate index is in the payload) except the
+        // identical padding entries, so "mine < other" is !(other < mine): one comparison
+        const bool lt = pair_less(ok, op, k[i], p[i]);
+        const bool take = (e < pe) ? lt : !lt;
         nk[i] = take ? ok : k[i];
         np[i] = take ? op : p[i];
     }
