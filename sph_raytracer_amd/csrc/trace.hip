@@ -60,6 +60,11 @@ __device__ __forceinline__ double wave_min(double v) {
     for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
     return v;
 }
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    return v;
+}
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -356,7 +361,32 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         }
         base += __popcll(m);
     };
-    auto keep = [](double t) { return __builtin_isfinite(t) && !(t < 0.0); };
+    // Only crossings inside the outer sphere's span [t_lo, t_hi] are listed and sorted: after
+    // the exit every segment lies outside (the r row stays -1: no sphere is crossed again), and
+    // for a start outside the outer sphere (t_lo > 0) the e/a rows entering it are those of the
+    // last cone / half-plane crossing before t_lo (the start entry's values if none).  That
+    // entry state is reduced across the wave below; a tie of different values in its last group
+    // defers the ray, exactly as a tie inside the list would.  (C2: 85 -> 62 entries per ray.)
+    const double t1c_o = __builtin_sqrt(G.r_outer * G.r_outer - g.dd * g.dd);  // = sphere nr
+    const double t_lo = g.tc - t1c_o, t_hi = g.tc + t1c_o;
+    const bool clip_lo = t_lo > 0.0;
+    auto keep = [&](double t) {
+        return __builtin_isfinite(t) && !(t < 0.0) && !(t > t_hi) && !(clip_lo && t < t_lo);
+    };
+    double pe_t = -1.0, pa_t = -1.0;      // this lane's last e / a update before t_lo
+    int pe_v = 0, pa_v = 0;
+    bool pe_amb = false, pa_amb = false;  // a second update at that distance, another value
+    auto pre = [&](bool v, double t, int reg, double& bt, int& bv, bool& amb) {
+        if (v && clip_lo && reg != -2 && !(t < 0.0) && t < t_lo) {
+            if (t > bt) {
+                bt = t;
+                bv = reg;
+                amb = false;
+            } else if (t == bt && reg != bv) {
+                amb = true;
+            }
+        }
+    };
 
     const int nbr = G.nbr, nbe = G.nbe, nba = G.nba;
     for (int j0 = 0; j0 < nbr; j0 += 64) {
@@ -382,6 +412,8 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         if (v) cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
         note(ta);
         note(tb);
+        pre(v, ta, ra, pe_t, pe_v, pe_amb);
+        pre(v, tb, rb, pe_t, pe_v, pe_amb);
         push(v && keep(ta), ta, ce0 + j, ra);
         push(v && keep(tb) && !(tb == ta && rb == ra), tb, ce0 + nbe + j, rb);
     }
@@ -393,14 +425,46 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         int r = 0, ng;
         if (v) plane_solve(G, g, j, t, r, ng);
         note(t);
+        pre(v, t, r, pa_t, pa_v, pa_amb);
         push(v && keep(t), t, ca0 + j, r);
     }
-    push(lane == 0, 0.0, G.K - 1, 0);  // the start entry (raytracer.py:111-122)
+    push(lane == 0 && !clip_lo, 0.0, G.K - 1, 0);  // the start entry (raytracer.py:111-122)
     const int F = base;
     tneg = wave_min(tneg);
+    // rows entering the outer sphere (start outside): the last pre-entry update group per row
+    int e_in = se, a_in = sa;
+    if (clip_lo) {
+        bool amb = false;
+        auto entry_row = [&](double bt, int bv, bool bamb, int start_val, int& out) {
+            const double m = wave_max(bt);
+            if (m < 0.0) return;                    // no update before t_lo: the start's value
+            const bool at = bt == m;
+            // at t = 0 the group also holds the start entry (sorted last among equals only by
+            // candidate index, so any other value there is an ambiguous tie)
+            const int v0 = m == 0.0 ? start_val : __shfl(bv, __builtin_ctzll(__ballot(at)));
+            amb |= __ballot(at && (bamb || bv != v0)) != 0;
+            out = v0;
+        };
+        entry_row(pe_t, pe_v, pe_amb, se, e_in);
+        entry_row(pa_t, pa_v, pa_amb, sa, a_in);
+        if (amb) {
+            if (lane == 0) {
+                const unsigned long long q = atomicAdd(o.n_deferred, 1ull);
+                o.deferred[q] = ray;
+            }
+            wave_sync();
+            return;
+        }
+    }
     wave_sync();
 
     // ---- 2. sort by (distance, candidate) ------------------------------------------------
+#if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 1
+    if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 1
+        if (lane == 0) o.counts[ray] = F;
+        return;
+    }
+#endif
     TRACE_T(ts1);
     TRACE_ADD(0, ts0, ts1);
     if (F <= 64) sort_regs<1>(keys, pays, F, lane);
@@ -410,6 +474,12 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
 #endif
     else sort_lds(keys, pays, F, lane);
 
+#if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 2
+    if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 2
+        if (lane == 0) o.counts[ray] = F;
+        return;
+    }
+#endif
     TRACE_T(ts2);
     TRACE_ADD(1, ts1, ts2);
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe, start_c = G.K - 1;
@@ -424,6 +494,12 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     }
 
     // ---- 3. forward fill, lengths, compaction ----------------------------------------------
+#if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 3
+    if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 3
+        if (lane == 0) o.counts[ray] = F;
+        return;
+    }
+#endif
     TRACE_T(ts3);
     TRACE_ADD(2, ts2, ts3);
     const bool start_ok = sr >= 0 && sr < G.nr && se >= 0 && se < G.ne && sa >= 0 && sa < G.na;
@@ -431,7 +507,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     const int head = (start_ok && tneg < 0.0) ? 1 : 0;
     double* seg_len = reinterpret_cast<double*>(keys);
     int32_t* seg_vox = reinterpret_cast<int32_t*>(pays);
-    int cr = sr, cE = se, cA = sa;  // state before the first sorted entry
+    int cr = sr, cE = e_in, cA = a_in;  // state before the first sorted entry
     int nseg = 0;
     for (int c0 = 0; c0 < F; c0 += 64) {
         const int e = c0 + lane;
@@ -483,6 +559,12 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     }
 
     // ---- 4. emit ---------------------------------------------------------------------------
+#if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 4
+    if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 4
+        if (lane == 0) o.counts[ray] = F;
+        return;
+    }
+#endif
     TRACE_T(ts4);
     TRACE_ADD(3, ts3, ts4);
     if (MODE == MODE_COUNT) {
