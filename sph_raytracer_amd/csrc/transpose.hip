@@ -12,19 +12,34 @@
 
 namespace sphrt {
 
-__global__ __launch_bounds__(256) void seg_keys_kernel(const int64_t* row_ptr, int64_t n_rays,
-                                                       const int32_t* vox, int32_t* keys,
-                                                       int32_t* idx, int32_t* seg_ray,
-                                                       int32_t* col_count) {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// Sort keys and values, one thread per segment (coalesced): key = voxel, value = segment.
+__global__ __launch_bounds__(256) void seg_keys_kernel(int64_t n_seg, const int32_t* vox,
+                                                       int32_t* keys, int32_t* idx) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= n_seg) return;
+    keys[s] = vox[s] & 0x7fffffff;
+    idx[s] = (int32_t)s;
+}
+
+// The ray of every segment: one wave per ray, its lanes over the ray's contiguous segments.
+__global__ __launch_bounds__(256) void seg_ray_kernel(const int64_t* row_ptr, int64_t n_rays,
+                                                      int32_t* seg_ray) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= n_rays) return;
-    for (int64_t s = row_ptr[r]; s < row_ptr[r + 1]; ++s) {
-        const int32_t v = vox[s] & 0x7fffffff;
-        keys[s] = v;
-        idx[s] = (int32_t)s;
-        seg_ray[s] = (int32_t)r;
-        atomicAdd(col_count + v, 1);
-    }
+    const int64_t a = row_ptr[r], e = row_ptr[r + 1];
+    for (int64_t s = a + (threadIdx.x & 63); s < e; s += 64) seg_ray[s] = (int32_t)r;
+}
+
+// col_ptr from the sorted voxel keys (no per-voxel atomics): at every key change from u to w,
+// voxels u+1 .. w start at position i; voxels up to the first key start at 0, those after the
+// last key at n.
+__global__ __launch_bounds__(256) void col_ptr_kernel(const int32_t* sorted, int64_t n,
+                                                      int64_t n_vox, int64_t* col_ptr) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i > n) return;
+    const int64_t lo = i == 0 ? -1 : (int64_t)sorted[i - 1];
+    const int64_t hi = i == n ? n_vox : (int64_t)sorted[i];
+    for (int64_t v = lo + 1; v <= hi; ++v) col_ptr[v] = i;
 }
 
 __global__ __launch_bounds__(256) void gather_cols_kernel(const int32_t* perm, int64_t n,
@@ -49,8 +64,8 @@ static size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 
 static size_t cub_bytes(int64_t n) {
     size_t b = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr,
-                                       (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 31);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr,
+                                             (int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, 31);
     return b;
 }
 
@@ -97,21 +112,29 @@ extern "C" int sphrt_csr_transpose(const sphrt_csr* c, int64_t n_vox, int64_t* c
     hipStream_t st = (hipStream_t)stream;
     TWs w;
     layout(c->n_segments, n_vox, (unsigned char*)workspace, &w);
-    if (hipMemsetAsync(w.count, 0, (size_t)n_vox * 4, st) != hipSuccess) return fail("memset failed");
-    if (c->n_rays > 0) {
-        hipLaunchKernelGGL(seg_keys_kernel, dim3((unsigned)((c->n_rays + 255) / 256)), dim3(256), 0,
-                           st, c->row_ptr, c->n_rays, c->vox, w.keys, w.idx, w.seg_ray, w.count);
-        if (int e = check_launch("seg_keys")) return e;
-    }
-    if (int e = sphrt_scan_counts(w.count, n_vox, col_ptr, w.scan, stream)) return e;
     const int64_t n = c->n_segments;
-    if (n == 0) return 0;
+    if (n == 0) {
+        if (hipMemsetAsync(col_ptr, 0, (size_t)(n_vox + 1) * 8, st) != hipSuccess)
+            return fail("memset failed");
+        return 0;
+    }
+    hipLaunchKernelGGL(seg_keys_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n,
+                       c->vox, w.keys, w.idx);
+    if (int e = check_launch("seg_keys")) return e;
+    if (c->n_rays > 0) {
+        hipLaunchKernelGGL(seg_ray_kernel, dim3((unsigned)((c->n_rays + 3) / 4)), dim3(256), 0, st,
+                           c->row_ptr, c->n_rays, w.seg_ray);
+        if (int e = check_launch("seg_ray")) return e;
+    }
     int bits = 1;
     while ((1LL << bits) < n_vox) ++bits;
     size_t cb = w.cub_bytes;
     if (hipcub::DeviceRadixSort::SortPairs(w.cub, cb, w.keys, w.keys_out, w.idx, w.perm, (int)n, 0,
                                            bits, st) != hipSuccess)
         return fail("radix sort failed");
+    hipLaunchKernelGGL(col_ptr_kernel, dim3((unsigned)((n + 1 + 255) / 256)), dim3(256), 0, st,
+                       w.keys_out, n, n_vox, col_ptr);
+    if (int e = check_launch("col_ptr")) return e;
     hipLaunchKernelGGL(gather_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                        w.perm, n, w.seg_ray, c->len, t_ray, t_len);
     return check_launch("gather_cols");

@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""The C5 retrieval (BASELINE configs[4], examples/static_retrieval.py shape): 64^3 grid, 64-view
+ConeCirc (100,50) orbit, FullyDenseModel, SquareLoss + NegRegularizer, Adam lr 0.1, float64
+coefficients, `gd` unchanged.  Reports the Operator construction, the measurement forward and the
+per-iteration time of `gd` (forward + autograd adjoint + Adam on the GPU; `gd` reads the loss
+values back every iteration, as the reference's progress bar does).
+
+    python tools/retrieval_bench.py [--iters 100] [--out profiles/r01_retrieval_c5.json]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--iters', type=int, default=100)
+    ap.add_argument('--out', default=None)
+    args = ap.parse_args()
+    import bench
+    from sph_raytracer_amd import Operator, retrieval
+    from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
+    from sph_raytracer_amd.model import FullyDenseModel
+    dev = torch.device('cuda', 0)
+    cfg = bench.CONFIGS['c5']
+    torch.manual_seed(0)
+    grid, geom = bench.build_geometry(cfg, 0, 1)
+    Operator(grid, geom, device=dev)            # warm-up (kernels loaded, allocator primed)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    op = Operator(grid, geom, device=dev)
+    torch.cuda.synchronize()
+    t_init = time.perf_counter() - t0
+    truth = torch.zeros(grid.shape, dtype=torch.float64, device=dev)   # static_retrieval.py:47-49
+    truth[:, 32:, :32] = 1
+    truth[:, :32, 32:] = 1
+    y = op(truth)
+    model = FullyDenseModel(grid)
+    losses = [SquareLoss(), NegRegularizer()]
+    retrieval.gd(op, y, model, num_iterations=3, loss_fns=losses, lr=1e-1, progress_bar=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    coeffs, y_hat, hist = retrieval.gd(op, y, model, num_iterations=args.iters, loss_fns=losses,
+                                       lr=1e-1, progress_bar=False)
+    torch.cuda.synchronize()
+    t_gd = time.perf_counter() - t0
+    fid = hist[losses[0]]
+    rec = {'config': 'C5 retrieval: 64^3 grid, 64-view ConeCirc (100,50) orbit, FullyDenseModel, '
+                     'SquareLoss + NegRegularizer, Adam lr 0.1, float64',
+           'rays': op._csr['n'], 'segments': op._csr['total'], 'iterations': args.iters,
+           'operator_init_ms': t_init * 1e3, 'gd_total_ms': t_gd * 1e3,
+           'ms_per_iteration': t_gd / args.iters * 1e3,
+           'fidelity_first': fid[0], 'fidelity_last': fid[-1],
+           'reference_cpu_s_per_iteration': 1.64,
+           'speedup_vs_reference_cpu': 1.64 / (t_gd / args.iters),
+           'peak_gb_resident': torch.cuda.max_memory_allocated(dev) / 1e9}
+    print(json.dumps(rec), flush=True)
+    if args.out:
+        with open(args.out, 'w') as f:
+            json.dump(rec, f, indent=1)
+
+
+if __name__ == '__main__':
+    main()
