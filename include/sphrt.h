@@ -134,7 +134,7 @@ int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const doubl
  * n_blocks = sphrt_csr_blocks(n_segments).  sphrt_csr_local_count/_fill then build tab and loc
  * (uint16, n_segments entries) for every block of at most 4096 segments and 2046 granules; with
  * loc/tab/n_cols/tab_stride set, a static forward on a 16-byte-aligned density stages each
- * block's granules in LDS (4 * (tab_stride + 1) elements, up to 48 KB) instead of gathering per
+ * block's granules in LDS (4 * (tab_stride + 1) elements, up to 64 KB) instead of gathering per
  * segment.
  * Per-segment arrays (vox, len, len32, loc) are read in aligned 8-entry chunks: allocate
  * them to round_up(n_segments, 8) entries (the entries past n_segments are never used).  `len32` is

@@ -487,7 +487,7 @@ class Operator:
         t = 'float, float' if d.dtype == tr.float32 else 'double, double'
         n_chan, div, _ = self._layout(d.shape)
         es = d.element_size()
-        table = (c.loc and div == 0 and 0 < c.tab_stride and (c.tab_stride + 1) * 4 * es <= 48 * 1024
+        table = (c.loc and div == 0 and 0 < c.tab_stride and (c.tab_stride + 1) * 4 * es <= 64 * 1024
                  and d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0))
         if table:
             return f'forward_kernel<{t}, 0, {"unsigned short" if c.tab_bytes == 2 else "int"}>'
