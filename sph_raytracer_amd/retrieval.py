@@ -58,6 +58,12 @@ def gd(f, y, model, coeffs=None, num_iterations=100, loss_fns=[SquareLoss()], op
     losses = {fn: [] for fn in loss_fns}
     o_stat = 0
     bar = _Bar(range(num_iterations), progress_bar)
+    # Without a progress bar nothing needs the loss values during the loop: they stay on the
+    # device and are read back once at the end (no host sync per iteration; same values, same
+    # return contract).  With a bar, every iteration reads them back as the reference does.
+    deferred = not progress_bar
+    pending = {fn: [] for fn in loss_fns}
+    improved = None                       # device flag: some iteration had total < best_loss
     try:
         for _ in bar:
             opt.zero_grad()
@@ -67,6 +73,9 @@ def gd(f, y, model, coeffs=None, num_iterations=100, loss_fns=[SquareLoss()], op
                 val = fn(f, y, density, coeffs)
                 if fn.use_grad and fn.kind != 'oracle':
                     total += val
+                if deferred:
+                    pending[fn].append(val.detach() if isinstance(val, t.Tensor) else val)
+                    continue
                 if fn.kind == 'oracle' and not math.isnan(val):
                     o_stat = val
                 elif fn.kind == 'fidelity':
@@ -74,13 +83,24 @@ def gd(f, y, model, coeffs=None, num_iterations=100, loss_fns=[SquareLoss()], op
                 elif fn.kind == 'regularizer':
                     r_stat += val
                 losses[fn].append(detach_loss(val))
-            bar.describe(f'F:{f_stat:.1e} R:{r_stat:.1e} O:{o_stat * 100:.0f}')
-            if total < best_loss:
-                best_coeffs = coeffs
+            if deferred:
+                ok = total < best_loss
+                improved = ok if improved is None else improved | ok
+            else:
+                bar.describe(f'F:{f_stat:.1e} R:{r_stat:.1e} O:{o_stat * 100:.0f}')
+                if total < best_loss:
+                    best_coeffs = coeffs
             total.backward(retain_graph=True)
             opt.step()
             if hasattr(model, 'proj'):
                 coeffs.data = model.proj(coeffs)
     except KeyboardInterrupt:
         pass
+    if deferred:
+        for fn, vals in pending.items():
+            tens = [v for v in vals if isinstance(v, t.Tensor)]
+            host = iter(t.stack(tens).cpu().tolist()) if tens else iter(())
+            losses[fn] = [next(host) if isinstance(v, t.Tensor) else v for v in vals]
+        if improved is not None and bool(improved):
+            best_coeffs = coeffs    # the same tensor object every iteration (updated in place)
     return best_coeffs, f(model(best_coeffs)), losses

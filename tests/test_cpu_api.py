@@ -219,6 +219,12 @@ def test_gd_with_linear_stand_in():
     hist = list(losses.values())[0]
     assert len(hist) == 20 and hist[-1] < hist[0]
     assert y_res.shape == (5, 6)
+    assert all(type(v) is float for vals in losses.values() for v in vals)
+    # loss values read back once at the end (no bar) == read back every iteration (bar)
+    c2, _, l2 = gd(f, y, FullyDenseModel(grid), num_iterations=20, lr=1e-2,
+                   loss_fns=[SquareLoss(), 0.5 * NegRegularizer()], progress_bar=True)
+    assert tr.equal(c2, coeffs)
+    assert [list(v) for v in l2.values()] == [list(v) for v in losses.values()]
 
 
 # ---- the C ABI library -------------------------------------------------------------------------
