@@ -14,6 +14,8 @@
 // gathers the density (a 0.5-8 MB volume, L2/MALL resident), reduces runs between head bits in
 // float64, and a block-level segmented scan stitches rows that cross thread chunks.  Balanced
 // whatever the row lengths, ~3 dependent global round trips per workgroup, deterministic order.
+#include <hipcub/hipcub.hpp>
+
 #include "common.hpp"
 
 namespace sphrt {
@@ -324,92 +326,9 @@ __device__ __forceinline__ uint16_t loc_code(int rank, uint32_t v, bool head) {
 // the granules into LDS with 16-byte LDS-DMA loads (one lane per granule, ~3x fewer lane accesses
 // than segments) and the segments read LDS.  n_tab = -1 marks a workgroup left on the
 // per-segment gather (more than kLocalMax segments or kMaxGran granules).
-template <bool FILL, typename TabT = int32_t>
-__global__ __launch_bounds__(kThreads) void local_table_kernel(int64_t* __restrict__ blocks,
-                                                               const int32_t* __restrict__ vox,
-                                                               uint16_t* __restrict__ loc,
-                                                               TabT* __restrict__ tab,
-                                                               int64_t tab_stride,
-                                                               unsigned long long* stats) {
-    __shared__ uint64_t key[kLocalMax];
-    __shared__ ScanShared sh;
-    int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
-    const int64_t s0 = m[2], s1 = m[3];
-    if (FILL && m[5] < 0) return;
-    const int n = (int)imin64(s1 - s0, (int64_t)kLocalMax + 1);
-    const int tid = threadIdx.x;
-    if (n > kLocalMax) {
-        if (tid == 0) {
-            m[5] = -1;
-            atomicAdd(stats, 1ull);
-        }
-        return;
-    }
-    int p = 1;
-    while (p < n) p <<= 1;
-    // key = voxel << 13 | position << 1 | head; voxel >> 2 is the granule
-    for (int i = tid; i < p; i += kThreads) {
-        uint64_t k = ~0ull;
-        if (i < n) {
-            const uint32_t x = (uint32_t)vox[s0 + i];
-            k = ((uint64_t)(x & ~kHead) << 13) | ((uint64_t)i << 1) | (uint64_t)(x >> 31);
-        }
-        key[i] = k;
-    }
-    __syncthreads();
-    for (int k = 2; k <= p; k <<= 1)          // bitonic sort, ascending
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < p; i += kThreads) {
-                const int ij = i ^ j;
-                if (ij > i) {
-                    const uint64_t x = key[i], y = key[ij];
-                    if (((i & k) == 0) == (x > y)) {
-                        key[i] = y;
-                        key[ij] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    // distinct granules: thread t owns sorted entries [16t, 16t+16)
-    constexpr int kEach = kLocalMax / kThreads;
-    auto gran = [](uint64_t k) { return k >> 15; };
-    int first_new = 0;
-#pragma unroll
-    for (int q = 0; q < kEach; ++q) {
-        const int i = tid * kEach + q;
-        if (i < n && (i == 0 || gran(key[i]) != gran(key[i - 1]))) ++first_new;
-    }
-    int n_tab;
-    int rank = block_excl_count(first_new, n_tab, sh) - 1;
-    if (!FILL) {                               // pass 1: table sizes, fallbacks, largest table
-        if (tid == 0) {
-            if (n_tab > kMaxGran) {
-                m[5] = -1;
-                atomicAdd(stats, 1ull);
-            } else {
-                m[5] = n_tab;
-                atomicMax(stats + 1, (unsigned long long)n_tab);
-            }
-        }
-        return;
-    }
-#pragma unroll
-    for (int q = 0; q < kEach; ++q) {
-        const int i = tid * kEach + q;
-        if (i >= n) break;
-        const uint64_t k = key[i];
-        if (i == 0 || gran(k) != gran(key[i - 1])) {
-            ++rank;
-            tab[(int64_t)blockIdx.x * tab_stride + rank] = (TabT)gran(k);
-        }
-        const int pos = (int)((k >> 1) & 0xfff);
-        loc[s0 + pos] = loc_code(rank, (uint32_t)(k >> 13), (k & 1) != 0);
-    }
-}
 
-// The same tables from a bitmap of the volume's granules in LDS instead of a sort, when the
-// bitmap fits (n_cols/4 bits; 128^3 voxels = 64 KiB): set one bit per segment, prefix-popcount
+// The tables from a bitmap of the volume's granules in LDS, when the
+// bitmap is small (n_cols/4 bits; 128^3 voxels = 64 KiB): set one bit per segment, prefix-popcount
 // the words, and a granule's rank is the number of set bits below it.  O(segments + words) per
 // workgroup, a handful of barriers.  Identical output to the sort (ascending distinct granules).
 template <bool FILL, typename TabT = int32_t>
@@ -475,6 +394,88 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
         const uint32_t v = x & ~kHead, g = v >> 2;
         const int rank = pre[g >> 5] + __builtin_popcount(bm[g >> 5] & ((1u << (g & 31)) - 1u));
         loc[s0 + i] = loc_code(rank, v, (x & kHead) != 0);
+    }
+}
+
+// Large volumes (the bitmap would not fit, or costs more than the segments): the same tables
+// from a block radix sort of the workgroup's segments by granule (hipCUB, 16 per thread), value
+// = position << 3 | head << 2 | voxel & 3.  O(segments · key bits) per workgroup instead of
+// O(volume): at C3 (2 M voxels, 64 k workgroups) 10.6 ms of bitmap work.  Identical output.
+constexpr int kRadixItems = kLocalMax / kThreads;   // 16
+template <bool FILL, typename TabT = int32_t>
+__global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
+    int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
+    TabT* __restrict__ tab, int64_t tab_stride, int key_bits, unsigned long long* stats) {
+    using Sort = hipcub::BlockRadixSort<uint32_t, kThreads, kRadixItems, uint16_t>;
+    __shared__ typename Sort::TempStorage sort_ts;
+    __shared__ uint32_t last_key[kThreads];
+    __shared__ ScanShared sh;
+    int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
+    const int64_t s0 = m[2], s1 = m[3];
+    if (FILL && m[5] < 0) return;
+    const int tid = threadIdx.x;
+    const int64_t n = s1 - s0;
+    if (n > kLocalMax) {
+        if (!FILL && tid == 0) {
+            m[5] = -1;
+            atomicAdd(stats, 1ull);
+        }
+        return;
+    }
+    uint32_t key[kRadixItems];
+    uint16_t val[kRadixItems];
+#pragma unroll
+    for (int i = 0; i < kRadixItems; ++i) {
+        const int p = tid * kRadixItems + i;
+        key[i] = 0xffffffffu;                     // padding sorts last
+        val[i] = 0;
+        if (p < n) {
+            const uint32_t x = (uint32_t)vox[s0 + p];
+            const uint32_t v = x & ~kHead;
+            key[i] = v >> 2;
+            val[i] = (uint16_t)((p << 3) | ((x >> 31) << 2) | (v & 3u));
+        }
+    }
+    Sort(sort_ts).Sort(key, val, 0, key_bits);   // blocked: thread t holds sorted [16t, 16t+16)
+    last_key[tid] = key[kRadixItems - 1];
+    __syncthreads();
+    uint32_t prev = tid > 0 ? last_key[tid - 1] : 0xffffffffu;
+    int first_new = 0;
+#pragma unroll
+    for (int i = 0; i < kRadixItems; ++i) {
+        const int p = tid * kRadixItems + i;
+        const bool fresh = p < n && (p == 0 || key[i] != prev);
+        first_new += fresh ? 1 : 0;
+        prev = key[i];
+    }
+    int n_tab;
+    int rank = block_excl_count(first_new, n_tab, sh) - 1;
+    if (!FILL) {
+        if (tid == 0) {
+            if (n_tab > kMaxGran) {
+                m[5] = -1;
+                atomicAdd(stats, 1ull);
+            } else {
+                m[5] = n_tab;
+                atomicMax(stats + 1, (unsigned long long)n_tab);
+            }
+        }
+        return;
+    }
+    prev = tid > 0 ? last_key[tid - 1] : 0xffffffffu;
+    TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
+#pragma unroll
+    for (int i = 0; i < kRadixItems; ++i) {
+        const int p = tid * kRadixItems + i;
+        if (p < n) {
+            if (p == 0 || key[i] != prev) {
+                ++rank;
+                tab_b[rank] = (TabT)key[i];
+            }
+            const uint32_t w = val[i];
+            loc[s0 + (w >> 3)] = loc_code(rank, w & 3u, (w >> 2) & 1u);
+        }
+        prev = key[i];
     }
 }
 
@@ -1038,10 +1039,17 @@ extern "C" int sphrt_diag_fwd_stamps(unsigned long long* host, int64_t n) {
 }
 #endif
 
-// bitmap words for a volume of n_cols voxels, or 0 when the bitmap does not fit in LDS
+// bitmap words for a volume of n_cols voxels, or 0 when the bitmap costs more than sorting the
+// workgroup's segments (every workgroup clears and scans the whole bitmap: <= 4096 words, i.e.
+// volumes up to 2^19 voxels; larger ones take the radix sort)
 static int table_bitmap_words(int64_t n_cols) {
     const int64_t words = ((n_cols + 3) / 4 + 31) / 32;
-    return n_cols > 0 && words * 8 <= 150 * 1024 ? (int)words : 0;
+    return n_cols > 0 && words <= 4096 ? (int)words : 0;
+}
+static int granule_key_bits(int64_t n_cols) {
+    int b = 1;
+    while ((1LL << b) < (n_cols + 3) / 4) ++b;
+    return b;
 }
 
 extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_t* stats,
@@ -1058,9 +1066,10 @@ extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_
                            0, words, (unsigned long long*)stats);
         return check_launch("local_table_bitmap_kernel<count>");
     }
-    hipLaunchKernelGGL((local_table_kernel<false, int32_t>), dim3((unsigned)c->n_blocks), dim3(kThreads), 0,
-                       st, blocks, c->vox, nullptr, nullptr, 0, (unsigned long long*)stats);
-    return check_launch("local_table_kernel<count>");
+    hipLaunchKernelGGL((local_table_radix_kernel<false, int32_t>), dim3((unsigned)c->n_blocks),
+                       dim3(kThreads), 0, st, blocks, c->vox, nullptr, nullptr, 0,
+                       granule_key_bits(c->n_cols), (unsigned long long*)stats);
+    return check_launch("local_table_radix_kernel<count>");
 }
 
 extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, uint16_t* loc,
@@ -1084,15 +1093,16 @@ extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, u
                                (int32_t*)tab, tab_stride, words, nullptr);
         return check_launch("local_table_bitmap_kernel<fill>");
     }
+    const int kb = granule_key_bits(c->n_cols);
     if (u16)
-        hipLaunchKernelGGL((local_table_kernel<true, uint16_t>), dim3((unsigned)c->n_blocks),
+        hipLaunchKernelGGL((local_table_radix_kernel<true, uint16_t>), dim3((unsigned)c->n_blocks),
                            dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (uint16_t*)tab,
-                           tab_stride, nullptr);
+                           tab_stride, kb, nullptr);
     else
-        hipLaunchKernelGGL((local_table_kernel<true, int32_t>), dim3((unsigned)c->n_blocks),
+        hipLaunchKernelGGL((local_table_radix_kernel<true, int32_t>), dim3((unsigned)c->n_blocks),
                            dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (int32_t*)tab,
-                           tab_stride, nullptr);
-    return check_launch("local_table_kernel<fill>");
+                           tab_stride, kb, nullptr);
+    return check_launch("local_table_radix_kernel<fill>");
 }
 
 static int check_csr(const sphrt_csr* c, int64_t n_chan, int64_t div) {

@@ -102,19 +102,30 @@ def test_fused_equals_csr(c2, gpu):
 
 
 def test_granule_tables(c2, gpu):
-    """Per-workgroup granule tables (sphrt_csr_local): each table ascending and distinct, every
-    segment's slot names its voxel's granule and lane and carries its row-head flag; the table
-    forward equals the per-segment-gather forward bitwise, for the forward and the transposed
-    adjoint."""
+    """Per-workgroup granule tables (sphrt_csr_local, LDS-bitmap build at 50^3): each table
+    ascending and distinct, every segment's slot names its voxel's granule and lane and carries
+    its row-head flag; the table forward equals the per-segment-gather forward bitwise, for the
+    forward and the transposed adjoint."""
+    _check_granule_tables(*c2, gpu, tab_bytes=2)
+
+
+def test_granule_tables_radix_build(gpu):
+    """The same checks on a grid above 2^19 voxels, whose tables come from the block radix sort
+    (and have 32-bit entries)."""
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(3, (48, 64), grid_shape=(96, 80, 90))
+    _check_granule_tables(grid, geom, Operator(grid, geom, device=gpu), gpu, tab_bytes=4)
+
+
+def _check_granule_tables(grid, geom, op, gpu, tab_bytes):
     from sph_raytracer_amd import _lib
-    grid, geom, op = c2
     csr = op._csr
     blocks = csr['blocks'].cpu().numpy().reshape(-1, _lib.BLOCK_FIELDS)
     vox = csr['vox'].cpu().numpy().view(np.uint32)[:csr['total']]
     loc = csr['loc'].cpu().numpy().view(np.uint16)[:csr['total']]
     tab = csr['tab'].cpu().numpy()
-    assert csr['desc'].tab_bytes == 2 and tab.dtype == np.int16   # 50^3 voxels: 16-bit entries
-    tab = tab.view(np.uint16).astype(np.int64)
+    assert csr['desc'].tab_bytes == tab_bytes
+    tab = tab.view(np.uint16).astype(np.int64) if tab_bytes == 2 else tab.astype(np.int64)
     s0, s1, n_tab = blocks[:, 2], blocks[:, 3], blocks[:, 5]
     assert (n_tab >= 0).all() and (n_tab <= s1 - s0).all() and csr['desc'].n_fallback == 0
     owner = np.repeat(np.arange(len(blocks)), s1 - s0)
