@@ -131,37 +131,51 @@ __device__ __forceinline__ uint64_t xlane64(uint64_t x, int lane) {
 }
 
 // One compare-exchange layer of the ascending-only ("flip") bitonic network over 64*M elements,
-// element e = i*64 + lane; partner = e ^ MASK.
+// lane-major: element e = lane*M + i, partner e ^ MASK.  Bits of MASK below M pair registers of
+// the same lane (no lane exchange: the 1-, 2-... layers, which every stage ends with); the rest
+// is a lane xor.  (The register-major order e = i*64 + lane exchanged lanes in all but the top
+// layers: 33 of 36 layers at M = 4 against 21 now.)
+template <int M>
+constexpr int kLogM = M == 1 ? 0 : M == 2 ? 1 : M == 4 ? 2 : 3;
 template <int M, int MASK>
 __device__ __forceinline__ void cas_layer(uint64_t (&k)[M], uint32_t (&p)[M], int lane) {
-    constexpr int LM = MASK & 63;
-    uint64_t nk[M];
-    uint32_t np[M];
+    constexpr int IM = MASK & (M - 1);          // register-index xor
+    constexpr int LM = MASK >> kLogM<M>;        // lane xor
+    if constexpr (LM == 0) {
 #pragma unroll
-    for (int i = 0; i < M; ++i) {
-        const int pi = i ^ (MASK >> 6);
-        uint64_t ok;
-        uint32_t op;
-        if constexpr (LM == 0) {
-            ok = k[pi];
-            op = p[pi];
-        } else {
-            ok = xlane64<LM>(k[pi], lane);
-            op = xlane<LM>(p[pi], lane);
+        for (int i = 0; i < M; ++i) {
+            const int pi = i ^ IM;
+            if (pi < i) continue;                   // each in-lane pair once: lower keeps the min
+            // (key, payload) pairs are distinct except the identical padding entries
+            const bool sw = pair_less(k[pi], p[pi], k[i], p[i]);
+            const uint64_t ka = k[i], kb = k[pi];
+            const uint32_t pa = p[i], pb = p[pi];
+            k[i] = sw ? kb : ka;
+            p[i] = sw ? pb : pa;
+            k[pi] = sw ? ka : kb;
+            p[pi] = sw ? pa : pb;
         }
-        const int e = i * 64 + lane;
-        const int pe = pi * 64 + (lane ^ LM);
-        // (key, payload) pairs are distinct (the candidate index is in the payload) except the
-        // identical padding entries, so "mine < other" is !(other < mine): one comparison
-        const bool lt = pair_less(ok, op, k[i], p[i]);
-        const bool take = (e < pe) ? lt : !lt;
-        nk[i] = take ? ok : k[i];
-        np[i] = take ? op : p[i];
-    }
+    } else {
+        uint64_t nk[M];
+        uint32_t np[M];
 #pragma unroll
-    for (int i = 0; i < M; ++i) {
-        k[i] = nk[i];
-        p[i] = np[i];
+        for (int i = 0; i < M; ++i) {
+            const int pi = i ^ IM;
+            const uint64_t ok = xlane64<LM>(k[pi], lane);
+            const uint32_t op = xlane<LM>(p[pi], lane);
+            const int e = lane * M + i;
+            const int pe = (lane ^ LM) * M + pi;
+            // "mine < other" is !(other < mine): one comparison per element
+            const bool lt = pair_less(ok, op, k[i], p[i]);
+            const bool take = (e < pe) ? lt : !lt;
+            nk[i] = take ? ok : k[i];
+            np[i] = take ? op : p[i];
+        }
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            k[i] = nk[i];
+            p[i] = np[i];
+        }
     }
 }
 
@@ -188,7 +202,7 @@ __device__ void sort_regs(uint64_t* keys, uint32_t* pays, int F, int lane) {
     uint32_t p[M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-        const int e = i * 64 + lane;
+        const int e = lane * M + i;
         const bool r = e < F;
         k[i] = r ? keys[e] : ~0ull;
         p[i] = r ? pays[e] : ~0u;
@@ -197,7 +211,7 @@ __device__ void sort_regs(uint64_t* keys, uint32_t* pays, int F, int lane) {
     wave_sync();
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-        const int e = i * 64 + lane;
+        const int e = lane * M + i;
         if (e < F) {
             keys[e] = k[i];
             pays[e] = p[i];
