@@ -8,7 +8,7 @@
 //      non-negative crossings to a per-wave LDS list (ballot + mbcnt compaction); the most
 //      negative finite distance is reduced across the wave (it bounds the behind-start segment);
 //   2. the list is sorted by (distance, candidate index) — a total order equal to a stable sort
-//      of the reference's concatenation — in registers (<= 256 entries) or in LDS;
+//      of the reference's concatenation — in registers (<= 512 entries) or in LDS;
 //   3. 64-entry chunks are scanned (forward fill of the r/e/a rows), differenced and the
 //      non-zero in-grid segments compacted, in order, back into LDS;
 //   4. depending on MODE the segments are counted, copied to the CSR, or integrated against
@@ -485,6 +485,9 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     else if (F <= 128) sort_regs<2>(keys, pays, F, lane);
 #if !defined(SPHRT_TRACE_NO_M4)
     else if (F <= 256) sort_regs<4>(keys, pays, F, lane);
+#endif
+#if !defined(SPHRT_TRACE_NO_M8)
+    else if (F <= 512) sort_regs<8>(keys, pays, F, lane);   // C3: 15 % of hit rays; 5.3 -> 4.5 ms
 #endif
     else sort_lds(keys, pays, F, lane);
 
