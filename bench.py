@@ -40,6 +40,10 @@ CONFIGS = {
            'C3: (128,128,128) grid, 128-view orbit x ConeRect (128,256), fp32 forward'),
     'c5': ((64, 64, 64), 64, (100, 50), 'circ', torch.float64,
            'C5: (64,64,64) grid, 64-view orbit x ConeCirc (100,50), fp64 forward'),
+    # dynamic grid: view i sees time slice i (Operator(..., dynamic=True), raytracer.py:703-712)
+    'c4': ((50, 50, 50, 50), 50, (100, 50), 'circ', torch.float32,
+           'C4: dynamic (50,50,50,50) grid, 50-view orbit x ConeCirc (100,50), view i <-> time i, '
+           'fp32 forward'),
 }
 
 
@@ -118,12 +122,13 @@ def cpu_baseline(cfg, sample_views, reps):
     regs, lens = ref_forward.dense_trace((grid.r_b, grid.e_b, grid.a_b), xs.numpy(), rays.numpy(),
                                          starts.numpy())
     t_trace = time.perf_counter() - t0
-    x = torch.rand(shape, dtype=dtype)
-    ref_forward.forward(regs, lens, x)           # warm-up
+    dyn = grid.dynamic          # view i <-> time i: the sample's views take the first slices
+    x = torch.rand((views,) + tuple(shape[1:]) if dyn else shape, dtype=dtype)
+    ref_forward.forward(regs, lens, x, dynamic=dyn)           # warm-up
     times = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        ref_forward.forward(regs, lens, x)
+        ref_forward.forward(regs, lens, x, dynamic=dyn)
         times.append(time.perf_counter() - t0)
     n = lens.numel() // lens.shape[-1]
     med = sorted(times)[len(times) // 2]
@@ -181,7 +186,7 @@ def main():
     t0 = time.perf_counter()
     if dist is None:
         grid, geom = build_geometry(cfg, 0, 1)
-        sop = op = Operator(grid, geom, device=dev)
+        sop = op = Operator(grid, geom, device=dev, dynamic=grid.dynamic)
     else:   # every rank sees the whole 50*N-view orbit and keeps its contiguous 50-view shard
         from sph_raytracer_amd.distributed import ShardedOperator
         grid, geom = build_geometry((shape, n_views * world) + cfg[2:], 0, 1)
@@ -236,7 +241,7 @@ def main():
         barrier()
         t0 = time.perf_counter()
         grid2, geom2 = build_geometry(cfg, rank, world)
-        op2 = Operator(grid2, geom2, device=dev)
+        op2 = Operator(grid2, geom2, device=dev, dynamic=grid2.dynamic)
         op2(x)
         torch.cuda.synchronize(dev)
         colds.append(time.perf_counter() - t0)

@@ -173,6 +173,13 @@ int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_
 int sphrt_csr_local_count(const sphrt_csr *csr, int64_t *blocks, int64_t *stats, void *stream);
 int sphrt_csr_local_fill(const sphrt_csr *csr, const int64_t *blocks, uint16_t *loc, void *tab,
                          int64_t tab_stride, void *stream);
+/* Time-paired columns for a dynamic operator whose view i sees time slice i (ray r reads slice
+ * r / div): vox_out[s] = (r / div) * vol + voxel, head bit kept, for every segment of ray r.  A
+ * CSR with these columns (and its own blocks / tables, n_cols = T * vol) is a static CSR over the
+ * flattened (T, vol) density: granule-table forward, transposed deterministic adjoint.
+ * Requires T * vol < 2^31. */
+int sphrt_csr_time_columns(const sphrt_csr *csr, int64_t div, int64_t vol, int32_t *vox_out,
+                           void *stream);
 
 /* ---- forward line integral on the CSR (replaces Operator.__call__, raytracer.py:692-713) -- */
 /* out[c*out_chan_stride + i] = sum_s density[c*chan_stride + vox[s]] * len[s] over ray i's row.

@@ -67,6 +67,7 @@ _SIGNATURES = [
     ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     ('sphrt_csr_local_count', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp]),
     ('sphrt_csr_local_fill', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp]),
+    ('sphrt_csr_time_columns', c_int, [ctypes.POINTER(CSR), c_i64, c_i64, c_vp, c_vp]),
     ('sphrt_forward_f32', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,
                                   c_vp]),
     ('sphrt_forward_f64', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,

@@ -994,9 +994,36 @@ __global__ __launch_bounds__(kThreads) void adjoint_kernel(
     }
 }
 
+// Time-paired columns: ray r reads time slice r / div, so its segments' columns become
+// (r / div) * vol + voxel (head bit kept).  One wave per ray over its contiguous segments.
+__global__ __launch_bounds__(256) void time_columns_kernel(const int64_t* row_ptr, int64_t n_rays,
+                                                           const int32_t* vox, int64_t div,
+                                                           int64_t vol, int32_t* out) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= n_rays) return;
+    const int64_t base = (r / div) * vol;
+    const int64_t a = row_ptr[r], e = row_ptr[r + 1];
+    for (int64_t s = a + (threadIdx.x & 63); s < e; s += 64) {
+        const uint32_t x = (uint32_t)vox[s];
+        out[s] = (int32_t)((x & kHead) | (uint32_t)(base + (int64_t)(x & ~kHead)));
+    }
+}
+
 }  // namespace sphrt
 
 using namespace sphrt;
+
+extern "C" int sphrt_csr_time_columns(const sphrt_csr* c, int64_t div, int64_t vol,
+                                      int32_t* vox_out, void* stream) {
+    if (!c || !c->row_ptr || !c->vox || !vox_out) return fail("incomplete CSR");
+    if (div < 1 || vol < 1) return fail("bad time pairing (div, vol)");
+    const int64_t n_t = (c->n_rays + div - 1) / div;
+    if (n_t * vol >= (int64_t)kHead) return fail("time-paired columns need T * voxels < 2^31");
+    if (c->n_rays == 0) return 0;
+    hipLaunchKernelGGL(time_columns_kernel, dim3((unsigned)((c->n_rays + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, c->row_ptr, c->n_rays, c->vox, div, vol, vox_out);
+    return check_launch("time_columns");
+}
 
 extern "C" int64_t sphrt_csr_blocks(int64_t n_segments) {
     return n_segments < 0 ? -1 : n_segments / kSegPerBlock + 1;

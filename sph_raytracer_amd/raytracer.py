@@ -470,22 +470,35 @@ class Operator:
             csr['desc'].len32 = l32.data_ptr()
         return csr['len32']
 
+    def _launch_args(self, d, n_chan, div):
+        """(csr desc, n_chan, chan_stride, div) of the launch for density d: a view <-> time
+        pairing runs as a static single-channel forward over the flattened (T, vol) density on
+        the time-paired CSR (its granule tables apply); everything else on the trace's CSR."""
+        vol = math.prod(self.grid.shape[-3:])
+        if div > 0:
+            rec = self._paired(d.shape[0], div)
+            if rec is not None:
+                rec['desc'].len32 = self._csr['desc'].len32
+                return rec['desc'], 1, rec['desc'].n_cols, 0
+        return self._csr['desc'], n_chan, vol, div
+
     def _launch_forward(self, d, out, n_chan, div):
         """Enqueue the forward kernel on the current stream: d (contiguous, compute device,
         float32/float64) -> out (preallocated, same dtype).  No allocation, no host sync."""
         csr = self._csr
         lib = _lib.load()
         self._lengths(d.dtype)
+        desc, n_chan, cs, div = self._launch_args(d, n_chan, div)
         fn = lib.sphrt_forward_f32 if d.dtype == tr.float32 else lib.sphrt_forward_f64
-        _lib.check(fn(csr['desc'], _lib.ptr(d), n_chan, math.prod(self.grid.shape[-3:]), div,
-                      _lib.ptr(out), csr['n'], _lib.stream_of(self._cdev)), 'sphrt_forward')
+        _lib.check(fn(desc, _lib.ptr(d), n_chan, cs, div, _lib.ptr(out), csr['n'],
+                      _lib.stream_of(self._cdev)), 'sphrt_forward')
 
     def _forward_kernel_name(self, d):
         """The forward kernel instantiation a launch on `d` runs (sphrt_forward_*'s choice, for
         reports): 0 = granule tables staged in LDS, 1 = per-segment gathers, 2 = time slices."""
-        c = self._csr['desc']
         t = 'float, float' if d.dtype == tr.float32 else 'double, double'
         n_chan, div, _ = self._layout(d.shape)
+        c, n_chan, _, div = self._launch_args(d, n_chan, div)
         es = d.element_size()
         table = (c.loc and div == 0 and 0 < c.tab_stride and (c.tab_stride + 1) * 4 * es <= 64 * 1024
                  and d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0))
@@ -508,17 +521,17 @@ class Operator:
         if density.device == dev and density.dtype == cdt and density.is_contiguous():
             lib = _lib.load()
             fn = lib.sphrt_forward_f32 if cdt == tr.float32 else lib.sphrt_forward_f64
+            desc, b_chan, b_cs, b_div = self._launch_args(d, n_chan, div)
             self._fast[(density.shape, density.dtype, density.device)] = (
-                fn, ctypes.byref(self._csr['desc']), n_chan, math.prod(self.grid.shape[-3:]), div,
-                n, alloc, tuple(out_shape))
+                fn, ctypes.byref(desc), b_chan, b_cs, b_div, n, alloc, tuple(out_shape))
             fast = _lib.load_fast()
             if fast is not None:
                 if self._fastc is None:
                     self._fastfn = fast.forward
                     self._fastc = fast.new(_lib.address(lib.sphrt_last_error))
                 fast.add(self._fastc, tuple(density.shape), cdt == tr.float64, dev.index,
-                         _lib.address(fn), ctypes.addressof(self._csr['desc']), n_chan,
-                         math.prod(self.grid.shape[-3:]), div, n, tuple(out_shape))
+                         _lib.address(fn), ctypes.addressof(desc), b_chan, b_cs, b_div, n,
+                         tuple(out_shape))
         out = out.view(out_shape)
         if out.device != density.device or cdt != in_dtype:
             out = out.to(device=density.device, dtype=in_dtype)
@@ -529,17 +542,22 @@ class Operator:
         forward's segmented gather-reduce with rays and voxels swapped — no atomics,
         bitwise reproducible."""
         csr = self._csr
-        if 'T' in csr:
-            return csr['T']
+        if 'T' not in csr:
+            csr['T'] = self._transpose_of(csr['desc'], math.prod(self.grid.shape[-3:]))
+        return csr['T']
+
+    def _transpose_of(self, src, n_cols):
+        """Transpose of the CSR `src` (columns < n_cols) with its own index and granule tables."""
+        csr = self._csr
         lib, dev = _lib.load(), self._cdev
         stream = _lib.stream_of(dev)
-        n_vox = math.prod(self.grid.shape[-3:])
+        n_vox = n_cols
         total = csr['total']
         col_ptr = tr.empty(n_vox + 1, dtype=tr.int64, device=dev)
         t_ray = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
         t_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
         ws = tr.empty(lib.sphrt_transpose_workspace_bytes(total, n_vox), dtype=tr.uint8, device=dev)
-        _lib.check(lib.sphrt_csr_transpose(csr['desc'], n_vox, _lib.ptr(col_ptr), _lib.ptr(t_ray),
+        _lib.check(lib.sphrt_csr_transpose(src, n_vox, _lib.ptr(col_ptr), _lib.ptr(t_ray),
                                            _lib.ptr(t_len), _lib.ptr(ws), ws.numel(), stream),
                    'sphrt_csr_transpose')
         del ws
@@ -562,9 +580,35 @@ class Operator:
         c.empty_ray = empty_vox.data_ptr()
         c.n_cols = csr['n']
         loc, tab = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
-        csr['T'] = dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, empty_vox, blocks,
-                                      loc, tab))
-        return csr['T']
+        return dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, empty_vox, blocks,
+                                  loc, tab))
+
+    def _paired(self, T, div):
+        """The trace with time-paired columns (ray r reads slice r // div: column
+        (r // div) * vol + voxel), its own blocks and granule tables: a view <-> time pairing is
+        then a static forward over the flattened (T, vol) density, and its adjoint the
+        transposed forward (deterministic, no atomics).  None when T * vol >= 2^31."""
+        csr = self._csr
+        key = ('paired', T, div)
+        if key in csr:
+            return csr[key]
+        vol = math.prod(self.grid.shape[-3:])
+        if T * vol >= 2 ** 31 - 1 or -(-csr['n'] // div) > T:
+            csr[key] = None
+            return None
+        lib, dev = _lib.load(), self._cdev
+        stream = _lib.stream_of(dev)
+        total, nblocks = csr['total'], csr['nblocks']
+        vox_p = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+        _lib.check(lib.sphrt_csr_time_columns(csr['desc'], div, vol, _lib.ptr(vox_p), stream),
+                   'sphrt_csr_time_columns')
+        blocks_p = csr['blocks'].clone()            # n_tab (field 5) is per table set
+        c = _lib.CSR.from_buffer_copy(csr['desc'])
+        c.vox, c.blocks, c.n_cols = vox_p.data_ptr(), blocks_p.data_ptr(), T * vol
+        c.loc, c.tab, c.tab_stride, c.n_fallback = None, None, 0, 0
+        loc, tab = _local_tables(lib, c, blocks_p, nblocks, total, dev, stream)
+        csr[key] = dict(desc=c, keep=(vox_p, blocks_p, loc, tab), n_t=T)
+        return csr[key]
 
     def _apply_adjoint(self, y, dshape, ddtype, ddevice):
         dev = self._cdev
@@ -576,14 +620,21 @@ class Operator:
         yv = y.detach().to(device=dev, dtype=ydt).reshape(-1).contiguous()
         if yv.numel() != n_chan * n:
             raise ValueError(f'adjoint input has {yv.numel()} values, expected {n_chan * n}')
-        if div == 0 and self.adjoint_mode == 'transpose':
+        paired = self._paired(dshape[0], div) if div > 0 else None
+        if self.adjoint_mode == 'transpose' and (div == 0 or paired is not None):
             cdt = ddtype if ddtype in (tr.float32, tr.float64) else tr.float32
             yv = yv.to(cdt)
+            if paired is not None:      # columns of the flattened (T, vol) density
+                if 'transposed' not in paired:
+                    paired['transposed'] = self._transpose_of(paired['desc'], paired['desc'].n_cols)
+                tdesc, n_chan, vol = paired['transposed']['desc'], 1, paired['desc'].n_cols
+            else:
+                tdesc = self._transposed()['desc']
             res = tr.empty(n_chan * vol, dtype=cdt, device=dev)
             lib = _lib.load()
             fn = lib.sphrt_forward_f32 if cdt == tr.float32 else lib.sphrt_forward_f64
-            _lib.check(fn(self._transposed()['desc'], _lib.ptr(yv), n_chan, n, 0, _lib.ptr(res),
-                          vol, _lib.stream_of(dev)), 'adjoint (transposed forward)')
+            _lib.check(fn(tdesc, _lib.ptr(yv), n_chan, n, 0, _lib.ptr(res), vol,
+                          _lib.stream_of(dev)), 'adjoint (transposed forward)')
             return res.reshape(dshape).to(device=ddevice, dtype=ddtype)
         acc = tr.zeros(math.prod(dshape), dtype=tr.float64, device=dev)
         _lib.check(_lib.load().sphrt_adjoint_accumulate(

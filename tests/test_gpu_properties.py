@@ -343,3 +343,45 @@ def test_fast_path_matches_general_path(c2, gpu):
         x2 = tr.stack([x, 2 * x])
         y3 = op(x2)
         assert y3.shape == (2,) + tuple(geom.shape) and tr.equal(y3[0], y0)
+
+
+def test_dynamic_pairing_forward_and_adjoint(gpu):
+    """View i <-> time slice i (dynamic grid, a collection of T views): the forward runs on the
+    time-paired CSR (granule tables over the flattened (T, vol) density) and the adjoint on its
+    transpose.  Forward equals the per-segment time-slice gather of the trace's CSR bitwise in
+    float64 up to summation order (1e-12), the adjoint equals the float64-atomic adjoint, and
+    <A x, y> = <x, A^T y>."""
+    from sph_raytracer_amd import ConeCircGeom, Operator, SphericalGrid
+    T = 6
+    grid = SphericalGrid(shape=(T, 20, 18, 24))
+    geom = sum(ConeCircGeom(shape=(30, 20), pos=(5 * tr.cos(th), 5 * tr.sin(th), 1), fov=(0, 45))
+               for th in tr.linspace(0, 2 * tr.pi, T))
+    op = Operator(grid, geom, dynamic=True, device=gpu)
+    g = tr.Generator(device=gpu).manual_seed(7)
+    x = tr.rand(grid.shape, dtype=tr.float64, device=gpu, generator=g)
+    y = tr.rand(geom.shape, dtype=tr.float64, device=gpu, generator=g)
+    fx = op(x)
+    n_chan, div, _ = op._layout(x.shape)
+    assert div > 0 and op._paired(T, div) is not None
+    assert op._forward_kernel_name(x).startswith('forward_kernel<double, double, 0')
+    # the trace's own CSR with the time-slice gather (kFwdDynamic)
+    ref = tr.empty(op._csr['n'], dtype=tr.float64, device=gpu)
+    lib = __import__('sph_raytracer_amd._lib', fromlist=['_lib'])
+    lib.check(lib.load().sphrt_forward_f64(op._csr['desc'], lib.ptr(x), 1, x[0].numel(), div,
+                                           lib.ptr(ref), op._csr['n'], lib.stream_of(gpu)), 'fwd')
+    assert tr.allclose(fx.reshape(-1), ref, rtol=1e-12, atol=1e-14)
+    xg = x.clone().requires_grad_(True)
+    (op(xg) * y).sum().backward()
+    atx = xg.grad
+    op.adjoint_mode = 'atomic'
+    xa = x.clone().requires_grad_(True)
+    (op(xa) * y).sum().backward()
+    op.adjoint_mode = 'transpose'
+    assert tr.allclose(atx, xa.grad, rtol=1e-12, atol=1e-14)
+    lhs, rhs = (fx * y).sum().item(), (x * atx).sum().item()
+    assert abs(lhs - rhs) <= 1e-12 * abs(lhs)
+    xg2 = x.clone().requires_grad_(True)
+    (op(xg2) * y).sum().backward()
+    assert tr.equal(xg2.grad, atx)                       # deterministic
+    f32 = op(x.float())
+    assert tr.allclose(f32.double(), fx, rtol=1e-5, atol=1e-6)
