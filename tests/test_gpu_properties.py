@@ -385,3 +385,4 @@ def test_dynamic_pairing_forward_and_adjoint(gpu):
     assert tr.equal(xg2.grad, atx)                       # deterministic
     f32 = op(x.float())
     assert tr.allclose(f32.double(), fx, rtol=1e-5, atol=1e-6)
+    assert op._fastc is not None and tr.equal(op(x), fx)     # bound: the CPython fast path
