@@ -656,6 +656,21 @@ __device__ __forceinline__ uint32_t window_chunk(const RawChunk<L, LOCAL>& r, in
     return hmask;
 }
 
+// Workgroup -> block of the CSR (ray-major: neighbouring blocks gather neighbouring voxels).
+// Workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8 share an L2).  `chunk` > 0 deals
+// runs of `chunk` consecutive blocks to each XCD instead (chunk > n/8: one contiguous range per
+// XCD), so blocks that gather the same lines share an L2; 0 keeps dispatch order.  Bijective for
+// any grid size.  Chosen per launch by fwd_chunk().
+__device__ __forceinline__ int64_t block_of(int chunk) {
+    const uint32_t n = gridDim.x, b = blockIdx.x;
+    if (chunk <= 0) return (int64_t)b;
+    const uint32_t q = n / 8, r = n % 8, x = b % 8, i = b / 8, k = (uint32_t)chunk;
+    if (k > q) return (int64_t)((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i);
+    // chunks of k blocks dealt round-robin over the XCDs; the ragged tail keeps dispatch order
+    if (b >= n / (8 * k) * (8 * k)) return (int64_t)b;
+    return (int64_t)(((i / k) * 8 + x) * k + i % k);
+}
+
 // ---- forward ------------------------------------------------------------------------------
 // Channels: static multichannel -> every ray for every channel c < n_chan; ray_chan_div > 0 ->
 // ray i reads channel i / div (a time slice per view) and writes out[i].
@@ -684,7 +699,7 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
     const int32_t* __restrict__ row_ray, const int32_t* __restrict__ empty_ray,
     const T* __restrict__ density, int64_t n_chan, int64_t cs, int64_t div, T* __restrict__ out,
     int64_t ocs, int64_t n_rays, int64_t n_seg, int64_t n_cols, int64_t tab_stride,
-    int fallback_only) {
+    int xcd_chunk, int fallback_only) {
     __shared__ FwdShared sh;
     extern __shared__ __attribute__((aligned(16))) unsigned char fwd_dyn_lds[];
     T* dens = reinterpret_cast<T*>(fwd_dyn_lds);   // 4 * tab_stride entries (table mode)
@@ -697,14 +712,15 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
     // Everything addressed by the workgroup index alone goes out before the block record
     // arrives: the first pass (rows of block b start in [b*kSegPerBlock, (b+1)*kSegPerBlock),
     // so its first pass is [b*kSegPerBlock, +kPass)) and the granule table (fixed stride).
+    const int64_t blk = block_of(xcd_chunk);
     FWD_STAMP(0);
-    const int64_t base0 = (int64_t)blockIdx.x * kSegPerBlock;
+    const int64_t base0 = blk * kSegPerBlock;
     const int64_t last_chunk = imax64((n_seg + kPer - 1) / kPer, 1) - 1;   // clamp for loads
     RawChunk<L, local> raw;
     raw_load<L, local>(vox, loc, len, imin64(base0 + o, last_chunk * kPer), raw);
     // table chunks beyond the stride read the next workgroup's entries (tab is padded by
     // kGranEarly*kThreads entries); they are never staged (j >= n_tab)
-    const TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
+    const TabT* tab_b = tab + blk * tab_stride;
     int32_t ti[kEarlyRounds<T>];
     if (local) {
         const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -713,7 +729,7 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             ti[r] = (int32_t)tab_b[gran_entry0<T>(r, w) + (tid & 63) / kGranLanes<T>];
     }
     __builtin_amdgcn_sched_barrier(0);
-    const int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
+    const int64_t* m = blocks + kBlockFields * blk;
     const int64_t s0 = m[2], k0 = m[4], n_tab = m[5];
     int64_t s1 = m[3];
     if (MODE == kFwdTable && n_tab < 0) s1 = s0;      // left to the kFwdGather fallback launch
@@ -1158,14 +1174,28 @@ static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int
     return true;
 }
 
+// Workgroup order of a forward launch (block_of).  Measured on MI355X (profiles/r01_apply_kernels):
+// when the gathered array (density columns, or the image for a transposed CSR) outgrows one XCD's
+// 4 MB L2, runs of 64 blocks per XCD keep its lines L2-resident (C3 forward f32 350 -> 268 us, f64
+// 596 -> 366 us; adjoint f64 377 -> 331 us); when the whole grid is resident at once (one wave of
+// <= 6 blocks per CU), one contiguous range per XCD cuts the first-touch misses (C2 forward f32
+// 7.0 -> 6.7 us); otherwise (the array fits every L2, several waves) dispatch order is as fast or
+// faster (C5 f64 64 vs 68 us with runs of 64).
+static int fwd_chunk(const sphrt_csr* c, size_t elem) {
+    if (c->n_cols * (int64_t)elem > (int64_t)(4 << 20)) return 64;
+    if (c->n_blocks <= 256 * 6) return INT32_MAX;
+    return 0;
+}
+
 template <typename T, typename L>
 static int launch_forward(const sphrt_csr* c, const L* len, const T* density, int64_t n_chan,
                           int64_t chan_stride, int64_t div, T* out, int64_t ocs, void* stream) {
     const dim3 grid((unsigned)c->n_blocks), block(kThreads);
     hipStream_t st = (hipStream_t)stream;
+    const int chunk = fwd_chunk(c, sizeof(T));
 #define SPHRT_FWD_ARGS(TabT) c->blocks, c->vox, c->loc, (const TabT*)c->tab, len, c->row_ray,  \
                        c->empty_ray, density, n_chan, chan_stride, div, out, ocs, c->n_rays,    \
-                       c->n_segments, c->n_cols, c->tab_stride
+                       c->n_segments, c->n_cols, c->tab_stride, chunk
     if (div > 0) {
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic>), grid, block, 0, st,
                            SPHRT_FWD_ARGS(int32_t), 0);

@@ -32,7 +32,7 @@ if [[ $STEPS == *prof* ]]; then
   for f in $(find $OUT/prof -name "*kernel_stats.csv"); do head -6 "$f"; done
 fi
 if [[ $STEPS == *configs* ]]; then
-  for c in c3 c5; do
+  for c in c3 c4 c5; do
     timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 --cpu-sample-views 1 --cpu-reps 3 > $OUT/bench_$c.json 2> $OUT/bench_$c.err
     cut -c1-200 $OUT/bench_$c.json
   done
