@@ -386,3 +386,43 @@ def test_dynamic_pairing_forward_and_adjoint(gpu):
     f32 = op(x.float())
     assert tr.allclose(f32.double(), fx, rtol=1e-5, atol=1e-6)
     assert op._fastc is not None and tr.equal(op(x), fx)     # bound: the CPython fast path
+
+
+@pytest.mark.parametrize('grid_shape,n_views,det,order', [
+    ((128, 128, 128), 6, (128, 128), 'runs'),     # density > 4 MB: runs of 64 blocks per XCD
+    ((50, 50, 50), 80, (50, 100), 'dispatch'),    # > 1536 blocks, small density
+    ((50, 50, 50), 10, (50, 100), 'range'),       # <= 1536 blocks: one range per XCD
+])
+def test_workgroup_orders_cover_every_block(grid_shape, n_views, det, order, gpu):
+    """The forward's workgroup -> block maps (apply.hip block_of / fwd_chunk) are bijections:
+    op(x) and op.T(y) equal a torch index_add over the CSR's own segments for each launch order
+    (float64 within 1e-12, float32 within 1e-5 of it)."""
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(n_views, det, grid_shape=grid_shape)
+    op = Operator(grid, geom, device=gpu)
+    csr = op._csr
+    n, nvox = csr['n'], math.prod(grid_shape)
+    total = csr['total']
+    ptr = csr['row_ptr']
+    ray = tr.repeat_interleave(tr.arange(n, device=gpu), ptr[1:] - ptr[:-1])
+    vox = (csr['vox'][:total] & 0x7fffffff).long()
+    ln = csr['len'][:total]
+    nblocks = csr['nblocks']
+    assert ray.numel() == total
+    if order == 'runs':      # with a ragged tail (blocks past the last whole 8 x 64 keep order)
+        assert nblocks > 512 and nblocks % 512 != 0, nblocks
+    elif order == 'dispatch':
+        assert nblocks > 1536, nblocks
+    else:
+        assert 8 < nblocks <= 1536 and nblocks % 8 != 0, nblocks
+    g = tr.Generator(device=gpu).manual_seed(7)
+    x = tr.rand(grid_shape, dtype=tr.float64, device=gpu, generator=g)
+    y = tr.rand(geom.shape, dtype=tr.float64, device=gpu, generator=g)
+    ref = tr.zeros(n, dtype=tr.float64, device=gpu).index_add_(0, ray, x.reshape(-1)[vox] * ln)
+    got = op(x).reshape(-1)
+    assert float((got - ref).abs().max()) <= 1e-12 * float(ref.abs().max())
+    got32 = op(x.float()).reshape(-1).double()
+    assert float((got32 - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+    reft = tr.zeros(nvox, dtype=tr.float64, device=gpu).index_add_(0, vox, y.reshape(-1)[ray] * ln)
+    gott = op.T(y).reshape(-1)
+    assert float((gott - reft).abs().max()) <= 1e-12 * float(reft.abs().max())
