@@ -6,6 +6,14 @@ by ``gd()`` as ``loss(f, y, density, coeffs)``; the fidelity losses call the Ope
 import torch as t
 
 
+def _scaled(m, x):
+    """m * x, skipping the multiply (one kernel, and one more in the backward) when m is the
+    scalar 1: x * 1 == x exactly."""
+    if isinstance(m, (int, float)) and not isinstance(m, bool) and m == 1:
+        return x
+    return m * x
+
+
 class Loss:
     """Base loss: ``compute(f, y, d, c)`` times weight ``lam``.
 
@@ -30,7 +38,7 @@ class Loss:
         else:
             with t.no_grad():
                 val = self.compute(f, y, d, c)
-        return None if val is None else self.lam * val
+        return None if val is None else _scaled(self.lam, val)
 
     def __mul__(self, other):
         self.lam = other
@@ -47,7 +55,7 @@ class SquareLoss(Loss):
     kind = 'fidelity'
 
     def compute(self, f, y, d, c):
-        return t.mean(self.projection_mask * (y - f(d * self.volume_mask)) ** 2)
+        return t.mean(_scaled(self.projection_mask, (y - f(_scaled(self.volume_mask, d))) ** 2))
 
 
 class SquareRelLoss(Loss):
@@ -55,11 +63,11 @@ class SquareRelLoss(Loss):
     kind = 'fidelity'
 
     def compute(self, f, y, d, c):
-        pred = f(d * self.volume_mask)
+        pred = f(_scaled(self.volume_mask, d))
         nz = y != 0
         rel = t.zeros_like(y)
         rel[nz] = (y - pred)[nz] / y[nz]
-        return t.mean((self.projection_mask * rel) ** 2)
+        return t.mean(_scaled(self.projection_mask, rel) ** 2)
 
 
 class AbsLoss(Loss):
@@ -67,7 +75,7 @@ class AbsLoss(Loss):
     kind = 'fidelity'
 
     def compute(self, f, y, d, c):
-        return t.mean(self.projection_mask * (y - f(d * self.volume_mask)).abs())
+        return t.mean(_scaled(self.projection_mask, (y - f(_scaled(self.volume_mask, d))).abs()))
 
 
 class CheaterLoss(Loss):
@@ -79,18 +87,18 @@ class CheaterLoss(Loss):
         super().__init__(**kwargs)
 
     def compute(self, f, y, d, c):
-        return t.mean(self.volume_mask * (d - self.density_truth) ** 2)
+        return t.mean(_scaled(self.volume_mask, (d - self.density_truth) ** 2))
 
 
 class NegRegularizer(Loss):
     """Mean magnitude of negative voxels."""
 
     def compute(self, f, y, d, c):
-        return t.mean(t.abs(self.volume_mask * d.clip(max=0)))
+        return t.mean(t.abs(_scaled(self.volume_mask, d.clip(max=0))))
 
 
 class NegSumRegularizer(Loss):
     """Summed magnitude of negative voxels."""
 
     def compute(self, f, y, d, c):
-        return t.sum(t.abs(self.volume_mask * d.clip(max=0)))
+        return t.sum(t.abs(_scaled(self.volume_mask, d.clip(max=0))))
