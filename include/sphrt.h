@@ -159,6 +159,17 @@ typedef struct sphrt_csr {
     const int32_t *empty_ray;  /* the rays without segments, ascending (n_rays - rows entries) */
     int64_t tab_stride;    /* granule-table entries per block (>= the largest n_tab) */
     int64_t tab_bytes;     /* 2: uint16 table entries (n_cols <= 2^18), else int32 */
+    /* Brick staging for the granule-table forward (all zero: off).  The columns are the voxels of
+     * an (Nr, Ne, Na) = stage_shape grid; the granule tables and loc address a copy of the
+     * density re-laid in bricks of stage_brick = (br, be, ba) voxels (each dim padded up to a
+     * multiple of its brick), so one 128-byte line holds a compact 3-D neighbourhood instead of a
+     * run along a.  Every table-mode forward first packs the density into `stage` (stage_bytes,
+     * >= n_chan * stage_cols * sizeof(T), else the call fails).  vox stays in natural order. */
+    int32_t stage_shape[3];
+    int32_t stage_brick[3];
+    int64_t stage_cols;    /* prod over dims of ceil(shape / brick) * brick */
+    void *stage;
+    int64_t stage_bytes;
 } sphrt_csr;
 
 int64_t sphrt_csr_blocks(int64_t n_segments);

@@ -39,7 +39,9 @@ class CSR(ctypes.Structure):
                 ('len', c_vp), ('len32', c_vp), ('row_ray', c_vp), ('blocks', c_vp),
                 ('n_blocks', c_i64), ('loc', c_vp), ('tab', c_vp), ('n_cols', c_i64),
                 ('n_fallback', c_i64), ('empty_ray', c_vp), ('tab_stride', c_i64),
-                ('tab_bytes', c_i64)]
+                ('tab_bytes', c_i64), ('stage_shape', ctypes.c_int32 * 3),
+                ('stage_brick', ctypes.c_int32 * 3), ('stage_cols', c_i64), ('stage', c_vp),
+                ('stage_bytes', c_i64)]
 
 
 ROW_HEAD = 0x80000000

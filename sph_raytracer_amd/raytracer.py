@@ -17,6 +17,7 @@ Differences from the reference, by design:
 """
 import ctypes
 import math
+import os
 
 import torch as tr
 
@@ -285,7 +286,8 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
     loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
     # 16-bit entries when every granule index fits (<= 2^18 columns): half the table bytes the
     # forward streams
-    desc.tab_bytes = 2 if (desc.n_cols + 3) // 4 <= 65536 else 4
+    cols = desc.stage_cols if desc.stage_shape[0] > 0 else desc.n_cols
+    desc.tab_bytes = 2 if (cols + 3) // 4 <= 65536 else 4
     tab = tr.empty(nblocks * stride + 3 * 256, dtype=tr.int16 if desc.tab_bytes == 2 else tr.int32,
                    device=dev)   # + early-fetch pad
     _lib.check(lib.sphrt_csr_local_fill(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(tab),
@@ -293,6 +295,44 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
     desc.n_fallback, desc.tab_stride = n_fallback, stride
     desc.loc, desc.tab = loc.data_ptr(), tab.data_ptr()
     return loc, tab
+
+
+_BRICK = (2, 4, 4)   # (r, e, a) voxels per staging brick: 32 = one 128-byte float line
+
+
+def _stage_brick(nblocks):
+    """Brick of the density staging for a trace CSR of `nblocks` workgroup blocks (sphrt.h
+    stage_*), or None.  It pays when the forward runs in several waves of workgroups, whose
+    granule DMA is bound by L2 requests (C3 f32 -17 %, C5 f32 -34 %, f64 -16 %); a grid that is
+    resident at once (C2: 1473 blocks) is latency-bound and would only pay the packing pass.
+    SPHRT_BRICK=off disables it, SPHRT_BRICK=br,be,ba forces a brick."""
+    env = os.environ.get('SPHRT_BRICK', 'auto')
+    if env == 'off':
+        return None
+    if env != 'auto':
+        return tuple(int(v) for v in env.split(','))
+    return _BRICK if nblocks > 256 * 6 else None
+
+
+def _set_stage(desc, shape, brick, dev):
+    """Fill the CSR's stage_* fields for `brick` (None: off) and allocate the float64-sized
+    single-channel stage buffer (grown on demand for more channels, _ensure_stage)."""
+    _clear_stage(desc)
+    if brick is None:
+        return None
+    cols = math.prod(-(-s // b) * b for s, b in zip(shape, brick))
+    for i in range(3):
+        desc.stage_shape[i], desc.stage_brick[i] = shape[i], brick[i]
+    desc.stage_cols = cols
+    stage = tr.zeros(cols, dtype=tr.float64, device=dev)
+    desc.stage, desc.stage_bytes = stage.data_ptr(), cols * 8
+    return stage
+
+
+def _clear_stage(desc):
+    for i in range(3):
+        desc.stage_shape[i] = desc.stage_brick[i] = 0
+    desc.stage_cols, desc.stage, desc.stage_bytes = 0, None, 0
 
 
 def _workspace(lib, plan, n, dev):
@@ -417,10 +457,12 @@ class Operator:
         c.row_ray, c.blocks, c.len32 = row_ray.data_ptr(), blocks.data_ptr(), None
         c.empty_ray = empty_ray.data_ptr()
         c.n_cols = math.prod(self.grid.shape[-3:])
+        shape3 = tuple(int(v) for v in self.grid.shape[-3:])
+        stage = _set_stage(c, shape3, _stage_brick(nblocks), dev)
         loc, tab = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
         self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, row_ray=row_ray,
                          empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, nblocks=nblocks,
-                         n=n, total=total, desc=c)
+                         n=n, total=total, desc=c, stage=stage)
         self._batch = batch
 
     # -- shape logic of raytracer.py:703-712 -----------------------------------------------------
@@ -484,11 +526,18 @@ class Operator:
 
     def _launch_forward(self, d, out, n_chan, div):
         """Enqueue the forward kernel on the current stream: d (contiguous, compute device,
-        float32/float64) -> out (preallocated, same dtype).  No allocation, no host sync."""
+        float32/float64) -> out (preallocated, same dtype).  No host sync; allocates only to grow
+        the brick stage on a first call with more channels."""
         csr = self._csr
         lib = _lib.load()
         self._lengths(d.dtype)
         desc, n_chan, cs, div = self._launch_args(d, n_chan, div)
+        if desc.stage_shape[0] > 0 and n_chan * desc.stage_cols * d.element_size() > desc.stage_bytes:
+            # more channels than the stage holds (first multichannel call): grow it
+            st = tr.zeros(-(-n_chan * desc.stage_cols * d.element_size() // 8), dtype=tr.float64,
+                          device=self._cdev)
+            csr['stage'] = st
+            desc.stage, desc.stage_bytes = st.data_ptr(), st.numel() * 8
         fn = lib.sphrt_forward_f32 if d.dtype == tr.float32 else lib.sphrt_forward_f64
         _lib.check(fn(desc, _lib.ptr(d), n_chan, cs, div, _lib.ptr(out), csr['n'],
                       _lib.stream_of(self._cdev)), 'sphrt_forward')
@@ -500,8 +549,9 @@ class Operator:
         n_chan, div, _ = self._layout(d.shape)
         c, n_chan, _, div = self._launch_args(d, n_chan, div)
         es = d.element_size()
+        aligned = d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0)
         table = (c.loc and div == 0 and 0 < c.tab_stride and (c.tab_stride + 1) * 4 * es <= 64 * 1024
-                 and d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0))
+                 and (c.stage_shape[0] > 0 or aligned))
         if table:
             return f'forward_kernel<{t}, 0, {"unsigned short" if c.tab_bytes == 2 else "int"}>'
         return f'forward_kernel<{t}, {2 if div else 1}, int>'
@@ -604,6 +654,7 @@ class Operator:
                    'sphrt_csr_time_columns')
         blocks_p = csr['blocks'].clone()            # n_tab (field 5) is per table set
         c = _lib.CSR.from_buffer_copy(csr['desc'])
+        _clear_stage(c)                             # time-paired columns are not bricked
         c.vox, c.blocks, c.n_cols = vox_p.data_ptr(), blocks_p.data_ptr(), T * vol
         c.loc, c.tab, c.tab_stride, c.n_fallback = None, None, 0, 0
         loc, tab = _local_tables(lib, c, blocks_p, nblocks, total, dev, stream)

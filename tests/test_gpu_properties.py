@@ -117,6 +117,35 @@ def test_granule_tables_radix_build(gpu):
     _check_granule_tables(grid, geom, Operator(grid, geom, device=gpu), gpu, tab_bytes=4)
 
 
+def _stage_col(v, shape, brick):
+    """Natural voxel -> brick-staged column (apply.hip stage_col), numpy."""
+    (nr, ne, na), (br, be, ba) = shape, brick
+    r, e, a = v // (ne * na), (v // na) % ne, v % na
+    nbe, nba = -(-ne // be), -(-na // ba)
+    blk = ((r // br) * nbe + e // be) * nba + a // ba
+    return blk * (br * be * ba) + ((r % br) * be + e % be) * ba + a % ba
+
+
+def test_brick_staged_tables(gpu, monkeypatch):
+    """Brick staging forced on a grid no brick divides (padded staging, 3 channels growing the
+    stage): tables and loc address the staged columns, and the staged table forward equals the
+    per-segment gather forward bitwise (_check_granule_tables), for two bricks."""
+    from sph_raytracer_amd import Operator
+    for brick in ('2,4,4', '4,4,2'):
+        monkeypatch.setenv('SPHRT_BRICK', brick)
+        grid, geom = _orbit(4, (24, 30), grid_shape=(30, 21, 26))
+        op = Operator(grid, geom, device=gpu)
+        d = op._csr['desc']
+        assert tuple(d.stage_brick) == tuple(int(b) for b in brick.split(','))
+        assert d.stage_cols == math.prod(-(-s // b) * b for s, b in zip((30, 21, 26), d.stage_brick))
+        _check_granule_tables(grid, geom, op, gpu, tab_bytes=2)
+        x = tr.rand((3,) + tuple(grid.shape), dtype=tr.float64, device=gpu)
+        out = op(x)
+        assert op._csr['desc'].stage_bytes >= 3 * d.stage_cols * 8
+        for i in range(3):
+            assert tr.equal(out[i], op(x[i]))
+
+
 def _check_granule_tables(grid, geom, op, gpu, tab_bytes):
     from sph_raytracer_amd import _lib
     csr = op._csr
@@ -134,6 +163,9 @@ def _check_granule_tables(grid, geom, op, gpu, tab_bytes):
     slot = off // 4 - 4
     assert (slot // 4 < n_tab[owner]).all()
     v = (vox & 0x7fffffff).astype(np.int64)
+    d = csr['desc']
+    if d.stage_shape[0] > 0:                 # brick staging: tables address the staged columns
+        v = _stage_col(v, tuple(d.stage_shape), tuple(d.stage_brick))
     stride = csr['desc'].tab_stride
     assert stride >= n_tab.max() and stride % 64 == 0
     assert np.array_equal(tab[owner * stride + slot // 4], v >> 2)
@@ -411,8 +443,8 @@ def test_workgroup_orders_cover_every_block(grid_shape, n_views, det, order, gpu
     assert ray.numel() == total
     if order == 'runs':      # with a ragged tail (blocks past the last whole 8 x 64 keep order)
         assert nblocks > 512 and nblocks % 512 != 0, nblocks
-    elif order == 'dispatch':
-        assert nblocks > 1536, nblocks
+    elif order == 'dispatch':                # (and brick staging, automatic above 1536 blocks)
+        assert nblocks > 1536 and csr['desc'].stage_shape[0] > 0, nblocks
     else:
         assert 8 < nblocks <= 1536 and nblocks % 8 != 0, nblocks
     g = tr.Generator(device=gpu).manual_seed(7)

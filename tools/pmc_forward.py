@@ -70,11 +70,14 @@ def main():
     ap.add_argument('--kernel', default=None,
                     help='kernel name substring (default: the instantiation the f32 forward runs)')
     ap.add_argument('--workdir', default=os.path.join(ROOT, 'gpurun_out', 'pmc'))
+    ap.add_argument('--extra', action='append', default=[],
+                    help='one more counter group (space-separated names) per use')
     args = ap.parse_args()
     if args.kernel is None:
         args.kernel = kernel_name(args.config)
     per_launch, dispatches, raw = {}, {}, []
-    for counters in PASSES:
+    passes = PASSES + [e.split() for e in args.extra]
+    for counters in passes:
         v, n, files = run_pass(counters, args.workdir, args.config, args.reps, args.kernel)
         per_launch.update(v)
         dispatches.update(n)
@@ -86,7 +89,7 @@ def main():
                       'gfx950 -> doubled; WRITE_SIZE exact; KB = 1024 B; one counter group per pass',
         'traffic_bytes_per_launch': (2 * per_launch['FETCH_SIZE'] + per_launch['WRITE_SIZE']) * 1024,
         'commands': [f'rocprofv3 --pmc {" ".join(c)} -d ... -- python tools/prof_forward.py --only '
-                     f'--reps {args.reps} --config {args.config}' for c in PASSES],
+                     f'--reps {args.reps} --config {args.config}' for c in passes],
     }
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with open(args.out, 'w') as f:
