@@ -322,7 +322,7 @@ __device__ __forceinline__ uint16_t loc_code(int rank, uint32_t v, bool head) {
 // inside one 128-byte line, so a workgroup's granules spread over as many lines as granules.
 // Staged, the columns are bricks of br x be x ba voxels (32 = one float line): the same granules
 // fall into 1.7x (C3) to 2.8x (C5) fewer lines, and the granule DMA's L2 requests drop with them
-// (C3 f32 forward 267 -> 221 us, C5 41 -> 30 us; tools/exp study).  Natural voxel v -> column:
+// (C3 f32 forward 267 -> 241 us, C5 41.9 -> 35.2 us with the pack; tools/brick_study.py).  Natural voxel v -> column:
 struct StageMap {
     uint32_t on, ne, na, br, be, ba, nbe, nba;
 };
