@@ -300,18 +300,26 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
 _BRICK = (2, 4, 4)   # (r, e, a) voxels per staging brick: 32 = one 128-byte float line
 
 
-def _stage_brick(nblocks):
+# Transposed CSRs (columns = rays) are not staged by default: detector tiles of (1, 4, 8) rays
+# measured C5 adjoint f32 40.5 -> 34.5 us but f64 59.6 -> 61.5 and C3 f32 229 -> 261, f64 327 ->
+# 354 us.  SPHRT_BRICK_T=b0,b1,b2 stages them (view, row, column).
+_BRICK_RAYS = None
+
+
+def _stage_brick(nblocks, env_name='SPHRT_BRICK', brick=_BRICK):
     """Brick of the density staging for a trace CSR of `nblocks` workgroup blocks (sphrt.h
     stage_*), or None.  It pays when the forward runs in several waves of workgroups, whose
-    granule DMA is bound by L2 requests (C3 f32 -17 %, C5 f32 -34 %, f64 -16 %); a grid that is
-    resident at once (C2: 1473 blocks) is latency-bound and would only pay the packing pass.
-    SPHRT_BRICK=off disables it, SPHRT_BRICK=br,be,ba forces a brick."""
-    env = os.environ.get('SPHRT_BRICK', 'auto')
+    granule DMA is bound by L2 requests (C3 f32 forward 267 -> 241 us, C5 41.9 -> 35.2 us, pack
+    included); a grid that is resident at once (C2: 1473 blocks) is latency-bound and would only
+    pay the packing pass.  The environment variable `env_name` (SPHRT_BRICK for the trace CSR,
+    SPHRT_BRICK_T for the transposed one, whose columns are rays) set to `off` disables it, to
+    `b0,b1,b2` forces that brick."""
+    env = os.environ.get(env_name, 'auto')
     if env == 'off':
         return None
     if env != 'auto':
         return tuple(int(v) for v in env.split(','))
-    return _BRICK if nblocks > 256 * 6 else None
+    return brick if brick is not None and nblocks > 256 * 6 else None
 
 
 def _set_stage(desc, shape, brick, dev):
@@ -596,8 +604,18 @@ class Operator:
             csr['T'] = self._transpose_of(csr['desc'], math.prod(self.grid.shape[-3:]))
         return csr['T']
 
+    def _ray_shape3(self):
+        """The rays' layout as 3 dims (views, rows, columns of the detector) for brick staging of
+        a transposed CSR, whose columns are rays."""
+        shape = [int(v) for v in self.geom.shape]
+        if math.prod(shape) != self._csr['n']:
+            return None
+        shape = [1] * max(0, 3 - len(shape)) + shape
+        return (math.prod(shape[:-2]), shape[-2], shape[-1])
+
     def _transpose_of(self, src, n_cols):
-        """Transpose of the CSR `src` (columns < n_cols) with its own index and granule tables."""
+        """Transpose of the CSR `src` (columns < n_cols) with its own index and granule tables;
+        its columns (rays) are brick-staged in detector tiles for multi-wave grids."""
         csr = self._csr
         lib, dev = _lib.load(), self._cdev
         stream = _lib.stream_of(dev)
@@ -629,9 +647,12 @@ class Operator:
         c.row_ray, c.blocks = vox_list.data_ptr(), blocks.data_ptr()
         c.empty_ray = empty_vox.data_ptr()
         c.n_cols = csr['n']
+        shape3 = self._ray_shape3()
+        stage = _set_stage(c, shape3, _stage_brick(nblocks, 'SPHRT_BRICK_T', _BRICK_RAYS)
+                           if shape3 else None, dev)
         loc, tab = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
         return dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, empty_vox, blocks,
-                                  loc, tab))
+                                  loc, tab, stage))
 
     def _paired(self, T, div):
         """The trace with time-paired columns (ray r reads slice r // div: column

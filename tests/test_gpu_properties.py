@@ -133,12 +133,15 @@ def test_brick_staged_tables(gpu, monkeypatch):
     from sph_raytracer_amd import Operator
     for brick in ('2,4,4', '4,4,2'):
         monkeypatch.setenv('SPHRT_BRICK', brick)
+        monkeypatch.setenv('SPHRT_BRICK_T', '1,2,8')     # transposed: rays, 30 columns padded
         grid, geom = _orbit(4, (24, 30), grid_shape=(30, 21, 26))
         op = Operator(grid, geom, device=gpu)
         d = op._csr['desc']
         assert tuple(d.stage_brick) == tuple(int(b) for b in brick.split(','))
         assert d.stage_cols == math.prod(-(-s // b) * b for s, b in zip((30, 21, 26), d.stage_brick))
         _check_granule_tables(grid, geom, op, gpu, tab_bytes=2)
+        t = op._transposed()['desc']
+        assert tuple(t.stage_brick) == (1, 2, 8) and tuple(t.stage_shape) == (4, 24, 30)
         x = tr.rand((3,) + tuple(grid.shape), dtype=tr.float64, device=gpu)
         out = op(x)
         assert op._csr['desc'].stage_bytes >= 3 * d.stage_cols * 8
