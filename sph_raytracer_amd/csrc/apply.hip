@@ -364,24 +364,36 @@ static bool stage_map(const sphrt_csr* c, StageMap& m) {
 static int64_t table_cols(const sphrt_csr* c) { return staged(c) ? c->stage_cols : c->n_cols; }
 
 // dst[c * stage_cols + p] = src[c * cs + v] for the voxel v staged at column p (0 on pad
-// columns): one thread per staged column, so the writes are contiguous and the reads gather 4-16 B
-// runs that neighbouring bricks share in L2.
+// columns).  One thread per brick row: ba voxels contiguous in both layouts (one 16-byte float
+// vector when ba = 4 and the rows are 16-byte aligned), 4 integer divisions per row.
 template <typename T>
 __global__ __launch_bounds__(256) void stage_pack_kernel(const T* __restrict__ src, int64_t cs,
                                                          int64_t n_chan, uint32_t nr, StageMap m,
                                                          int64_t stage_cols, T* __restrict__ dst) {
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= stage_cols) return;
-    const uint32_t bv = m.br * m.be * m.ba;
-    const uint32_t blk = (uint32_t)p / bv, in = (uint32_t)p % bv;
-    const uint32_t a = (blk % m.nba) * m.ba + in % m.ba;
-    const uint32_t q = blk / m.nba;
-    const uint32_t e = (q % m.nbe) * m.be + (in / m.ba) % m.be;
-    const uint32_t r = (q / m.nbe) * m.br + in / (m.ba * m.be);
-    const bool real = r < nr && e < m.ne && a < m.na;
-    const int64_t v = ((int64_t)r * m.ne + e) * m.na + a;
-    for (int64_t c = blockIdx.y; c < n_chan; c += gridDim.y)
-        dst[c * stage_cols + p] = real ? src[c * cs + v] : (T)0;
+    const uint32_t rows = m.br * m.be;                        // rows per brick
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= stage_cols / m.ba) return;
+    const uint32_t blk = (uint32_t)t / rows, row = (uint32_t)t % rows;
+    const uint32_t a0 = (blk % m.nba) * m.ba, q = blk / m.nba;
+    const uint32_t e = (q % m.nbe) * m.be + row % m.be;
+    const uint32_t r = (q / m.nbe) * m.br + row / m.be;
+    const int64_t p0 = (int64_t)t * m.ba;
+    const bool real = r < nr && e < m.ne;
+    const int64_t v0 = ((int64_t)r * m.ne + e) * m.na + a0;
+    const bool vec = m.ba == 4 && a0 + 4 <= m.na && (m.na & 3u) == 0 && (cs & 3) == 0 &&
+                     (stage_cols & 3) == 0 && ((uintptr_t)src & 15) == 0;
+    for (int64_t c = blockIdx.y; c < n_chan; c += gridDim.y) {
+        const T* sr = src + c * cs + v0;
+        T* dr = dst + c * stage_cols + p0;
+        if (vec && real) {          // 16 (float) or 32 (double) aligned bytes
+            const float4* s4 = reinterpret_cast<const float4*>(sr);
+            float4* d4 = reinterpret_cast<float4*>(dr);
+            d4[0] = s4[0];
+            if constexpr (sizeof(T) == 8) d4[1] = s4[1];
+        } else {
+            for (uint32_t i = 0; i < m.ba; ++i) dr[i] = real && a0 + i < m.na ? sr[i] : (T)0;
+        }
+    }
 }
 
 // ---- per-workgroup granule table ----------------------------------------------------------
@@ -1281,7 +1293,8 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
         if (sm.on) {   // natural -> brick layout, every channel
             if (!c->stage || (int64_t)sizeof(T) * n_chan * c->stage_cols > c->stage_bytes)
                 return fail("brick stage buffer missing or too small for this call");
-            const dim3 pg((unsigned)((c->stage_cols + 255) / 256), (unsigned)imin64(n_chan, 65535));
+            const int64_t brick_rows = c->stage_cols / c->stage_brick[2];
+            const dim3 pg((unsigned)((brick_rows + 255) / 256), (unsigned)imin64(n_chan, 65535));
             hipLaunchKernelGGL(stage_pack_kernel<T>, pg, dim3(256), 0, st, density, chan_stride,
                                n_chan, (uint32_t)c->stage_shape[0], sm, c->stage_cols, (T*)c->stage);
             if (int e = check_launch("stage_pack_kernel")) return e;
