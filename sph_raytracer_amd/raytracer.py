@@ -329,6 +329,8 @@ def _set_stage(desc, shape, brick, dev):
     if brick is None:
         return None
     cols = math.prod(-(-s // b) * b for s, b in zip(shape, brick))
+    if cols >= 2 ** 31 - 1 or math.prod(brick) % 4:    # 32-bit staged columns, whole granules
+        return None
     for i in range(3):
         desc.stage_shape[i], desc.stage_brick[i] = shape[i], brick[i]
     desc.stage_cols = cols
