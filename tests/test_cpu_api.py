@@ -291,3 +291,27 @@ def test_batched_orbit_spec_matches_per_view():
             assert fast[i].shape == ref.shape and tr.equal(fast[i].contiguous(), ref), (kind, i)
     mixed = ConeRectGeom((7, 9), pos=(3, 0, 1), fov=(30, 30)) + ConeRectGeom((7, 9), pos=(0, 3, 1))
     assert mixed._ray_spec_batched() is None and mixed._ray_spec()[1].shape == (2, 9)
+
+
+def test_brick_stage_fields(monkeypatch):
+    """Host side of brick staging (raytracer._stage_brick/_set_stage, sphrt.h stage_*): the
+    automatic rule (multi-wave grids only), the environment overrides, the padded column count,
+    and the 32-bit / whole-granule guards."""
+    from sph_raytracer_amd import _lib
+    from sph_raytracer_amd import raytracer as rt
+    monkeypatch.delenv('SPHRT_BRICK', raising=False)
+    assert rt._stage_brick(1536) is None and rt._stage_brick(1537) == rt._BRICK
+    assert rt._stage_brick(10 ** 6, 'SPHRT_BRICK_T', rt._BRICK_RAYS) is None
+    monkeypatch.setenv('SPHRT_BRICK', 'off')
+    assert rt._stage_brick(10 ** 6) is None
+    monkeypatch.setenv('SPHRT_BRICK', '4,4,2')
+    assert rt._stage_brick(8) == (4, 4, 2)
+    c = _lib.CSR()
+    stage = rt._set_stage(c, (30, 21, 26), (2, 4, 4), 'cpu')
+    assert tuple(c.stage_shape) == (30, 21, 26) and tuple(c.stage_brick) == (2, 4, 4)
+    assert c.stage_cols == 30 * 24 * 28 and c.stage_bytes == 8 * c.stage_cols
+    assert stage.numel() == c.stage_cols and c.stage == stage.data_ptr()
+    assert rt._set_stage(c, (30, 21, 26), None, 'cpu') is None and c.stage_shape[0] == 0
+    assert rt._set_stage(c, (2048, 1024, 1024), (2, 4, 4), 'cpu') is None   # 2^31 columns
+    assert rt._set_stage(c, (30, 21, 26), (1, 1, 3), 'cpu') is None          # partial granules
+    assert c.stage_cols == 0 and not c.stage
