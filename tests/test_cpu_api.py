@@ -315,3 +315,37 @@ def test_brick_stage_fields(monkeypatch):
     assert rt._set_stage(c, (2048, 1024, 1024), (2, 4, 4), 'cpu') is None   # 2^31 columns
     assert rt._set_stage(c, (30, 21, 26), (1, 1, 3), 'cpu') is None          # partial granules
     assert c.stage_cols == 0 and not c.stage
+
+
+def test_ctypes_structs_match_the_c_header(tmp_path):
+    """The ctypes mirrors in _lib (GridDesc, RayBatch, CSR) have the C ABI layout of
+    include/sphrt.h: every field at the C offset, same struct size (gcc on the header)."""
+    import shutil
+    import subprocess
+    from sph_raytracer_amd import _lib
+    gcc = shutil.which('gcc')
+    if gcc is None:
+        pytest.skip('gcc not available')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pairs = [('sphrt_grid_desc', _lib.GridDesc), ('sphrt_rays', _lib.RayBatch),
+             ('sphrt_csr', _lib.CSR)]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "sphrt.h"', 'int main(void) {']
+    for cname, py in pairs:
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines += ['return 0;', '}']
+    src = tmp_path / 'abi.c'
+    src.write_text('\n'.join(lines))
+    exe = tmp_path / 'abi'
+    subprocess.run([gcc, '-std=c11', '-I', os.path.join(root, 'include'), str(src), '-o', str(exe)],
+                   check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                               text=True).stdout.splitlines():
+        s, f, v = line.split()
+        got[(s, f)] = int(v)
+    for cname, py in pairs:
+        assert got[(cname, 'sizeof')] == ctypes.sizeof(py), cname
+        for f in py._fields_:
+            assert got[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])
