@@ -28,9 +28,6 @@ constexpr int kThreads = 256;
 #ifndef SPHRT_FWD_MINB32
 #define SPHRT_FWD_MINB32 6   // the same for float32
 #endif
-#ifndef SPHRT_FWD_EMIT
-#define SPHRT_FWD_EMIT 2   // row-close emission: 2 selects, 1 rank walk, 0 per-slot window tests
-#endif
 // 64-bit min/max as plain selects (HIP's min<int64_t>/max<int64_t> went through double
 // conversions on VALU even for uniform operands).
 __host__ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
@@ -886,17 +883,12 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             // rows this thread closes: the run open at its start (row hb-1) and its first own row
             // (row hb) are fetched now, under the segmented scan; further ones (rare) at the store
             const int32_t* rows = row_ray + k0 + rbase + hb;
-#if SPHRT_FWD_EMIT
             // unconditional loads (clamped into row_ray's n_rays entries): no branch, so nothing
             // waits for them before the first store
             const int64_t ri = k0 + rbase + hb;
             const int32_t r_prev = row_ray[imax64(ri - 1, 0)];
             const int32_t r_first = row_ray[imin64(ri, n_rays - 1)];
             const int32_t r_second = row_ray[imin64(ri + 1, n_rays - 1)];
-#else
-            const int32_t r_prev = hb > 0 || base != base0 ? rows[-1] : 0;
-            const int32_t r_first = hcount > 0 ? rows[0] : 0;
-#endif
             auto row_of = [&](int i) -> int64_t {     // ray of the row after i own heads
                 return i < 0 ? r_prev : i == 0 ? r_first : rows[i];
             };
@@ -924,7 +916,6 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             A p[kPer];
 #pragma unroll
             for (int k = 0; k < kPer; ++k) p[k] = (A)rv[k] * (A)l[k];
-#if SPHRT_FWD_EMIT == 2
             // Row closes: at every head except the workgroup's first segment, and at position kPer
             // in the thread holding the workgroup's last segment when this pass reaches it (masked
             // slots carry no head and zero length, so no per-slot window test is needed).  With
@@ -946,14 +937,6 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
                 v2 = k == h3 ? tail : v2;
                 if (k < kPer) tail = ((hmask >> k) & 1 ? (A)0 : tail) + p[k];
             }
-#else
-            A tail = (A)0;
-#pragma unroll
-            for (int k = 0; k < kPer; ++k) {
-                if ((hmask >> k) & 1) tail = (A)0;
-                tail += p[k];
-            }
-#endif
             bool tot_has;
             double tot_sum;
             const double ex = block_excl_segsum1(hmask != 0, (double)tail, tot_has, tot_sum,
@@ -963,7 +946,6 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             // the run open at this thread's start: the segmented prefix of the earlier threads,
             // plus the carry of earlier passes when no earlier thread of this pass saw a head
             const double run0 = hb > 0 ? ex : carry + ex;
-#if SPHRT_FWD_EMIT == 2
             uint32_t cmask = hmask;
             {
                 const int first = lo - o, end = hi - o;
@@ -986,57 +968,6 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
                     }
                 }
             }
-#elif SPHRT_FWD_EMIT == 1
-            // Row closes, as a bit mask over chunk positions 0..kPer: every head except the
-            // workgroup's first segment, and position kPer in the thread holding the workgroup's
-            // last segment when this pass reaches it (masked slots carry no head and zero length,
-            // so no per-slot window test is needed).  The close at the first head (or at kPer when
-            // the chunk has none) ends the run open at the chunk start: run0 + its own part, in
-            // double, stored once after the loop; every later close stores the thread-local run.
-            uint32_t cmask = hmask;
-            {
-                const int first = lo - o, end = hi - o;
-                if (base == base0 && first >= 0 && first < kPer) cmask &= ~(1u << first);
-                if (base + kPass >= s1 && end > 0 && end <= kPer) cmask |= 1u << kPer;
-            }
-            const int fo = __builtin_ctz(hmask | (1u << kPer));
-            A q = (A)0, qa = (A)0;
-            int rank = 0;                             // own heads passed
-#pragma unroll
-            for (int k = 0; k <= kPer; ++k) {
-                if (k == fo) {
-                    qa = q;
-                } else if ((cmask >> k) & 1) {        // rank >= 1: rows hb, hb+1 prefetched
-                    const int64_t ray = rank == 1 ? r_first : rank == 2 ? r_second : rows[rank - 1];
-                    oc[ray] = (T)q;
-                }
-                if (k < kPer) {
-                    const bool h = (hmask >> k) & 1;
-                    rank += h;
-                    q = (h ? (A)0 : q) + p[k];
-                }
-            }
-            if ((cmask >> fo) & 1) oc[r_prev] = (T)(run0 + (double)qa);
-#else
-            A lr = (A)0;                              // this thread's part of the current run
-            bool open0 = true;                        // the current run started before this thread
-            int seen = -1;                            // own heads passed so far, minus one
-            const int first = lo - o, end = hi - o;   // chunk-relative window
-            const bool closes = base + kPass >= s1;   // the window end closes the last row
-            auto value = [&]() { return open0 ? (T)(run0 + (double)lr) : (T)lr; };
-#pragma unroll
-            for (int k = 0; k < kPer; ++k) {
-                if (k < first || k >= end) continue;
-                if ((hmask >> k) & 1) {
-                    if (k > first || base != base0) oc[row_of(seen)] = value();   // close a row
-                    lr = (A)0;
-                    open0 = false;
-                    ++seen;
-                }
-                lr += p[k];
-                if (k == end - 1 && closes) oc[row_of(seen)] = value();   // the last row
-            }
-#endif
             carry = tot_has ? tot_sum : carry + tot_sum;
             rbase += pass_heads;
         }
