@@ -34,8 +34,11 @@ __host__ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { retur
 __host__ __device__ __forceinline__ int64_t imax64(int64_t a, int64_t b) { return a > b ? a : b; }
 constexpr int kPer = 8;                         // segments per thread per pass
 constexpr int kPass = kThreads * kPer;          // 2048 segments per pass
-constexpr int64_t kSegPerBlock = 1792;          // row starts per workgroup (leaves room for the
-                                                // last row's overhang inside one pass)
+#ifndef SPHRT_SEG_PER_BLOCK
+#define SPHRT_SEG_PER_BLOCK 1792
+#endif
+constexpr int64_t kSegPerBlock = SPHRT_SEG_PER_BLOCK;   // row starts per workgroup (leaves room
+                                                // for the last row's overhang inside one pass)
 constexpr int kBlockFields = 6;                 // empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab
 constexpr int kLocalMax = 4096;                 // segments per workgroup with a granule table
 constexpr int kMaxGran = 2046;                  // granules per table (sphrt_csr_local): loc's
