@@ -180,7 +180,8 @@ int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_
 /* Granule tables in two passes.  _count sets n_tab in blocks (-1: no table) and writes two
  * device int64 to stats: {blocks without a table, largest n_tab}; the caller copies the first to
  * csr->n_fallback, picks tab_stride >= the second (csr->tab_stride; tab holds n_blocks *
- * tab_stride entries) and runs _fill. */
+ * tab_stride entries) and runs _fill.  Brick staging (stage_* fields) is decided before _count:
+ * both passes and every later forward on the tables use the same stage_* values. */
 int sphrt_csr_local_count(const sphrt_csr *csr, int64_t *blocks, int64_t *stats, void *stream);
 int sphrt_csr_local_fill(const sphrt_csr *csr, const int64_t *blocks, uint16_t *loc, void *tab,
                          int64_t tab_stride, void *stream);
