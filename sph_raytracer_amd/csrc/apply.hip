@@ -486,7 +486,10 @@ __global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
     unsigned long long* stats) {
-    using Sort = hipcub::BlockRadixSort<uint32_t, kThreads, kRadixItems, uint16_t>;
+    // the count pass sorts keys only (its values are dead)
+    using Sort = typename std::conditional<
+        FILL, hipcub::BlockRadixSort<uint32_t, kThreads, kRadixItems, uint16_t>,
+        hipcub::BlockRadixSort<uint32_t, kThreads, kRadixItems>>::type;
     __shared__ typename Sort::TempStorage sort_ts;
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
@@ -516,7 +519,8 @@ __global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
             val[i] = (uint16_t)((p << 3) | ((x >> 31) << 2) | (v & 3u));
         }
     }
-    Sort(sort_ts).Sort(key, val, 0, key_bits);   // blocked: thread t holds sorted [16t, 16t+16)
+    if constexpr (FILL) Sort(sort_ts).Sort(key, val, 0, key_bits);   // blocked: thread t holds
+    else Sort(sort_ts).Sort(key, 0, key_bits);                       // sorted [16t, 16t+16)
     last_key[tid] = key[kRadixItems - 1];
     __syncthreads();
     uint32_t prev = tid > 0 ? last_key[tid - 1] : 0xffffffffu;
