@@ -870,7 +870,9 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
         for (int64_t base = base0; base < s1; base += kPass) {
             int lo, hi;
             window(base, lo, hi);
-            if (base != base0 || c != 0) {
+            // later channels of a one-pass block reuse the decoded first chunk: the segments
+            // are streamed once, only the granules are staged per channel
+            if (base != base0 || (c != 0 && s1 > base0 + kPass)) {
                 RawChunk<L, local> rc;
                 raw_load<L, local>(vox, loc, len, imin64(base + o, last_chunk * kPer), rc);
                 hmask = window_chunk<L, local>(rc, o, lo, hi, v, l);
