@@ -1,3 +1,9 @@
+#!/usr/bin/env python3
+"""Multichannel forward timing: one launch over C = 1 and 8 channels (f32, f64) on the C2 and C5
+workloads, HIP-event graph replay (prof_forward.graph_time_us).
+
+    python tools/multichannel_time.py
+"""
 import os, sys, json
 import torch
 sys.path.insert(0, os.getcwd()); sys.path.insert(0, os.path.join(os.getcwd(), 'tools'))
