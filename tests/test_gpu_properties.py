@@ -322,7 +322,8 @@ def _deferred_count(grid, geom, gpu):
 
 
 @pytest.mark.parametrize('shape,a_full', [((64, 64, 64), False), ((17, 9, 30), False),
-                                          ((12, 20, 7), True), ((40, 3, 100), True)])
+                                          ((12, 20, 7), True), ((40, 3, 100), True),
+                                          ((900, 4, 30), False)])   # K 1844: serial exact kernel
 def test_exact_tie_rays_vs_oracle(shape, a_full, gpu):
     """Rays that hit exact ties (through the origin: every cone and half-plane crossed at one
     distance; starts on the a = 0 half-plane) take the exact path, whose emulated introsort
