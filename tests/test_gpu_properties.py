@@ -147,6 +147,13 @@ def test_brick_staged_tables(gpu, monkeypatch):
         assert op._csr['desc'].stage_bytes >= 3 * d.stage_cols * 8
         for i in range(3):
             assert tr.equal(out[i], op(x[i]))
+        # a density 4 bytes off 16-byte alignment (the pack's scalar path), float32
+        x32 = x[0].float()
+        big = tr.empty(x32.numel() + 1, dtype=tr.float32, device=gpu)
+        off = big[1:].view(grid.shape)
+        off.copy_(x32)
+        assert off.data_ptr() % 16 != 0
+        assert tr.equal(op(off), op(x32))
 
 
 def _check_granule_tables(grid, geom, op, gpu, tab_bytes):
