@@ -265,11 +265,15 @@ def main():
     k_ms, k_method = kernel_time_ms(op, x)
     kname = op._forward_kernel_name(x)
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, 'profiles', f'r01_forward_{args.config}_pmc.json')
-    if os.path.exists(pmc):     # HBM bytes per launch from the committed rocprofv3 --pmc passes
+    # HBM bytes per launch from the newest committed rocprofv3 --pmc passes of this kernel
+    for tag in ('r06', 'r05', 'r04', 'r03', 'r02', 'r01'):
+        pmc = os.path.join(ROOT, 'profiles', f'{tag}_forward_{args.config}_pmc.json')
+        if not os.path.exists(pmc):
+            continue
         rec_pmc = json.load(open(pmc))
         if rec_pmc.get('kernel') == kname and rec_pmc.get('config') == args.config:
             traffic, traffic_src = rec_pmc['traffic_bytes_per_launch'], os.path.relpath(pmc, ROOT)
+            break
     # bytes/ray = s_y + 4 + S*(4 + s_len + s_rho); f32 path s_len = s_rho = 4
     es = x.element_size()
     alg_bytes = n_rays * (es + 4) + total_seg * (4 + es + es)
@@ -301,6 +305,10 @@ def main():
                          'first_in_process includes HIP/torch initialisation)'},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                     'achieved_basis': 'algorithmic bytes (SURVEY 8(d): s_y + 4 + S*(4 + s_len + '
+                                       's_rho) per ray; density gathers counted as HBM)',
+                     'traffic_gbs': traffic / (k_ms * 1e-3) / 1e9 if traffic else None,
+                     'traffic_frac': traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                      'traffic_source': traffic_src, 'kernel': kname,
                      'kernel_ms': k_ms, 'bytes_per_launch': alg_bytes, 'timing': k_method},
     }

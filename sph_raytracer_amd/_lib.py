@@ -139,13 +139,31 @@ def check(status, what):
         raise RuntimeError(f'{what} failed: {msg}')
 
 
-def require_gpu():
-    """The device every kernel runs on.  No GPU -> loud failure (no CPU fallback)."""
+def compute_device(device=None, current=None):
+    """The GPU a call computes on: `device` itself when it names a GPU ('cuda', 'cuda:1',
+    torch.device), else (None, 'cpu': results are returned to the host) the current GPU.
+    `current` stands in for torch.cuda.current_device() (tests)."""
+    if device is not None:
+        d = torch.device(device)
+        if d.type == 'cuda':
+            if d.index is not None:
+                return d
+            device = None
+    idx = torch.cuda.current_device() if current is None else current
+    return torch.device('cuda', idx)
+
+
+def require_gpu(device=None):
+    """The device every kernel of a call runs on (compute_device).  No GPU -> loud failure (no
+    CPU fallback)."""
     if not torch.cuda.is_available():
         raise RuntimeError('sph_raytracer_amd requires a ROCm GPU (MI355X / gfx950); '
                            'torch.cuda.is_available() is False and there is no CPU fallback.')
     load()
-    return torch.device('cuda', torch.cuda.current_device())
+    dev = compute_device(device)
+    if dev.index >= torch.cuda.device_count():
+        raise RuntimeError(f'{dev} does not exist ({torch.cuda.device_count()} GPUs visible)')
+    return dev
 
 
 def stream_of(device):

@@ -53,7 +53,8 @@ def fast_command(out=FAST_OUT):
     return ['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-D__HIP_PLATFORM_AMD__=1',
             '-DUSE_ROCM=1', '-I', os.path.join(tdir, 'include'),
             '-I', os.path.join(tdir, 'include', 'torch', 'csrc', 'api', 'include'),
-            '-I', '/opt/rocm/include', '-I', sysconfig.get_paths()['include'],
+            '-I', '/opt/rocm/include', '-I', os.path.join(ROOT, 'include'),
+            '-I', sysconfig.get_paths()['include'],
             os.path.join(CSRC, 'fastpath.cpp'), '-L', os.path.join(tdir, 'lib'),
             '-ltorch_python', '-ltorch', '-ltorch_cpu', '-lc10', '-lc10_hip',
             f'-Wl,-rpath,{os.path.join(tdir, "lib")}', '-o', out]
@@ -62,7 +63,8 @@ def fast_command(out=FAST_OUT):
 def build_fast(force=False, verbose=False):
     src = os.path.join(CSRC, 'fastpath.cpp')
     if not force and os.path.exists(FAST_OUT) and \
-            os.path.getmtime(FAST_OUT) >= max(os.path.getmtime(src), os.path.getmtime(__file__)):
+            os.path.getmtime(FAST_OUT) >= max(os.path.getmtime(src), os.path.getmtime(__file__),
+                                              os.path.getmtime(os.path.join(ROOT, 'include', 'sphrt.h'))):
         return FAST_OUT
     cmd = fast_command(FAST_OUT + '.tmp')
     if verbose:

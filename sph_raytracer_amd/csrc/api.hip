@@ -24,17 +24,6 @@ int check_launch(const char* what) {
     return 0;
 }
 
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
 
 // ---------------------------------------------------------------------------------------------
 // exclusive scan of int32 counts -> int64 row pointers (3 launches, 1024 counts per block)
@@ -220,6 +209,7 @@ extern "C" size_t sphrt_scan_workspace_bytes(int64_t n) {
 extern "C" int sphrt_scan_counts(const int32_t* counts, int64_t n, int64_t* row_ptr,
                                  void* workspace, void* stream) {
     if (n < 0) return fail("negative length");
+    StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     if (n == 0) {
         if (hipMemsetAsync(row_ptr, 0, sizeof(int64_t), st) != hipSuccess) return fail("memset failed");
@@ -239,6 +229,7 @@ extern "C" int sphrt_scan_counts(const int32_t* counts, int64_t n, int64_t* row_
 
 extern "C" int sphrt_f64_to_f32(const double* src, float* dst, int64_t n, void* stream) {
     if (n == 0) return 0;
+    StreamGuard guard(stream);
     hipLaunchKernelGGL(f64_to_f32_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
                        (hipStream_t)stream, src, dst, n);
     return check_launch("f64_to_f32");

@@ -1056,6 +1056,7 @@ extern "C" int sphrt_csr_time_columns(const sphrt_csr* c, int64_t div, int64_t v
     const int64_t n_t = (c->n_rays + div - 1) / div;
     if (n_t * vol >= (int64_t)kHead) return fail("time-paired columns need T * voxels < 2^31");
     if (c->n_rays == 0) return 0;
+    StreamGuard guard(stream);
     hipLaunchKernelGGL(time_columns_kernel, dim3((unsigned)((c->n_rays + 3) / 4)), dim3(256), 0,
                        (hipStream_t)stream, c->row_ptr, c->n_rays, c->vox, div, vol, vox_out);
     return check_launch("time_columns");
@@ -1078,6 +1079,7 @@ extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* 
                                void* workspace, void* stream) {
     if (n_rays < 0 || n_blocks < 1) return fail("bad CSR index sizes");
     if (n_rays == 0) return 0;
+    StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     unsigned char* ws = (unsigned char*)workspace;
     int32_t* flags = (int32_t*)ws;
@@ -1121,6 +1123,7 @@ extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_
     if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
     StageMap sm;
     if (!stage_map(c, sm)) return fail("inconsistent brick staging fields");
+    StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(stats, 0, 2 * sizeof(int64_t), st) != hipSuccess)
         return fail("hipMemsetAsync failed");
@@ -1150,6 +1153,7 @@ extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, u
     const bool u16 = c->tab_bytes == 2;
     if (u16 && (cols + 3) / 4 > 65536) return fail("16-bit granule tables need <= 2^18 columns");
     if (c->n_segments == 0) return 0;
+    StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     if (const int words = table_bitmap_words(cols)) {
         if (u16)
@@ -1217,6 +1221,7 @@ template <typename T, typename L>
 static int launch_forward(const sphrt_csr* c, const L* len, const T* density, int64_t n_chan,
                           int64_t chan_stride, int64_t div, T* out, int64_t ocs, void* stream) {
     const dim3 grid((unsigned)c->n_blocks), block(kThreads);
+    StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     const int chunk = fwd_chunk(c, sizeof(T));
     StageMap sm;
@@ -1283,6 +1288,7 @@ extern "C" int sphrt_adjoint_accumulate(const sphrt_csr* c, const void* y, int y
     if (int e = check_csr(c, n_chan, div)) return e;
     if (!c->len) return fail("missing segment lengths");
     if (c->n_rays == 0) return 0;
+    StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     if (y_is_f64)
         hipLaunchKernelGGL((adjoint_kernel<double>), dim3((unsigned)c->n_blocks), dim3(kThreads), 0,

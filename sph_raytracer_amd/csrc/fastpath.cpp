@@ -11,12 +11,15 @@
 
 #include <ATen/ATen.h>
 #include <ATen/core/grad_mode.h>
+#include <c10/hip/HIPFunctions.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
 #include <string>
 #include <vector>
+
+#include "sphrt.h"
 
 namespace {
 
@@ -32,6 +35,7 @@ struct Binding {
     const void* csr;
     int64_t n_chan, n_vox, div, n;
     std::vector<int64_t> out_shape;  // the call's result shape (contiguous, n_chan * n or n)
+    int64_t stage_bytes;             // > 0: brick-staged CSR, a stage buffer of this size per call
 };
 
 struct Bindings {
@@ -72,10 +76,11 @@ PyObject* py_new(PyObject*, PyObject* arg) {
     return PyCapsule_New(b, kCapsule, destroy);
 }
 
-// add(capsule, in_sizes, is_f64, device, fn_address, csr_address, n_chan, n_vox, div, n, out_shape)
+// add(capsule, in_sizes, is_f64, device, fn_address, csr_address, n_chan, n_vox, div, n, out_shape,
+//     stage_bytes)
 PyObject* py_add(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-    if (nargs != 11) {
-        PyErr_SetString(PyExc_TypeError, "add() takes 11 arguments");
+    if (nargs != 12) {
+        PyErr_SetString(PyExc_TypeError, "add() takes 12 arguments");
         return nullptr;
     }
     auto* b = static_cast<Bindings*>(PyCapsule_GetPointer(args[0], kCapsule));
@@ -91,6 +96,8 @@ PyObject* py_add(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     x.div = PyLong_AsLongLong(args[8]);
     x.n = PyLong_AsLongLong(args[9]);
     if (PyErr_Occurred() || !int_tuple(args[10], x.out_shape)) return nullptr;
+    x.stage_bytes = PyLong_AsLongLong(args[11]);
+    if (PyErr_Occurred()) return nullptr;
     if (!x.fn || !x.csr) {
         PyErr_SetString(PyExc_ValueError, "null forward entry point or CSR");
         return nullptr;
@@ -119,12 +126,25 @@ PyObject* py_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     if (d.requires_grad() && at::GradMode::is_enabled()) Py_RETURN_NONE;
     const at::ScalarType dt = d.scalar_type();
     const int dev = d.get_device();
+    // launches go to the current HIP device's streams: another current device takes the general
+    // path (which makes the operator's device current)
+    if (dev != (int)c10::hip::current_device()) Py_RETURN_NONE;
     const auto sizes = d.sizes();
     for (const Binding& x : b->list) {
         if (x.dtype != dt || x.device != dev || !sizes.equals(x.in_sizes)) continue;
         at::Tensor out = at::empty(x.out_shape, d.options());
         void* stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
-        const int rc = x.fn(x.csr, d.const_data_ptr(), x.n_chan, x.n_vox, x.div,
+        const void* csr = x.csr;
+        sphrt_csr staged;
+        at::Tensor stage;      // this call's brick stage (caching allocator, current stream)
+        if (x.stage_bytes > 0) {
+            stage = at::empty({x.stage_bytes}, d.options().dtype(at::kByte));
+            staged = *static_cast<const sphrt_csr*>(x.csr);
+            staged.stage = stage.mutable_data_ptr();
+            staged.stage_bytes = x.stage_bytes;
+            csr = &staged;
+        }
+        const int rc = x.fn(csr, d.const_data_ptr(), x.n_chan, x.n_vox, x.div,
                             out.mutable_data_ptr(), x.n, stream);
         if (rc != 0) {
             const std::string msg = std::string("sphrt_forward: ") +

@@ -65,6 +65,7 @@ extern "C" int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ,
     if (!frame || !row || !col || !rays) return fail("null pointer");
     const int64_t n = n_views * h * w;
     if (n == 0) return 0;
+    StreamGuard guard(stream);
     const int64_t blocks = (n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536;
     hipLaunchKernelGGL(cone_rays_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                        n_views, h, w, circ, frame, row, col, rays);

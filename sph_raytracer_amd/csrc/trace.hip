@@ -1081,13 +1081,17 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
 // ---- host launchers ----------------------------------------------------------------------
 static int trace_cap(const GridDev& G) { return ((G.K + 63) / 64) * 64; }
 constexpr int kExactBlocks = 4096;   // one wave per deferred ray, 16 per CU
+// The serial kernel (grids whose list does not fit LDS) keeps each wave's list in the workspace:
+// its grid, and so the workspace, is capped at one wave per CU (deferred rays are rare; the
+// waves stride over them) — 256 * K * 16 B, e.g. 56 MB at K = 13653 instead of 0.9 GB.
+constexpr int kExactSerialBlocks = 256;
 constexpr size_t kWsHead = 256;      // deferred counter, padded
 
 static bool exact_in_lds(const GridDev& G) {
     return exact_wave_lds(G.K) <= kExactWaveLdsMax;
 }
 static size_t exact_scratch_bytes(const GridDev& G) {   // lists of large-K grids, one per wave
-    return exact_in_lds(G) ? 0 : (size_t)kExactBlocks * G.K * sizeof(Cand);
+    return exact_in_lds(G) ? 0 : (size_t)kExactSerialBlocks * G.K * sizeof(Cand);
 }
 static size_t hits_bytes(int64_t n) { return (((size_t)n * sizeof(HitRay) + 255) / 256) * 256; }
 static size_t workspace_bytes(const GridDev& G, int64_t n) {
@@ -1130,7 +1134,7 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
         hipLaunchKernelGGL((exact_wave_kernel<MODE, T>), dim3(kExactBlocks), dim3(64),
                            exact_wave_lds(G.K), st, G, R, o);
     else
-        hipLaunchKernelGGL((exact_kernel<MODE, T>), dim3(kExactBlocks), dim3(64), 0, st, G, R, o,
+        hipLaunchKernelGGL((exact_kernel<MODE, T>), dim3(kExactSerialBlocks), dim3(64), 0, st, G, R, o,
                            scratch);
     return check_launch("exact_kernel");
 }
@@ -1159,7 +1163,8 @@ extern "C" int sphrt_trace_count(const sphrt_plan* plan, const sphrt_rays* rays,
                                  void* workspace, size_t workspace_size, void* stream) {
     GridDev G;
     RaysDev R;
-    if (int e = resolve(plan, rays, G, R)) return e;
+    if (int e = resolve(plan, rays, G, R, stream)) return e;
+    DeviceGuard guard(plan->device);
     TraceOut<double> o{};
     o.counts = counts;
     return launch_trace<MODE_COUNT, double>(G, R, o, workspace, workspace_size,
@@ -1171,7 +1176,8 @@ extern "C" int sphrt_trace_fill(const sphrt_plan* plan, const sphrt_rays* rays,
                                 void* workspace, size_t workspace_size, void* stream) {
     GridDev G;
     RaysDev R;
-    if (int e = resolve(plan, rays, G, R)) return e;
+    if (int e = resolve(plan, rays, G, R, stream)) return e;
+    DeviceGuard guard(plan->device);
     TraceOut<double> o{};
     o.row_ptr = row_ptr;
     o.vox = vox;
@@ -1187,7 +1193,8 @@ static int trace_integrate(const sphrt_plan* plan, const sphrt_rays* rays, const
                            void* stream) {
     GridDev G;
     RaysDev R;
-    if (int e = resolve(plan, rays, G, R)) return e;
+    if (int e = resolve(plan, rays, G, R, stream)) return e;
+    DeviceGuard guard(plan->device);
     if (n_chan < 1) return fail("n_chan must be >= 1");
     if (ray_chan_div > 0 && n_chan != 1) return fail("ray_chan_div requires n_chan == 1");
     TraceOut<T> o{};
@@ -1222,7 +1229,8 @@ extern "C" int sphrt_solve(const sphrt_plan* plan, const sphrt_rays* rays, int f
                            int32_t* region, int8_t* neg, void* stream) {
     GridDev G;
     RaysDev R;
-    if (int e = resolve(plan, rays, G, R)) return e;
+    if (int e = resolve(plan, rays, G, R, stream)) return e;
+    DeviceGuard guard(plan->device);
     if (family < 0 || family > 2) return fail("family must be 0 (r), 1 (e) or 2 (a)");
     if (R.n == 0) return 0;
     const int64_t grid = (R.n + 255) / 256;

@@ -109,6 +109,7 @@ extern "C" int sphrt_csr_transpose(const sphrt_csr* c, int64_t n_vox, int64_t* c
         return fail("transpose supports < 2^31 rays and segments");
     if (workspace_size < sphrt_transpose_workspace_bytes(c->n_segments, n_vox))
         return fail("transpose workspace too small");
+    StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     TWs w;
     layout(c->n_segments, n_vox, (unsigned char*)workspace, &w);

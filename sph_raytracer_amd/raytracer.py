@@ -12,7 +12,8 @@ Differences from the reference, by design:
   ``op.regs`` / ``op.lens`` rebuild a padded compatibility view on demand;
 - crossings at exactly equal distances are ordered as the reference's libstdc++ introsort orders
   them whenever that order can change a voxel (rare rays, replayed by an exact kernel);
-- forward sums accumulate in float64 and round once to the density dtype;
+- float64 forwards accumulate in float64; float32 forwards multiply and sum runs of up to 8
+  segments in float32 and stitch the runs of a row in float64, rounding each row once;
 - the caller's ``geom.rays`` tensor is never normalised in place.
 """
 import ctypes
@@ -200,23 +201,24 @@ class _RayBatch:
 def _solve(family, bounds, xs, rays, ftype, itype, device):
     if ftype != tr.float64:
         raise NotImplementedError('sph_raytracer_amd traces in float64 only')
-    dev = _lib.require_gpu()
-    bounds = tr.asarray(bounds, dtype=tr.float64)
-    unit = tr.tensor([0.0, 1.0], dtype=tr.float64)
-    grid_b = tuple(bounds if i == family else unit for i in range(3))
-    plan = _Plan(None, dev, boundaries=grid_b)
-    batch = _RayBatch(None, xs, rays, dev)
-    nb = len(bounds)
-    width = nb if family == 2 else 2 * nb
-    t = tr.empty(batch.shape + (width,), dtype=tr.float64, device=dev)
-    reg = tr.empty(batch.shape + (width,), dtype=tr.int32, device=dev)
-    neg = tr.empty(batch.shape + (width,), dtype=tr.int8, device=dev)
-    _lib.check(_lib.load().sphrt_solve(plan.handle, batch.desc, family, _lib.ptr(t),
-                                       _lib.ptr(reg), _lib.ptr(neg), _lib.stream_of(dev)),
-               'sphrt_solve')
-    inds = tr.arange(nb, dtype=itype)
-    inds = (inds if family == 2 else tr.cat((inds, inds))).repeat(*batch.shape, 1)
-    return t.to(device), reg.to(itype).to(device), inds.to(device), neg.to(device)
+    dev = _lib.require_gpu(device)
+    with tr.cuda.device(dev):
+        bounds = tr.asarray(bounds, dtype=tr.float64)
+        unit = tr.tensor([0.0, 1.0], dtype=tr.float64)
+        grid_b = tuple(bounds if i == family else unit for i in range(3))
+        plan = _Plan(None, dev, boundaries=grid_b)
+        batch = _RayBatch(None, xs, rays, dev)
+        nb = len(bounds)
+        width = nb if family == 2 else 2 * nb
+        t = tr.empty(batch.shape + (width,), dtype=tr.float64, device=dev)
+        reg = tr.empty(batch.shape + (width,), dtype=tr.int32, device=dev)
+        neg = tr.empty(batch.shape + (width,), dtype=tr.int8, device=dev)
+        _lib.check(_lib.load().sphrt_solve(plan.handle, batch.desc, family, _lib.ptr(t),
+                                           _lib.ptr(reg), _lib.ptr(neg), _lib.stream_of(dev)),
+                   'sphrt_solve')
+        inds = tr.arange(nb, dtype=itype)
+        inds = (inds if family == 2 else tr.cat((inds, inds))).repeat(*batch.shape, 1)
+        return t.to(device), reg.to(itype).to(device), inds.to(device), neg.to(device)
 
 
 def r_torch(r, xs, rays, ftype=FTYPE, itype=ITYPE, device=DEVICE):
@@ -264,9 +266,11 @@ def _layout_for(grid, ray_shape, shape):
 
 try:   # the current HIP stream as an int without building a torch Stream object (~0.3 vs 1.9 us)
     _raw_stream = tr._C._cuda_getCurrentRawStream
+    _cur_dev = tr._C._cuda_getDevice
 except AttributeError:   # pragma: no cover - older torch
     def _raw_stream(index):
         return tr.cuda.current_stream(index).cuda_stream
+    _cur_dev = tr.cuda.current_device
 
 
 def _seg_alloc(total):
@@ -322,21 +326,40 @@ def _stage_brick(nblocks, env_name='SPHRT_BRICK', brick=_BRICK):
     return brick if brick is not None and nblocks > 256 * 6 else None
 
 
-def _set_stage(desc, shape, brick, dev):
-    """Fill the CSR's stage_* fields for `brick` (None: off) and allocate the float64-sized
-    single-channel stage buffer (grown on demand for more channels, _ensure_stage)."""
+def _set_stage(desc, shape, brick):
+    """Fill the CSR's stage_* fields for `brick` (None: off); True when staging is on.  The
+    stage buffer itself is not part of the operator: every forward call gets its own
+    (_call_forward), so calls on different streams never share one."""
     _clear_stage(desc)
     if brick is None:
-        return None
+        return False
     cols = math.prod(-(-s // b) * b for s, b in zip(shape, brick))
     if cols >= 2 ** 31 - 1 or math.prod(brick) % 4:    # 32-bit staged columns, whole granules
-        return None
+        return False
     for i in range(3):
         desc.stage_shape[i], desc.stage_brick[i] = shape[i], brick[i]
     desc.stage_cols = cols
-    stage = tr.zeros(cols, dtype=tr.float64, device=dev)
-    desc.stage, desc.stage_bytes = stage.data_ptr(), cols * 8
-    return stage
+    return True
+
+
+def _stage_bytes(desc, n_chan, elem):
+    """Bytes of the brick stage one forward call on `desc` needs (0: not staged)."""
+    return n_chan * desc.stage_cols * elem if desc.stage_shape[0] > 0 else 0
+
+
+def _call_forward(fn, desc, d, n_chan, cs, div, out, ocs, dev):
+    """sphrt_forward_f32/_f64 on the current stream of `dev`.  A brick-staged CSR gets this
+    call's stage buffer from torch's caching allocator on that stream (released to the same
+    stream afterwards: stream-ordered reuse, never shared with a call on another stream)."""
+    need = _stage_bytes(desc, n_chan, d.element_size())
+    stage = None
+    if need:
+        stage = tr.empty(need, dtype=tr.uint8, device=dev)
+        desc = _lib.CSR.from_buffer_copy(desc)
+        desc.stage, desc.stage_bytes = stage.data_ptr(), need
+    _lib.check(fn(desc, _lib.ptr(d), n_chan, cs, div, _lib.ptr(out), ocs, _lib.stream_of(dev)),
+               'sphrt_forward')
+    del stage
 
 
 def _clear_stage(desc):
@@ -354,22 +377,23 @@ def line_integrals(grid, geom, density):
 
     Same result as ``Operator(grid, geom)(density)`` (not differentiable), without building the
     segment CSR — the memory-capped / cold path (one kernel, O(output) memory)."""
-    dev = _lib.require_gpu()
-    plan = _Plan(grid, dev)
-    batch = _RayBatch(grid, geom.ray_starts, _geom_rays(geom, dev), dev)
     density = tr.as_tensor(density)
-    n_chan, div, out_shape = _layout_for(grid, batch.shape, density.shape)
-    cdt = density.dtype if density.dtype in (tr.float32, tr.float64) else tr.float32
-    d = density.detach().to(device=dev, dtype=cdt).contiguous()
-    n = batch.n
-    out = tr.empty((n_chan, n) if div == 0 else (n,), dtype=cdt, device=dev)
-    lib = _lib.load()
-    ws = _workspace(lib, plan, n, dev)
-    fn = lib.sphrt_trace_integrate_f32 if cdt == tr.float32 else lib.sphrt_trace_integrate_f64
-    _lib.check(fn(plan.handle, batch.desc, _lib.ptr(d), n_chan, math.prod(grid.shape[-3:]), div,
-                  _lib.ptr(out), n, _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)),
-               'sphrt_trace_integrate')
-    return out.reshape(out_shape).to(device=density.device, dtype=density.dtype)
+    dev = _lib.require_gpu(density.device)    # a GPU density computes where it lives
+    with tr.cuda.device(dev):
+        plan = _Plan(grid, dev)
+        batch = _RayBatch(grid, geom.ray_starts, _geom_rays(geom, dev), dev)
+        n_chan, div, out_shape = _layout_for(grid, batch.shape, density.shape)
+        cdt = density.dtype if density.dtype in (tr.float32, tr.float64) else tr.float32
+        d = density.detach().to(device=dev, dtype=cdt).contiguous()
+        n = batch.n
+        out = tr.empty((n_chan, n) if div == 0 else (n,), dtype=cdt, device=dev)
+        lib = _lib.load()
+        ws = _workspace(lib, plan, n, dev)
+        fn = lib.sphrt_trace_integrate_f32 if cdt == tr.float32 else lib.sphrt_trace_integrate_f64
+        _lib.check(fn(plan.handle, batch.desc, _lib.ptr(d), n_chan, math.prod(grid.shape[-3:]),
+                      div, _lib.ptr(out), n, _lib.ptr(ws), ws.numel(), _lib.stream_of(dev)),
+                   'sphrt_trace_integrate')
+        return out.reshape(out_shape).to(device=density.device, dtype=density.dtype)
 
 
 # ----- the operator ---------------------------------------------------------------------------
@@ -428,8 +452,14 @@ class Operator:
 
     # -- trace ---------------------------------------------------------------------------------
     def _trace(self):
-        dev = _lib.require_gpu()
+        """The trace runs on the GPU `device` names (else the current GPU), with that GPU
+        current for every allocation and launch; later calls run there too (_cdev)."""
+        dev = _lib.require_gpu(self.device)
         self._cdev = dev
+        with tr.cuda.device(dev):
+            self._trace_on(dev)
+
+    def _trace_on(self, dev):
         lib = _lib.load()
         self._plan = _Plan(self.grid, dev)
         batch = _RayBatch(self.grid, self.geom.ray_starts, _geom_rays(self.geom, dev), dev)
@@ -468,11 +498,11 @@ class Operator:
         c.empty_ray = empty_ray.data_ptr()
         c.n_cols = math.prod(self.grid.shape[-3:])
         shape3 = tuple(int(v) for v in self.grid.shape[-3:])
-        stage = _set_stage(c, shape3, _stage_brick(nblocks), dev)
+        _set_stage(c, shape3, _stage_brick(nblocks))
         loc, tab = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
         self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, row_ray=row_ray,
                          empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, nblocks=nblocks,
-                         n=n, total=total, desc=c, stage=stage)
+                         n=n, total=total, desc=c)
         self._batch = batch
 
     # -- shape logic of raytracer.py:703-712 -----------------------------------------------------
@@ -495,7 +525,8 @@ class Operator:
             # steady-state fast path: a density already on the compute device, in a dtype and
             # shape seen before -> one allocation and one C call
             ent = self._fast.get((density.shape, density.dtype, density.device))
-            if ent is not None and density.is_contiguous():
+            if ent is not None and density.is_contiguous() and \
+                    _cur_dev() == density.device.index:
                 fn, desc, n_chan, n_vox, div, n, alloc, shape = ent
                 out = tr.empty(alloc, dtype=density.dtype, device=density.device)
                 st = _raw_stream(density.device.index)
@@ -536,21 +567,13 @@ class Operator:
 
     def _launch_forward(self, d, out, n_chan, div):
         """Enqueue the forward kernel on the current stream: d (contiguous, compute device,
-        float32/float64) -> out (preallocated, same dtype).  No host sync; allocates only to grow
-        the brick stage on a first call with more channels."""
-        csr = self._csr
+        float32/float64) -> out (preallocated, same dtype).  No host sync; a brick-staged CSR
+        allocates its stage for the call from the caching allocator."""
         lib = _lib.load()
         self._lengths(d.dtype)
         desc, n_chan, cs, div = self._launch_args(d, n_chan, div)
-        if desc.stage_shape[0] > 0 and n_chan * desc.stage_cols * d.element_size() > desc.stage_bytes:
-            # more channels than the stage holds (first multichannel call): grow it
-            st = tr.zeros(-(-n_chan * desc.stage_cols * d.element_size() // 8), dtype=tr.float64,
-                          device=self._cdev)
-            csr['stage'] = st
-            desc.stage, desc.stage_bytes = st.data_ptr(), st.numel() * 8
         fn = lib.sphrt_forward_f32 if d.dtype == tr.float32 else lib.sphrt_forward_f64
-        _lib.check(fn(desc, _lib.ptr(d), n_chan, cs, div, _lib.ptr(out), csr['n'],
-                      _lib.stream_of(self._cdev)), 'sphrt_forward')
+        _call_forward(fn, desc, d, n_chan, cs, div, out, self._csr['n'], self._cdev)
 
     def _forward_kernel_name(self, d):
         """The forward kernel instantiation a launch on `d` runs (sphrt_forward_*'s choice, for
@@ -567,6 +590,10 @@ class Operator:
         return f'forward_kernel<{t}, {2 if div else 1}, int>'
 
     def _apply_forward(self, density):
+        with tr.cuda.device(self._cdev):      # launches and allocations on the operator's GPU
+            return self._apply_forward_on(density)
+
+    def _apply_forward_on(self, density):
         dev = self._cdev
         n_chan, div, out_shape = self._layout(density.shape)
         in_dtype = density.dtype
@@ -582,8 +609,10 @@ class Operator:
             lib = _lib.load()
             fn = lib.sphrt_forward_f32 if cdt == tr.float32 else lib.sphrt_forward_f64
             desc, b_chan, b_cs, b_div = self._launch_args(d, n_chan, div)
-            self._fast[(density.shape, density.dtype, density.device)] = (
-                fn, ctypes.byref(desc), b_chan, b_cs, b_div, n, alloc, tuple(out_shape))
+            stage = _stage_bytes(desc, b_chan, d.element_size())
+            if not stage:     # the ctypes fast path has no per-call stage
+                self._fast[(density.shape, density.dtype, density.device)] = (
+                    fn, ctypes.byref(desc), b_chan, b_cs, b_div, n, alloc, tuple(out_shape))
             fast = _lib.load_fast()
             if fast is not None:
                 if self._fastc is None:
@@ -591,7 +620,7 @@ class Operator:
                     self._fastc = fast.new(_lib.address(lib.sphrt_last_error))
                 fast.add(self._fastc, tuple(density.shape), cdt == tr.float64, dev.index,
                          _lib.address(fn), ctypes.addressof(desc), b_chan, b_cs, b_div, n,
-                         tuple(out_shape))
+                         tuple(out_shape), stage)
         out = out.view(out_shape)
         if out.device != density.device or cdt != in_dtype:
             out = out.to(device=density.device, dtype=in_dtype)
@@ -650,11 +679,11 @@ class Operator:
         c.empty_ray = empty_vox.data_ptr()
         c.n_cols = csr['n']
         shape3 = self._ray_shape3()
-        stage = _set_stage(c, shape3, _stage_brick(nblocks, 'SPHRT_BRICK_T', _BRICK_RAYS)
-                           if shape3 else None, dev)
+        _set_stage(c, shape3, _stage_brick(nblocks, 'SPHRT_BRICK_T', _BRICK_RAYS)
+                   if shape3 else None)
         loc, tab = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
         return dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, empty_vox, blocks,
-                                  loc, tab, stage))
+                                  loc, tab))
 
     def _paired(self, T, div):
         """The trace with time-paired columns (ray r reads slice r // div: column
@@ -685,6 +714,10 @@ class Operator:
         return csr[key]
 
     def _apply_adjoint(self, y, dshape, ddtype, ddevice):
+        with tr.cuda.device(self._cdev):
+            return self._apply_adjoint_on(y, dshape, ddtype, ddevice)
+
+    def _apply_adjoint_on(self, y, dshape, ddtype, ddevice):
         dev = self._cdev
         n_chan, div, out_shape = self._layout(dshape)
         csr = self._csr
@@ -707,8 +740,7 @@ class Operator:
             res = tr.empty(n_chan * vol, dtype=cdt, device=dev)
             lib = _lib.load()
             fn = lib.sphrt_forward_f32 if cdt == tr.float32 else lib.sphrt_forward_f64
-            _lib.check(fn(tdesc, _lib.ptr(yv), n_chan, n, 0, _lib.ptr(res), vol,
-                          _lib.stream_of(dev)), 'adjoint (transposed forward)')
+            _call_forward(fn, tdesc, yv, n_chan, n, 0, res, vol, dev)
             return res.reshape(dshape).to(device=ddevice, dtype=ddtype)
         acc = tr.zeros(math.prod(dshape), dtype=tr.float64, device=dev)
         _lib.check(_lib.load().sphrt_adjoint_accumulate(

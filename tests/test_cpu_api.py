@@ -266,7 +266,7 @@ def test_fastpath_entry_builds_and_declines_foreign_inputs():
     assert fast.forward(b, torch.zeros(4)) is None
     assert fast.forward(b, [1.0]) is None
     with pytest.raises(ValueError):
-        fast.add(b, (2, 2), False, 0, 0, 0, 1, 4, 0, 4, (4,))
+        fast.add(b, (2, 2), False, 0, 0, 0, 1, 4, 0, 4, (4,), 0)
 
 
 def test_batched_orbit_spec_matches_per_view():
@@ -307,14 +307,28 @@ def test_brick_stage_fields(monkeypatch):
     monkeypatch.setenv('SPHRT_BRICK', '4,4,2')
     assert rt._stage_brick(8) == (4, 4, 2)
     c = _lib.CSR()
-    stage = rt._set_stage(c, (30, 21, 26), (2, 4, 4), 'cpu')
+    assert rt._set_stage(c, (30, 21, 26), (2, 4, 4))
     assert tuple(c.stage_shape) == (30, 21, 26) and tuple(c.stage_brick) == (2, 4, 4)
-    assert c.stage_cols == 30 * 24 * 28 and c.stage_bytes == 8 * c.stage_cols
-    assert stage.numel() == c.stage_cols and c.stage == stage.data_ptr()
-    assert rt._set_stage(c, (30, 21, 26), None, 'cpu') is None and c.stage_shape[0] == 0
-    assert rt._set_stage(c, (2048, 1024, 1024), (2, 4, 4), 'cpu') is None   # 2^31 columns
-    assert rt._set_stage(c, (30, 21, 26), (1, 1, 3), 'cpu') is None          # partial granules
+    assert c.stage_cols == 30 * 24 * 28
+    # the operator owns no stage buffer: each forward call allocates its own
+    assert not c.stage and c.stage_bytes == 0
+    assert rt._stage_bytes(c, 3, 4) == 3 * 4 * c.stage_cols
+    assert not rt._set_stage(c, (30, 21, 26), None) and c.stage_shape[0] == 0
+    assert rt._stage_bytes(c, 3, 4) == 0
+    assert not rt._set_stage(c, (2048, 1024, 1024), (2, 4, 4))   # 2^31 columns
+    assert not rt._set_stage(c, (30, 21, 26), (1, 1, 3))          # partial granules
     assert c.stage_cols == 0 and not c.stage
+
+
+def test_compute_device_resolution():
+    """Operator(device=...) computes on the GPU `device` names; 'cpu' / None (results on the
+    host) compute on the current GPU (_lib.compute_device)."""
+    from sph_raytracer_amd import _lib
+    assert _lib.compute_device('cuda:1', current=0) == tr.device('cuda', 1)
+    assert _lib.compute_device(tr.device('cuda', 2), current=0) == tr.device('cuda', 2)
+    assert _lib.compute_device('cuda', current=3) == tr.device('cuda', 3)
+    assert _lib.compute_device('cpu', current=1) == tr.device('cuda', 1)
+    assert _lib.compute_device(None, current=0) == tr.device('cuda', 0)
 
 
 def test_ctypes_structs_match_the_c_header(tmp_path):

@@ -144,7 +144,7 @@ def test_brick_staged_tables(gpu, monkeypatch):
         assert tuple(t.stage_brick) == (1, 2, 8) and tuple(t.stage_shape) == (4, 24, 30)
         x = tr.rand((3,) + tuple(grid.shape), dtype=tr.float64, device=gpu)
         out = op(x)
-        assert op._csr['desc'].stage_bytes >= 3 * d.stage_cols * 8
+        assert op._csr['desc'].stage_bytes == 0 and not op._csr['desc'].stage   # per call
         for i in range(3):
             assert tr.equal(out[i], op(x[i]))
         # a density 4 bytes off 16-byte alignment (the pack's scalar path), float32
@@ -499,3 +499,56 @@ def test_gd_fused_optimiser_matches_foreach(gpu):
     assert ha[0][-1] < 0.2 * ha[0][0]
     assert tr.allclose(ca, cb, rtol=1e-9, atol=1e-12)
     assert tr.allclose(ya, yb, rtol=1e-9, atol=1e-12)
+
+
+def test_staged_forward_on_concurrent_streams(gpu, monkeypatch):
+    """A brick-staged operator called on two streams at once: each call packs into a stage of its
+    own (per-call caching-allocator buffer), so both results equal the sequential
+    ones bitwise — forward and transposed adjoint, float32 and float64."""
+    from sph_raytracer_amd import Operator
+    monkeypatch.setenv('SPHRT_BRICK', '2,4,4')
+    grid, geom = _orbit(6, (24, 30), grid_shape=(30, 21, 26))
+    op = Operator(grid, geom, device=gpu)
+    assert op._csr['desc'].stage_shape[0] > 0
+    g = tr.Generator(device=gpu).manual_seed(3)
+    for dt in (tr.float32, tr.float64):
+        xs = [tr.rand(grid.shape, dtype=dt, device=gpu, generator=g) for _ in range(2)]
+        ref = [op(x) for x in xs]
+        s1, s2 = tr.cuda.Stream(device=gpu), tr.cuda.Stream(device=gpu)
+        tr.cuda.synchronize(gpu)
+        outs = [None, None]
+        for _ in range(20):
+            for i, s in enumerate((s1, s2)):
+                s.wait_stream(tr.cuda.current_stream(gpu))
+                with tr.cuda.stream(s):
+                    outs[i] = op(xs[i])
+            tr.cuda.current_stream(gpu).wait_stream(s1)
+            tr.cuda.current_stream(gpu).wait_stream(s2)
+            tr.cuda.synchronize(gpu)
+            assert tr.equal(outs[0], ref[0]) and tr.equal(outs[1], ref[1])
+
+
+def test_operator_device_argument(gpu):
+    """Operator(device='cuda:k') traces and computes on GPU k whatever device is current (ADVICE
+    r1): the compute device follows `device`; with two GPUs an operator built on cuda:1 while
+    cuda:0 is current (and called after the current device changed) matches the cuda:0 one."""
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(3, (16, 20), grid_shape=(12, 10, 16))
+    op0 = Operator(grid, geom, device=gpu)
+    assert op0._cdev == tr.device('cuda', 0)
+    x = tr.rand(grid.shape, dtype=tr.float64, device=gpu)
+    y0 = op0(x)
+    assert y0.device == gpu
+    if tr.cuda.device_count() < 2:
+        pytest.skip('one GPU: the cross-device half needs two')
+    dev1 = tr.device('cuda', 1)
+    with tr.cuda.device(0):
+        op1 = Operator(grid, geom, device=dev1)
+    assert op1._cdev == dev1 and op1._csr['row_ptr'].device == dev1
+    x1 = x.to(dev1)
+    with tr.cuda.device(0):
+        y1 = op1(x1)          # current device 0, operator and density on 1
+    assert y1.device == dev1 and tr.equal(y1.cpu(), y0.cpu())
+    with tr.cuda.device(0):
+        g1 = op1.T(y1)
+    assert tr.allclose(g1.cpu(), op0.T(y0).cpu(), rtol=1e-12, atol=1e-12)
