@@ -111,6 +111,27 @@ int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64
                      int32_t *vox, double *len, void *workspace, size_t workspace_size,
                      void *stream);
 
+/* One-pass trace (the same CSR as count + fill, tracing every ray once instead of twice):
+ *  1. sphrt_trace_bound: screens the rays and writes an upper bound of every ray's segment count
+ *     from its geometry alone (int32 `bounds`, 0 for rays that miss the grid); the caller scans
+ *     them (sphrt_scan_counts) into bound_ptr (n+1) and allocates a staging CSR of
+ *     bound_ptr[n] entries (svox int32, slen float64).
+ *  2. sphrt_trace_emit (same workspace: it traces the hit list step 1 left there): every ray's
+ *     exact segment count into `counts`, and its segments into staging slot
+ *     [bound_ptr[ray], bound_ptr[ray+1]) when they fit.  *n_over (device int64) = rays that did
+ *     not fit; if it is non-zero the staging is incomplete and the caller runs sphrt_trace_fill
+ *     instead of step 3 (the counts are exact either way).
+ *  3. after sphrt_scan_counts(counts) -> row_ptr: sphrt_trace_compact moves the rows into the
+ *     tight CSR (vox, len: row_ptr[n] entries). */
+int sphrt_trace_bound(const sphrt_plan *plan, const sphrt_rays *rays, int32_t *bounds,
+                      void *workspace, size_t workspace_size, void *stream);
+int sphrt_trace_emit(const sphrt_plan *plan, const sphrt_rays *rays, const int64_t *bound_ptr,
+                     int32_t *counts, int32_t *svox, double *slen, int64_t *n_over,
+                     void *workspace, size_t workspace_size, void *stream);
+int sphrt_trace_compact(int64_t n, const int64_t *bound_ptr, const int32_t *svox,
+                        const double *slen, const int64_t *row_ptr, int32_t *vox, double *len,
+                        void *stream);
+
 /* ---- on-device cone-beam ray directions (replaces ConeRectGeom.rays, geometry.py:493-508, and
  * ConeCircGeom.rays, geometry.py:570-582) ----------------------------------------------------- */
 /* rays[v][a][b][0..2] for n_views views of h x w pixels, bit-identical to the torch expressions.

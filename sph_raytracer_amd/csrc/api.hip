@@ -139,8 +139,8 @@ extern "C" int sphrt_plan_create(const sphrt_grid_desc* gd, int device, sphrt_pl
         if (!(gd->r_b[j] >= gd->r_b[j - 1])) return fail("r_b must be ascending");
     const int64_t K = 2LL * nbr + 2LL * nbe + nba + 1;
     if (K >= 65535) return fail("too many boundaries (K=%lld)", (long long)K);
-    // table layout: r_b | c2_e | cos_a | sin_a (doubles) | e_flags (bytes)
-    const size_t nd = (size_t)nbr + nbe + 2 * (size_t)nba;
+    // table layout: r_b | c2_e | cos_a | sin_a | e_b | a_b (doubles) | e_flags (bytes)
+    const size_t nd = (size_t)nbr + 2 * (size_t)nbe + 3 * (size_t)nba;
     const size_t bytes = nd * sizeof(double) + (size_t)nbe;
     double* host = (double*)malloc(bytes);
     if (!host) return fail("host allocation failed");
@@ -148,11 +148,18 @@ extern "C" int sphrt_plan_create(const sphrt_grid_desc* gd, int device, sphrt_pl
     double* h_c2 = h_r + nbr;
     double* h_ca = h_c2 + nbe;
     double* h_sa = h_ca + nba;
-    uint8_t* h_fl = (uint8_t*)(h_sa + nba);
+    double* h_eb = h_sa + nba;
+    double* h_ab = h_eb + nbe;
+    uint8_t* h_fl = (uint8_t*)(h_ab + nba);
     memcpy(h_r, gd->r_b, nbr * sizeof(double));
     memcpy(h_c2, gd->cos2_e, nbe * sizeof(double));
     memcpy(h_ca, gd->cos_a, nba * sizeof(double));
     memcpy(h_sa, gd->sin_a, nba * sizeof(double));
+    memcpy(h_eb, gd->e_b, nbe * sizeof(double));
+    memcpy(h_ab, gd->a_b, nba * sizeof(double));
+    int e_asc = 1, a_asc = 1;
+    for (int j = 1; j < nbe; ++j) e_asc &= gd->e_b[j] > gd->e_b[j - 1] ? 1 : 0;
+    for (int j = 1; j < nba; ++j) a_asc &= gd->a_b[j] > gd->a_b[j - 1] ? 1 : 0;
     const double half_pi = 3.141592653589793 / 2;  // tr.pi / 2 (raytracer.py:457)
     for (int j = 0; j < nbe; ++j) {
         uint8_t f = 0;
@@ -184,6 +191,8 @@ extern "C" int sphrt_plan_create(const sphrt_grid_desc* gd, int device, sphrt_pl
     G.close_tol = gd->close_tol;
     G.plane_par_tol = gd->plane_par_tol;
     G.r_outer = gd->r_b[gd->nr];
+    G.e_asc = e_asc;
+    G.a_asc = a_asc;
     double* d = (double*)dmem;
     G.r_b = d;   // the rest of the block follows it (GridDev accessors)
     *out = p;

@@ -24,15 +24,19 @@ struct GridDev {
     double close_tol;      // isclose() threshold (raytracer.py:246)
     double plane_par_tol;  // a_torch parallel threshold (raytracer.py:521)
     double r_outer;        // r_b[nr]
-    // One table block: r_b (nbr) | cos(e_b)**2 (nbe) | cos(a_b) (nba) | sin(a_b) (nba) as doubles,
-    // then e_flags (nbe bytes; bit0: cos(e_b) >= 0, bit1: shadow test exempt, e_b ~ pi/2).  One
-    // pointer instead of five: the trace kernel's arguments stay in fewer SGPRs.
+    int e_asc, a_asc;      // e_b / a_b strictly ascending (segment bounds may binary-search them)
+    // One table block: r_b (nbr) | cos(e_b)**2 (nbe) | cos(a_b) (nba) | sin(a_b) (nba) | e_b (nbe)
+    // | a_b (nba) as doubles, then e_flags (nbe bytes; bit0: cos(e_b) >= 0, bit1: shadow test
+    // exempt, e_b ~ pi/2).  One pointer instead of seven: the trace kernel's arguments stay in
+    // fewer SGPRs.
     const double* r_b;
     __device__ __forceinline__ const double* c2_e() const { return r_b + nbr; }
     __device__ __forceinline__ const double* cos_a() const { return r_b + nbr + nbe; }
     __device__ __forceinline__ const double* sin_a() const { return r_b + nbr + nbe + nba; }
+    __device__ __forceinline__ const double* e_b() const { return r_b + nbr + nbe + 2 * nba; }
+    __device__ __forceinline__ const double* a_b() const { return r_b + nbr + 2 * nbe + 2 * nba; }
     __device__ __forceinline__ const uint8_t* e_flags() const {
-        return reinterpret_cast<const uint8_t*>(r_b + nbr + nbe + 2 * nba);
+        return reinterpret_cast<const uint8_t*>(r_b + nbr + 2 * nbe + 3 * nba);
     }
 };
 

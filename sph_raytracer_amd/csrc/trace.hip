@@ -30,7 +30,11 @@
 
 namespace sphrt {
 
-enum { MODE_COUNT = 0, MODE_FILL = 1, MODE_INTEGRATE = 2 };
+// COUNT / FILL: the two-pass trace (counts, then segments at row_ptr).  BOUND (screen only) and
+// EMIT: the one-pass trace — an upper bound of every ray's segment count from its geometry, then
+// one pass that writes each ray's segments into its bounded slot of a staging CSR (compacted
+// afterwards).  INTEGRATE: the no-store forward.
+enum { MODE_COUNT = 0, MODE_FILL = 1, MODE_INTEGRATE = 2, MODE_EMIT = 3, MODE_BOUND = 4 };
 constexpr int kNone = 0x7fffffff;  // "no update" in the forward-fill scans
 constexpr int kWavesPerBlock = 4;
 
@@ -275,7 +279,20 @@ struct TraceOut {
     int64_t* deferred;               // workspace: deferred ray ids
     unsigned* n_hits;                // workspace: screened hit-ray counter
     HitRay* hits;                    // workspace: hit rays
+    unsigned long long* n_over;      // EMIT: rays whose segments exceed their bound
 };
+
+// EMIT: ray `ray` has `cnt` segments; its staging slot is [row_ptr[ray], row_ptr[ray + 1]) (the
+// scanned bounds).  Returns the slot start, or -1 (counted in n_over) when they do not fit.
+template <typename T>
+__device__ __forceinline__ int64_t emit_slot(const TraceOut<T>& o, int64_t ray, int64_t cnt,
+                                             bool leader) {
+    const int64_t b0 = o.row_ptr[ray], cap = o.row_ptr[ray + 1] - b0;
+    if (leader) o.counts[ray] = (int32_t)cnt;
+    if (cnt <= cap) return b0;
+    if (leader) atomicAdd(o.n_over, 1ull);
+    return -1;
+}
 
 // region rows a candidate updates: bit0 r, bit1 e, bit2 a (start entry: all)
 __device__ __forceinline__ int update_mask(uint32_t pay, int r_lim, int e_lim, int start_c) {
@@ -586,8 +603,13 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     TRACE_ADD(3, ts3, ts4);
     if (MODE == MODE_COUNT) {
         if (lane == 0) o.counts[ray] = head + nseg;
-    } else if (MODE == MODE_FILL) {
-        const int64_t r0 = o.row_ptr[ray];
+    } else if (MODE == MODE_FILL || MODE == MODE_EMIT) {
+        const int64_t r0 = MODE == MODE_FILL ? o.row_ptr[ray]
+                                             : emit_slot(o, ray, head + nseg, lane == 0);
+        if (r0 < 0) {
+            wave_sync();
+            return;
+        }
         if (head && lane == 0) {
             o.vox[r0] = (sr * G.ne + se) * G.na + sa;
             o.len[r0] = -tneg;
@@ -624,6 +646,89 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
 #endif
 }
 
+// ---- segment-count bounds for the one-pass trace (MODE_BOUND) -------------------------------
+// First index of the ascending b[0, n) whose entry is >= v (n when none).
+__device__ __forceinline__ int first_ge(const double* b, int n, double v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (b[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+// Entries of the ascending b[0, n) inside [lo, hi].
+__device__ __forceinline__ int count_in(const double* b, int n, double lo, double hi) {
+    if (!(lo <= hi)) return 0;
+    const int a = first_ge(b, n, lo);
+    int l = a, h = n;                                   // first entry > hi
+    while (l < h) {
+        const int mid = (l + h) >> 1;
+        if (b[mid] <= hi) l = mid + 1;
+        else h = mid;
+    }
+    return l - a;
+}
+__device__ __forceinline__ double polar(double px, double py, double pz) {
+    return atan2(hypot(px, py), pz);
+}
+
+// Upper bound of the segments trace_one emits for a hit ray: the crossings it lists lie in the
+// outer sphere's span [max(t_lo, 0), t_hi] (plus the start entry and the behind-start head), and
+// along a line every family's crossings there are countable from the geometry alone:
+//   spheres  2 per shell of radius >= the line's distance from the centre;
+//   planes   one per half-plane whose azimuth the span's projection sweeps (the sweep is < pi;
+//            a projection through the z axis sweeps them all);
+//   cones    the elevation along a line has at most one extremum (its cosine's derivative has a
+//            linear numerator), so one per cone angle on each monotone stretch.
+// Angle margins (1e-6 rad planes, 1e-4 rad cones: the reference snaps |discriminant| < 1e-5 to a
+// double root) and +2 / +4 absorb rounding.  A bound that fails anyway only costs time: the ray
+// is counted in n_over and the caller falls back to the two-pass trace.  Starts inside a voxel
+// get K: the exact (tie) path may split the behind-start stretch at every crossing behind it.
+__device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok) {
+    if (start_ok) return G.K;
+    const double R = G.r_outer;
+    const double t1c = __builtin_sqrt(R * R - g.dd * g.dd);
+    const double ta = fmax(g.tc - t1c, 0.0), tb = g.tc + t1c;
+    if (!(tb >= ta)) return 2;                       // (NaN: a miss; behind the start: nothing)
+    const double eps = 1e-9;
+    const int n_s = G.nbr - first_ge(G.r_b, G.nbr, g.dd * (1.0 - 1e-12));
+    const double ax = g.x0 + ta * g.w0, ay = g.x1 + ta * g.w1, az = g.x2 + ta * g.w2;
+    const double bx = g.x0 + tb * g.w0, by = g.x1 + tb * g.w1, bz = g.x2 + tb * g.w2;
+    int b_a = G.nba;
+    {
+        const double na = hypot(ax, ay), nb = hypot(bx, by);
+        const double cr = ax * by - ay * bx, dt = ax * bx + ay * by;
+        const bool through_axis = na <= eps * R || nb <= eps * R ||
+                                  (__builtin_fabs(cr) <= eps * na * nb && dt < 0.0);
+        if (G.a_asc && !through_axis) {
+            const double pa = atan2(ay, ax), dp = atan2(cr, dt);
+            const double lo = fmin(pa, pa + dp) - 1e-6, hi = fmax(pa, pa + dp) + 1e-6;
+            const double two_pi = 6.283185307179586;
+            int c = 0;
+            for (int k = -2; k <= 2; ++k) c += count_in(G.a_b(), G.nba, lo + k * two_pi, hi + k * two_pi);
+            if (__builtin_isfinite(lo) && __builtin_isfinite(hi)) b_a = min(c + 2, G.nba);
+        }
+    }
+    int b_e = 2 * G.nbe;
+    if (G.e_asc && g.dd > eps * R) {
+        const double th_a = polar(ax, ay, az), th_b = polar(bx, by, bz);
+        // extremum of cos(elevation) along x + t w: t* = (z0 (x.w) - wz |x|^2) / (wz (x.w) - z0)
+        const double ts = (g.x2 * g.wx - g.w2 * g.nx2) / (g.w2 * g.wx - g.x2);
+        const double m = 1e-4;
+        int c;
+        if (ts > ta && ts < tb) {
+            const double th_s = polar(g.x0 + ts * g.w0, g.x1 + ts * g.w1, g.x2 + ts * g.w2);
+            c = count_in(G.e_b(), G.nbe, fmin(th_a, th_s) - m, fmax(th_a, th_s) + m) +
+                count_in(G.e_b(), G.nbe, fmin(th_s, th_b) - m, fmax(th_s, th_b) + m);
+        } else {
+            c = count_in(G.e_b(), G.nbe, fmin(th_a, th_b) - m, fmax(th_a, th_b) + m);
+        }
+        if (__builtin_isfinite(th_a) && __builtin_isfinite(th_b)) b_e = min(c + 4, 2 * G.nbe);
+    }
+    return min(2 * n_s + b_e + b_a + 4, G.K);
+}
+
 // Screen one ray per lane: a ray yields a segment only if it reaches the outer sphere or starts
 // in a voxel — otherwise every r-row value stays the (invalid) start region (t1c is NaN for every
 // shell when it is NaN for the outermost: monotone in R; tangents excluded).  Misses get their
@@ -640,6 +745,10 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
     const double t1c_outer = __builtin_sqrt(G.r_outer * G.r_outer - g.dd * g.dd);
     const bool start_r_ok = s[0] >= 0 && s[0] < G.nr;
     const bool hit = active && !(!start_r_ok && __builtin_isnan(t1c_outer));
+    if (MODE == MODE_BOUND && active)
+        o.counts[ray] = hit ? segment_bound(G, g, start_r_ok && s[1] >= 0 && s[1] < G.ne &&
+                                                      s[2] >= 0 && s[2] < G.na)
+                            : 0;
     if (active && !hit) {
         if (MODE == MODE_COUNT) o.counts[ray] = 0;
         if (MODE == MODE_INTEGRATE) {
@@ -773,7 +882,8 @@ __device__ void exact_walk(const GridDev& G, const TraceOut<T>& o, int64_t ray, 
         int cr = s[0], ce = s[1], ca = s[2];
         int64_t nseg = 0;
         double acc = 0.0;
-        const int64_t base = MODE == MODE_FILL ? o.row_ptr[ray] : 0;
+        const int64_t base = MODE == MODE_FILL || MODE == MODE_EMIT ? o.row_ptr[ray] : 0;
+        const int64_t cap = MODE == MODE_EMIT ? o.row_ptr[ray + 1] - base : INT64_MAX;
         auto cur = v.get(0);
         for (int k = 0; k < K; ++k) {
             const double t = cur.t;
@@ -792,7 +902,7 @@ __device__ void exact_walk(const GridDev& G, const TraceOut<T>& o, int64_t ray, 
             if (!(len > 0.0) || !__builtin_isfinite(len)) continue;
             if (cr < 0 || cr >= G.nr || ce < 0 || ce >= G.ne || ca < 0 || ca >= G.na) continue;
             const int vx = (cr * G.ne + ce) * G.na + ca;
-            if (MODE == MODE_FILL) {
+            if (MODE == MODE_FILL || (MODE == MODE_EMIT && nseg < cap)) {
                 o.vox[base + nseg] = vx;
                 o.len[base + nseg] = len;
             } else if (MODE == MODE_INTEGRATE) {
@@ -801,6 +911,7 @@ __device__ void exact_walk(const GridDev& G, const TraceOut<T>& o, int64_t ray, 
             ++nseg;
         }
         if (MODE == MODE_COUNT) o.counts[ray] = (int32_t)nseg;
+        if (MODE == MODE_EMIT) (void)emit_slot(o, ray, nseg, true);
         if (MODE == MODE_INTEGRATE) {
             const int64_t oc = o.ray_chan_div > 0 ? 0 : c;
             o.out[oc * o.out_chan_stride + ray] = (T)acc;
@@ -861,9 +972,9 @@ __device__ void exact_walk_wave(const GridDev& G, const TraceOut<T>& o, int64_t 
     wave_sync();
     if (MODE == MODE_COUNT) {
         if (lane == 0) o.counts[ray] = nseg;
-    } else if (MODE == MODE_FILL) {
-        const int64_t r0 = o.row_ptr[ray];
-        for (int q = lane; q < nseg; q += 64) {
+    } else if (MODE == MODE_FILL || MODE == MODE_EMIT) {
+        const int64_t r0 = MODE == MODE_FILL ? o.row_ptr[ray] : emit_slot(o, ray, nseg, lane == 0);
+        for (int q = lane; r0 >= 0 && q < nseg; q += 64) {
             o.vox[r0 + q] = seg_vox[q];
             o.len[r0 + q] = seg_len[q];
         }
@@ -1078,6 +1189,36 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
     }
 }
 
+// ---- one-pass trace: staging slots -> tight CSR ---------------------------------------------
+// Every wave moves the rows of 64 consecutive rays: lane i reads ray i's slot and row pointers,
+// then the wave copies the rows one after the other (rows average 10-60 segments).
+__global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* __restrict__ slot,
+                                                      const int64_t* __restrict__ row_ptr,
+                                                      const int32_t* __restrict__ svox,
+                                                      const double* __restrict__ slen,
+                                                      int32_t* __restrict__ vox,
+                                                      double* __restrict__ len) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    for (int64_t r0 = wave * 64; r0 < n; r0 += nw * 64) {
+        const int64_t r = r0 + lane;
+        const bool in = r < n;
+        const int64_t a = in ? row_ptr[r] : 0, c = in ? row_ptr[r + 1] - a : 0;
+        const int64_t b = in ? slot[r] : 0;
+        uint64_t todo = __ballot(c > 0);
+        while (todo) {
+            const int i = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int64_t ai = __shfl(a, i), ci = __shfl(c, i), bi = __shfl(b, i);
+            for (int64_t q = lane; q < ci; q += 64) {
+                vox[ai + q] = svox[bi + q];
+                len[ai + q] = slen[bi + q];
+            }
+        }
+    }
+}
+
 // ---- host launchers ----------------------------------------------------------------------
 static int trace_cap(const GridDev& G) { return ((G.K + 63) / 64) * 64; }
 constexpr int kExactBlocks = 4096;   // one wave per deferred ray, 16 per CU
@@ -1099,9 +1240,14 @@ static size_t workspace_bytes(const GridDev& G, int64_t n) {
            exact_scratch_bytes(G);
 }
 
+// Which launches of a trace a call makes: screen (hit list; counts/zeros/bounds of the misses)
+// and trace (the hit rays + the deferred exact ones).  BOUND screens only; EMIT traces the hit
+// list an earlier BOUND call left in the same workspace.
+enum { kScreen = 1, kTrace = 2 };
+
 template <int MODE, typename T>
 static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void* workspace,
-                        size_t workspace_size, hipStream_t st) {
+                        size_t workspace_size, hipStream_t st, int steps = kScreen | kTrace) {
     if (G.nr < 1 || G.ne < 1 || G.na < 1) return fail("tracing needs at least one voxel per axis");
     if (R.n == 0) return 0;
     if (!workspace || workspace_size < workspace_bytes(G, R.n))
@@ -1121,10 +1267,18 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     o.deferred = (int64_t*)(ws + kWsHead);
     o.hits = (HitRay*)(ws + kWsHead + (((size_t)R.n * sizeof(int64_t) + 255) / 256) * 256);
     Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
-    if (hipMemsetAsync(ws, 0, kWsHead, st) != hipSuccess) return fail("memset failed");
-    hipLaunchKernelGGL((screen_kernel<MODE, T>), dim3((unsigned)((R.n + 255) / 256)), dim3(256), 0,
-                       st, G, R, o);
-    if (int e = check_launch("screen_kernel")) return e;
+    if constexpr (MODE == MODE_BOUND) steps = kScreen;
+    if constexpr (MODE == MODE_EMIT) steps = kTrace;
+    if (steps & kScreen) {
+        if (hipMemsetAsync(ws, 0, kWsHead, st) != hipSuccess) return fail("memset failed");
+        hipLaunchKernelGGL((screen_kernel<MODE, T>), dim3((unsigned)((R.n + 255) / 256)), dim3(256),
+                           0, st, G, R, o);
+        if (int e = check_launch("screen_kernel")) return e;
+    } else if (hipMemsetAsync(o.n_deferred, 0, sizeof(unsigned long long), st) != hipSuccess) {
+        return fail("memset failed");
+    }
+    if constexpr (MODE == MODE_BOUND) return 0;
+    if (!(steps & kTrace)) return 0;
     // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
     const int64_t grid = 2048 * kWavesPerBlock / waves;
     hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,
@@ -1169,6 +1323,53 @@ extern "C" int sphrt_trace_count(const sphrt_plan* plan, const sphrt_rays* rays,
     o.counts = counts;
     return launch_trace<MODE_COUNT, double>(G, R, o, workspace, workspace_size,
                                             (hipStream_t)stream);
+}
+
+extern "C" int sphrt_trace_bound(const sphrt_plan* plan, const sphrt_rays* rays, int32_t* bounds,
+                                 void* workspace, size_t workspace_size, void* stream) {
+    GridDev G;
+    RaysDev R;
+    if (int e = resolve(plan, rays, G, R, stream)) return e;
+    DeviceGuard guard(plan->device);
+    if (!bounds) return fail("null bounds");
+    TraceOut<double> o{};
+    o.counts = bounds;
+    return launch_trace<MODE_BOUND, double>(G, R, o, workspace, workspace_size,
+                                            (hipStream_t)stream, kScreen);
+}
+
+extern "C" int sphrt_trace_emit(const sphrt_plan* plan, const sphrt_rays* rays,
+                                const int64_t* bound_ptr, int32_t* counts, int32_t* svox,
+                                double* slen, int64_t* n_over, void* workspace,
+                                size_t workspace_size, void* stream) {
+    GridDev G;
+    RaysDev R;
+    if (int e = resolve(plan, rays, G, R, stream)) return e;
+    DeviceGuard guard(plan->device);
+    if (!bound_ptr || !counts || !svox || !slen || !n_over) return fail("null emit argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(n_over, 0, sizeof(int64_t), st) != hipSuccess) return fail("memset failed");
+    TraceOut<double> o{};
+    o.row_ptr = bound_ptr;
+    o.counts = counts;
+    o.vox = svox;
+    o.len = slen;
+    o.n_over = (unsigned long long*)n_over;
+    return launch_trace<MODE_EMIT, double>(G, R, o, workspace, workspace_size, st, kTrace);
+}
+
+extern "C" int sphrt_trace_compact(int64_t n, const int64_t* bound_ptr, const int32_t* svox,
+                                   const double* slen, const int64_t* row_ptr, int32_t* vox,
+                                   double* len, void* stream) {
+    if (n < 0) return fail("negative ray count");
+    if (n == 0) return 0;
+    if (!bound_ptr || !svox || !slen || !row_ptr || !vox || !len) return fail("null compact argument");
+    StreamGuard guard(stream);
+    const int64_t waves = (n + 63) / 64;
+    const int64_t blocks = (waves + 3) / 4 < 8192 ? (waves + 3) / 4 : 8192;
+    hipLaunchKernelGGL(compact_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       n, bound_ptr, row_ptr, svox, slen, vox, len);
+    return check_launch("compact_kernel");
 }
 
 extern "C" int sphrt_trace_fill(const sphrt_plan* plan, const sphrt_rays* rays,

@@ -372,6 +372,68 @@ def _workspace(lib, plan, n, dev):
     return tr.empty(lib.sphrt_trace_workspace_bytes(plan.handle, n), dtype=tr.uint8, device=dev)
 
 
+_bound_hook = None   # tests only: callable(bounds) run on the one-pass trace's bounds
+
+
+def _trace_csr(lib, plan, batch, dev, stream):
+    """Trace every ray of `batch` into the segment CSR -> (row_ptr, vox, len, total).
+
+    One pass (sphrt_trace_bound / _emit / _compact, include/sphrt.h): a geometric upper bound of
+    every ray's segment count sizes a staging CSR, every ray is traced once into its slot, and
+    the rows are compacted — two host syncs (the bound total; the segment total).  The two-pass
+    trace (count, then fill: every ray traced twice, one sync) serves when the staging would
+    not fit comfortably in free device memory, when a bound failed (then only the fill pass
+    runs: the counts are exact), and on request (SPHRT_TRACE=twopass)."""
+    n = batch.n
+    counts = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
+    row_ptr = tr.empty(n + 1, dtype=tr.int64, device=dev)
+    ws = tr.empty(lib.sphrt_scan_workspace_bytes(n), dtype=tr.uint8, device=dev)
+    tws = _workspace(lib, plan, n, dev)
+    h, d, tw = plan.handle, batch.desc, (_lib.ptr(tws), tws.numel())
+
+    def scan(src, dst):
+        _lib.check(lib.sphrt_scan_counts(_lib.ptr(src), n, _lib.ptr(dst), _lib.ptr(ws), stream),
+                   'sphrt_scan_counts')
+
+    def fill(total):
+        vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+        seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
+        _lib.check(lib.sphrt_trace_fill(h, d, _lib.ptr(row_ptr), _lib.ptr(vox), _lib.ptr(seg_len),
+                                        *tw, stream), 'sphrt_trace_fill')
+        return vox, seg_len
+
+    if n > 0 and os.environ.get('SPHRT_TRACE', 'onepass') != 'twopass':
+        bound_ptr = tr.empty(n + 1, dtype=tr.int64, device=dev)
+        _lib.check(lib.sphrt_trace_bound(h, d, _lib.ptr(counts), *tw, stream), 'sphrt_trace_bound')
+        if _bound_hook is not None:      # tests: shrink bounds to exercise the fallback
+            _bound_hook(counts[:n])
+        scan(counts, bound_ptr)          # (counts holds the bounds until the emit pass)
+        cap = int(bound_ptr[n].item())   # host sync 1
+        if cap * 12 <= 0.4 * tr.cuda.mem_get_info(dev)[0]:
+            svox = tr.empty(max(cap, 1), dtype=tr.int32, device=dev)
+            slen = tr.empty(max(cap, 1), dtype=tr.float64, device=dev)
+            over = tr.empty(1, dtype=tr.int64, device=dev)
+            _lib.check(lib.sphrt_trace_emit(h, d, _lib.ptr(bound_ptr), _lib.ptr(counts),
+                                            _lib.ptr(svox), _lib.ptr(slen), _lib.ptr(over),
+                                            *tw, stream), 'sphrt_trace_emit')
+            scan(counts, row_ptr)
+            total, n_over = tr.stack((row_ptr[n], over[0])).tolist()   # host sync 2
+            if n_over == 0:
+                vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+                seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
+                _lib.check(lib.sphrt_trace_compact(n, _lib.ptr(bound_ptr), _lib.ptr(svox),
+                                                   _lib.ptr(slen), _lib.ptr(row_ptr),
+                                                   _lib.ptr(vox), _lib.ptr(seg_len), stream),
+                           'sphrt_trace_compact')
+                return row_ptr, vox, seg_len, total
+            del svox, slen
+            return (row_ptr,) + fill(total) + (total,)
+    _lib.check(lib.sphrt_trace_count(h, d, _lib.ptr(counts), *tw, stream), 'sphrt_trace_count')
+    scan(counts, row_ptr)
+    total = int(row_ptr[n].item())        # the one host sync of the two-pass trace
+    return (row_ptr,) + fill(total) + (total,)
+
+
 def line_integrals(grid, geom, density):
     """No-store forward: trace and integrate in one fused pass, nothing persisted.
 
@@ -466,21 +528,7 @@ class Operator:
         self._ray_shape = batch.shape
         n = batch.n
         stream = _lib.stream_of(dev)
-        counts = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
-        row_ptr = tr.empty(n + 1, dtype=tr.int64, device=dev)
-        ws = tr.empty(lib.sphrt_scan_workspace_bytes(n), dtype=tr.uint8, device=dev)
-        tws = _workspace(lib, self._plan, n, dev)
-        _lib.check(lib.sphrt_trace_count(self._plan.handle, batch.desc, _lib.ptr(counts),
-                                         _lib.ptr(tws), tws.numel(), stream), 'sphrt_trace_count')
-        _lib.check(lib.sphrt_scan_counts(_lib.ptr(counts), n, _lib.ptr(row_ptr), _lib.ptr(ws),
-                                         stream), 'sphrt_scan_counts')
-        total = int(row_ptr[n].item())          # the one host sync of the trace
-        vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
-        seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
-        _lib.check(lib.sphrt_trace_fill(self._plan.handle, batch.desc, _lib.ptr(row_ptr),
-                                        _lib.ptr(vox), _lib.ptr(seg_len), _lib.ptr(tws),
-                                        tws.numel(), stream), 'sphrt_trace_fill')
-        del tws
+        row_ptr, vox, seg_len, total = _trace_csr(lib, self._plan, batch, dev, stream)
         # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
         nblocks = lib.sphrt_csr_blocks(total)
         row_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)

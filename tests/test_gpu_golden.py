@@ -166,3 +166,28 @@ def test_device_rays_bit_identical(gpu):
         got = _device_rays(g, gpu)
         assert got is not None
         assert tr.equal(got.cpu(), g.rays), type(g).__name__
+
+
+def _csr(op):
+    c = op._csr
+    return (c['row_ptr'].cpu(), c['vox'][:c['total']].cpu(), c['len'][:c['total']].cpu())
+
+
+@pytest.mark.parametrize('name', gc.CASES)
+def test_onepass_trace_equals_twopass(name, gpu, monkeypatch):
+    """The one-pass trace (geometric segment bounds -> staging slots -> compaction) builds the
+    same CSR as the two-pass count + fill, bit for bit; so does its fallback when bounds fail
+    (forced by halving every bound: the emit pass overflows, the counts stay exact and only the
+    fill pass runs)."""
+    from sph_raytracer_amd import raytracer as rt
+    case = gc.load(name)
+    monkeypatch.setenv('SPHRT_TRACE', 'twopass')
+    ref = _csr(_op(case, gpu))
+    monkeypatch.setenv('SPHRT_TRACE', 'onepass')
+    got = _csr(_op(case, gpu))
+    for a, b in zip(ref, got):
+        assert tr.equal(a, b), name
+    monkeypatch.setattr(rt, '_bound_hook', lambda b: b.div_(2, rounding_mode='floor'))
+    got = _csr(_op(case, gpu))
+    for a, b in zip(ref, got):
+        assert tr.equal(a, b), name + ' (fallback)'

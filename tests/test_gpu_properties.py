@@ -552,3 +552,31 @@ def test_operator_device_argument(gpu):
     with tr.cuda.device(0):
         g1 = op1.T(y1)
     assert tr.allclose(g1.cpu(), op0.T(y0).cpu(), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize('kind, n_views, det, grid_shape', [
+    ('rect', 50, (50, 100), (50, 50, 50)),          # C2
+    ('circ', 64, (100, 50), (64, 64, 64)),          # C5 geometry: ring 0 through the origin
+    ('rect', 8, (64, 96), (40, 70, 33)),
+])
+def test_onepass_trace_full_size(kind, n_views, det, grid_shape, gpu, monkeypatch):
+    """At full size the one-pass trace equals the two-pass one bit for bit and no ray exceeds its
+    geometric bound (every bound holds: the fallback is not taken)."""
+    from sph_raytracer_amd import Operator, raytracer as rt
+    grid, geom = _orbit(n_views, det, kind=kind, grid_shape=grid_shape)
+    monkeypatch.setenv('SPHRT_TRACE', 'twopass')
+    ref = Operator(grid, geom, device=gpu)._csr
+    monkeypatch.setenv('SPHRT_TRACE', 'onepass')
+    calls = []
+    orig = rt._lib.load().sphrt_trace_fill
+
+    def spy(*a):
+        calls.append(1)
+        return orig(*a)
+    monkeypatch.setattr(rt._lib.load(), 'sphrt_trace_fill', spy)
+    got = Operator(grid, geom, device=gpu)._csr
+    assert not calls, 'a segment bound failed: the one-pass trace fell back to the fill pass'
+    assert ref['total'] == got['total']
+    for k in ('row_ptr', 'vox', 'len'):
+        assert tr.equal(ref[k][:ref['total'] if k != 'row_ptr' else None],
+                        got[k][:got['total'] if k != 'row_ptr' else None]), k
