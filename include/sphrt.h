@@ -212,6 +212,15 @@ int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_
 int sphrt_csr_local_count(const sphrt_csr *csr, int64_t *blocks, int64_t *stats, void *stream);
 int sphrt_csr_local_fill(const sphrt_csr *csr, const int64_t *blocks, uint16_t *loc, void *tab,
                          int64_t tab_stride, void *stream);
+/* The same tables in one pass: _build decides n_tab (and the fallback blocks) and writes loc and
+ * each kept block's table at the fixed wide stride SPHRT_TAB_WIDE (tab_wide: n_blocks *
+ * SPHRT_TAB_WIDE entries of tab_bytes each), with stats as in _count; the caller picks tab_stride
+ * from stats and _pack copies the tables to that stride.  Same output as _count + _fill. */
+#define SPHRT_TAB_WIDE 2048
+int sphrt_csr_local_build(const sphrt_csr *csr, int64_t *blocks, uint16_t *loc, void *tab_wide,
+                          int64_t *stats, void *stream);
+int sphrt_csr_local_pack(const sphrt_csr *csr, const int64_t *blocks, const void *tab_wide,
+                         void *tab, int64_t tab_stride, void *stream);
 /* Time-paired columns for a dynamic operator whose view i sees time slice i (ray r reads slice
  * r / div): vox_out[s] = (r / div) * vol + voxel, head bit kept, for every segment of ray r.  A
  * CSR with these columns (and its own blocks / tables, n_cols = T * vol) is a static CSR over the

@@ -47,6 +47,7 @@ class CSR(ctypes.Structure):
 ROW_HEAD = 0x80000000
 BLOCK_FIELDS = 6           # SPHRT_BLOCK_FIELDS
 LOC_HEAD = 0x8000          # SPHRT_LOC_HEAD
+TAB_WIDE = 2048            # SPHRT_TAB_WIDE
 
 # (name, restype, argtypes) — mirrors include/sphrt.h one to one
 _SIGNATURES = [
@@ -74,6 +75,8 @@ _SIGNATURES = [
     ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     ('sphrt_csr_local_count', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp]),
     ('sphrt_csr_local_fill', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp]),
+    ('sphrt_csr_local_build', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ('sphrt_csr_local_pack', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp]),
     ('sphrt_csr_time_columns', c_int, [ctypes.POINTER(CSR), c_i64, c_i64, c_vp, c_vp]),
     ('sphrt_forward_f32', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,
                                   c_vp]),

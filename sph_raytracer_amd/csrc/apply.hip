@@ -44,6 +44,13 @@ constexpr int kLocalMax = 4096;                 // segments per workgroup with a
 constexpr int kMaxGran = 2046;                  // granules per table (sphrt_csr_local): loc's
                                                 // 15-bit byte offsets reach 16*(2046+1)+12
 constexpr int kGranEarly = 3;                   // table chunks of 256 fetched before the record
+// Granule-table build modes: kTabCount — n_tab and the fallback decision only (stats); kTabFill —
+// the tables of the blocks kTabCount kept, at a caller-chosen stride; kTabBuild — both in one
+// pass, tables at the wide stride kTabWide (sphrt_csr_local_build), packed to the final stride
+// afterwards (sphrt_csr_local_pack).
+enum { kTabCount = 0, kTabFill = 1, kTabBuild = 2 };
+constexpr int kTabWide = SPHRT_TAB_WIDE;
+static_assert(kTabWide >= kMaxGran, "wide tables hold every table");
 
 // Diagnostic build only (-DSPHRT_FWD_STAMPS, tools/fwd_timeline.py): s_memrealtime (100 MHz)
 // stamps of wave 0 of every forward workgroup at its phase boundaries.
@@ -410,7 +417,7 @@ __global__ __launch_bounds__(256) void stage_pack_kernel(const T* __restrict__ s
 // bitmap is small (n_cols/4 bits; 128^3 voxels = 64 KiB): set one bit per segment, prefix-popcount
 // the words, and a granule's rank is the number of set bits below it.  O(segments + words) per
 // workgroup, a handful of barriers.  Identical output to the sort (ascending distinct granules).
-template <bool FILL, typename TabT = int32_t>
+template <int TM, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int n_words, StageMap sm,
@@ -421,11 +428,11 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
     __shared__ ScanShared sh;
     int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
     const int64_t s0 = m[2], s1 = m[3];
-    if (FILL && m[5] < 0) return;
+    if (TM == kTabFill && m[5] < 0) return;
     const int tid = threadIdx.x;
     const int64_t n = s1 - s0;
     if (n > kLocalMax) {
-        if (!FILL && tid == 0) {
+        if (TM != kTabFill && tid == 0) {
             m[5] = -1;
             atomicAdd(stats, 1ull);
         }
@@ -445,7 +452,7 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
     for (int w = w0; w < w1; ++w) cnt += __builtin_popcount(bm[w]);
     int n_tab;
     int run = block_excl_count(cnt, n_tab, sh);
-    if (!FILL) {
+    if (TM != kTabFill) {
         if (tid == 0) {
             if (n_tab > kMaxGran) {
                 m[5] = -1;
@@ -455,7 +462,7 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
                 atomicMax(stats + 1, (unsigned long long)n_tab);
             }
         }
-        return;
+        if (TM == kTabCount || n_tab > kMaxGran) return;
     }
     TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
     for (int w = w0; w < w1; ++w) {
@@ -480,36 +487,30 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
 // from a block radix sort of the workgroup's segments by granule (hipCUB, 16 per thread), value
 // = position << 3 | head << 2 | voxel & 3.  O(segments · key bits) per workgroup instead of
 // O(volume): at C3 (2 M voxels, 64 k workgroups) 10.6 ms of bitmap work.  Identical output.
-constexpr int kRadixItems = kLocalMax / kThreads;   // 16
-template <bool FILL, typename TabT = int32_t>
-__global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
-    int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
-    TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
-    unsigned long long* stats) {
+template <int ITEMS, int TM>
+struct RadixTable {
     // the count pass sorts keys only (its values are dead)
     using Sort = typename std::conditional<
-        FILL, hipcub::BlockRadixSort<uint32_t, kThreads, kRadixItems, uint16_t>,
-        hipcub::BlockRadixSort<uint32_t, kThreads, kRadixItems>>::type;
-    __shared__ typename Sort::TempStorage sort_ts;
-    __shared__ uint32_t last_key[kThreads];
-    __shared__ ScanShared sh;
-    int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
-    const int64_t s0 = m[2], s1 = m[3];
-    if (FILL && m[5] < 0) return;
+        TM != kTabCount, hipcub::BlockRadixSort<uint32_t, kThreads, ITEMS, uint16_t>,
+        hipcub::BlockRadixSort<uint32_t, kThreads, ITEMS>>::type;
+    using Storage = typename Sort::TempStorage;
+};
+
+// One block's table from a sort of its n <= ITEMS * kThreads segments (block-uniform call).
+template <int ITEMS, int TM, typename TabT>
+__device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restrict__ vox,
+                                            uint16_t* __restrict__ loc, TabT* __restrict__ tab_b,
+                                            int64_t s0, int n, int key_bits, const StageMap& sm,
+                                            unsigned char* ts_raw, uint32_t* last_key,
+                                            ScanShared& sh, unsigned long long* stats) {
+    using RT = RadixTable<ITEMS, TM>;
+    auto& ts = *reinterpret_cast<typename RT::Storage*>(ts_raw);
     const int tid = threadIdx.x;
-    const int64_t n = s1 - s0;
-    if (n > kLocalMax) {
-        if (!FILL && tid == 0) {
-            m[5] = -1;
-            atomicAdd(stats, 1ull);
-        }
-        return;
-    }
-    uint32_t key[kRadixItems];
-    uint16_t val[kRadixItems];
+    uint32_t key[ITEMS];
+    uint16_t val[ITEMS];
 #pragma unroll
-    for (int i = 0; i < kRadixItems; ++i) {
-        const int p = tid * kRadixItems + i;
+    for (int i = 0; i < ITEMS; ++i) {
+        const int p = tid * ITEMS + i;
         key[i] = 0xffffffffu;                     // padding sorts last
         val[i] = 0;
         if (p < n) {
@@ -519,22 +520,22 @@ __global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
             val[i] = (uint16_t)((p << 3) | ((x >> 31) << 2) | (v & 3u));
         }
     }
-    if constexpr (FILL) Sort(sort_ts).Sort(key, val, 0, key_bits);   // blocked: thread t holds
-    else Sort(sort_ts).Sort(key, 0, key_bits);                       // sorted [16t, 16t+16)
-    last_key[tid] = key[kRadixItems - 1];
+    if constexpr (TM != kTabCount) typename RT::Sort(ts).Sort(key, val, 0, key_bits);   // blocked:
+    else typename RT::Sort(ts).Sort(key, 0, key_bits);            // thread t: [ITEMS t, ITEMS t + ITEMS)
+    last_key[tid] = key[ITEMS - 1];
     __syncthreads();
     uint32_t prev = tid > 0 ? last_key[tid - 1] : 0xffffffffu;
     int first_new = 0;
 #pragma unroll
-    for (int i = 0; i < kRadixItems; ++i) {
-        const int p = tid * kRadixItems + i;
+    for (int i = 0; i < ITEMS; ++i) {
+        const int p = tid * ITEMS + i;
         const bool fresh = p < n && (p == 0 || key[i] != prev);
         first_new += fresh ? 1 : 0;
         prev = key[i];
     }
     int n_tab;
     int rank = block_excl_count(first_new, n_tab, sh) - 1;
-    if (!FILL) {
+    if (TM != kTabFill) {
         if (tid == 0) {
             if (n_tab > kMaxGran) {
                 m[5] = -1;
@@ -544,13 +545,12 @@ __global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
                 atomicMax(stats + 1, (unsigned long long)n_tab);
             }
         }
-        return;
+        if (TM == kTabCount || n_tab > kMaxGran) return;
     }
     prev = tid > 0 ? last_key[tid - 1] : 0xffffffffu;
-    TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
 #pragma unroll
-    for (int i = 0; i < kRadixItems; ++i) {
-        const int p = tid * kRadixItems + i;
+    for (int i = 0; i < ITEMS; ++i) {
+        const int p = tid * ITEMS + i;
         if (p < n) {
             if (p == 0 || key[i] != prev) {
                 ++rank;
@@ -561,6 +561,52 @@ __global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
         }
         prev = key[i];
     }
+}
+
+// Blocks of up to 2048 segments (most: a block owns the rows starting in 1792 segments) sort 8
+// keys per thread, larger ones 16: half the sort work for the common case.
+template <int TM, typename TabT = int32_t>
+__global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
+    int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
+    TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
+    unsigned long long* stats) {
+    constexpr size_t kTs = sizeof(typename RadixTable<16, TM>::Storage) >
+                                   sizeof(typename RadixTable<8, TM>::Storage)
+                               ? sizeof(typename RadixTable<16, TM>::Storage)
+                               : sizeof(typename RadixTable<8, TM>::Storage);
+    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[kTs];
+    __shared__ uint32_t last_key[kThreads];
+    __shared__ ScanShared sh;
+    int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
+    const int64_t s0 = m[2], s1 = m[3];
+    if (TM == kTabFill && m[5] < 0) return;
+    const int64_t n = s1 - s0;
+    if (n > kLocalMax) {
+        if (TM != kTabFill && threadIdx.x == 0) {
+            m[5] = -1;
+            atomicAdd(stats, 1ull);
+        }
+        return;
+    }
+    TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
+    if (n <= 8 * kThreads)
+        radix_table<8, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key,
+                                 sh, stats);
+    else
+        radix_table<16, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key,
+                                  sh, stats);
+}
+
+// Wide tables (one-pass build, kTabWide entries per block) -> the final stride.
+template <typename TabT>
+__global__ __launch_bounds__(kThreads) void table_pack_kernel(const int64_t* __restrict__ blocks,
+                                                              const TabT* __restrict__ wide,
+                                                              TabT* __restrict__ tab,
+                                                              int64_t tab_stride) {
+    const int64_t b = blockIdx.x;
+    const int64_t n_tab = blocks[kBlockFields * b + 5];
+    for (int64_t i = threadIdx.x; i < n_tab; i += kThreads)
+        tab[b * tab_stride + i] = wide[b * kTabWide + i];
 }
 
 // LDS image of a workgroup's granule table: granule 0 is zero (the read of every masked slot),
@@ -1130,12 +1176,12 @@ extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_
     if (c->n_segments == 0) return 0;
     const int64_t cols = table_cols(c);
     if (const int words = table_bitmap_words(cols)) {
-        hipLaunchKernelGGL((local_table_bitmap_kernel<false, int32_t>), dim3((unsigned)c->n_blocks),
+        hipLaunchKernelGGL((local_table_bitmap_kernel<kTabCount, int32_t>), dim3((unsigned)c->n_blocks),
                            dim3(kThreads), (size_t)words * 8, st, blocks, c->vox, nullptr, nullptr,
                            0, words, sm, (unsigned long long*)stats);
         return check_launch("local_table_bitmap_kernel<count>");
     }
-    hipLaunchKernelGGL((local_table_radix_kernel<false, int32_t>), dim3((unsigned)c->n_blocks),
+    hipLaunchKernelGGL((local_table_radix_kernel<kTabCount, int32_t>), dim3((unsigned)c->n_blocks),
                        dim3(kThreads), 0, st, blocks, c->vox, nullptr, nullptr, 0,
                        granule_key_bits(cols), sm, (unsigned long long*)stats);
     return check_launch("local_table_radix_kernel<count>");
@@ -1157,25 +1203,81 @@ extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, u
     hipStream_t st = (hipStream_t)stream;
     if (const int words = table_bitmap_words(cols)) {
         if (u16)
-            hipLaunchKernelGGL((local_table_bitmap_kernel<true, uint16_t>), dim3((unsigned)c->n_blocks),
+            hipLaunchKernelGGL((local_table_bitmap_kernel<kTabFill, uint16_t>), dim3((unsigned)c->n_blocks),
                                dim3(kThreads), (size_t)words * 8, st, (int64_t*)blocks, c->vox, loc,
                                (uint16_t*)tab, tab_stride, words, sm, nullptr);
         else
-            hipLaunchKernelGGL((local_table_bitmap_kernel<true, int32_t>), dim3((unsigned)c->n_blocks),
+            hipLaunchKernelGGL((local_table_bitmap_kernel<kTabFill, int32_t>), dim3((unsigned)c->n_blocks),
                                dim3(kThreads), (size_t)words * 8, st, (int64_t*)blocks, c->vox, loc,
                                (int32_t*)tab, tab_stride, words, sm, nullptr);
         return check_launch("local_table_bitmap_kernel<fill>");
     }
     const int kb = granule_key_bits(cols);
     if (u16)
-        hipLaunchKernelGGL((local_table_radix_kernel<true, uint16_t>), dim3((unsigned)c->n_blocks),
+        hipLaunchKernelGGL((local_table_radix_kernel<kTabFill, uint16_t>), dim3((unsigned)c->n_blocks),
                            dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (uint16_t*)tab,
                            tab_stride, kb, sm, nullptr);
     else
-        hipLaunchKernelGGL((local_table_radix_kernel<true, int32_t>), dim3((unsigned)c->n_blocks),
+        hipLaunchKernelGGL((local_table_radix_kernel<kTabFill, int32_t>), dim3((unsigned)c->n_blocks),
                            dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (int32_t*)tab,
                            tab_stride, kb, sm, nullptr);
     return check_launch("local_table_radix_kernel<fill>");
+}
+
+extern "C" int sphrt_csr_local_build(const sphrt_csr* c, int64_t* blocks, uint16_t* loc,
+                                     void* tab_wide, int64_t* stats, void* stream) {
+    if (!c || !c->vox || !blocks || !loc || !tab_wide || !stats)
+        return fail("incomplete CSR for the granule tables");
+    if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
+    StageMap sm;
+    if (!stage_map(c, sm)) return fail("inconsistent brick staging fields");
+    const int64_t cols = table_cols(c);
+    const bool u16 = c->tab_bytes == 2;
+    if (u16 && (cols + 3) / 4 > 65536) return fail("16-bit granule tables need <= 2^18 columns");
+    StreamGuard guard(stream);
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(stats, 0, 2 * sizeof(int64_t), st) != hipSuccess)
+        return fail("hipMemsetAsync failed");
+    if (c->n_segments == 0) return 0;
+    const dim3 g((unsigned)c->n_blocks), b(kThreads);
+    unsigned long long* s = (unsigned long long*)stats;
+    if (const int words = table_bitmap_words(cols)) {
+        const size_t lds = (size_t)words * 8;
+        if (u16)
+            hipLaunchKernelGGL((local_table_bitmap_kernel<kTabBuild, uint16_t>), g, b, lds, st,
+                               blocks, c->vox, loc, (uint16_t*)tab_wide, kTabWide, words, sm, s);
+        else
+            hipLaunchKernelGGL((local_table_bitmap_kernel<kTabBuild, int32_t>), g, b, lds, st,
+                               blocks, c->vox, loc, (int32_t*)tab_wide, kTabWide, words, sm, s);
+        return check_launch("local_table_bitmap_kernel<build>");
+    }
+    const int kb = granule_key_bits(cols);
+    if (u16)
+        hipLaunchKernelGGL((local_table_radix_kernel<kTabBuild, uint16_t>), g, b, 0, st, blocks,
+                           c->vox, loc, (uint16_t*)tab_wide, kTabWide, kb, sm, s);
+    else
+        hipLaunchKernelGGL((local_table_radix_kernel<kTabBuild, int32_t>), g, b, 0, st, blocks,
+                           c->vox, loc, (int32_t*)tab_wide, kTabWide, kb, sm, s);
+    return check_launch("local_table_radix_kernel<build>");
+}
+
+extern "C" int sphrt_csr_local_pack(const sphrt_csr* c, const int64_t* blocks,
+                                    const void* tab_wide, void* tab, int64_t tab_stride,
+                                    void* stream) {
+    if (!c || !blocks || !tab_wide || !tab) return fail("incomplete CSR for the granule tables");
+    if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
+    if (tab_stride < 1 || tab_stride > (kMaxGran + 63) / 64 * 64)
+        return fail("bad granule table stride");
+    if (c->n_segments == 0) return 0;
+    StreamGuard guard(stream);
+    const dim3 g((unsigned)c->n_blocks), b(kThreads);
+    if (c->tab_bytes == 2)
+        hipLaunchKernelGGL(table_pack_kernel<uint16_t>, g, b, 0, (hipStream_t)stream, blocks,
+                           (const uint16_t*)tab_wide, (uint16_t*)tab, tab_stride);
+    else
+        hipLaunchKernelGGL(table_pack_kernel<int32_t>, g, b, 0, (hipStream_t)stream, blocks,
+                           (const int32_t*)tab_wide, (int32_t*)tab, tab_stride);
+    return check_launch("table_pack_kernel");
 }
 
 static int check_csr(const sphrt_csr* c, int64_t n_chan, int64_t div) {

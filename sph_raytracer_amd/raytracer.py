@@ -280,22 +280,37 @@ def _seg_alloc(total):
 
 
 def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
-    """Per-workgroup granule tables of a CSR (sphrt_csr_local_count/_fill); sets desc.loc/.tab/
-    .tab_stride/.n_fallback.  One host sync (the largest table decides the stride)."""
+    """Per-workgroup granule tables of a CSR; sets desc.loc/.tab/.tab_stride/.n_fallback.  One
+    host sync (the largest table decides the stride).  One pass (sphrt_csr_local_build into
+    SPHRT_TAB_WIDE-strided tables, then _pack to the stride) unless the wide tables would not fit
+    comfortably in free memory or SPHRT_TABLES=twopass (sphrt_csr_local_count, then _fill)."""
     stats = tr.empty(2, dtype=tr.int64, device=dev)
-    _lib.check(lib.sphrt_csr_local_count(desc, _lib.ptr(blocks), _lib.ptr(stats), stream),
-               'sphrt_csr_local_count')
-    n_fallback, max_tab = stats.tolist()
-    stride = max(64, (max_tab + 63) // 64 * 64)
     loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
     # 16-bit entries when every granule index fits (<= 2^18 columns): half the table bytes the
     # forward streams
     cols = desc.stage_cols if desc.stage_shape[0] > 0 else desc.n_cols
     desc.tab_bytes = 2 if (cols + 3) // 4 <= 65536 else 4
-    tab = tr.empty(nblocks * stride + 3 * 256, dtype=tr.int16 if desc.tab_bytes == 2 else tr.int32,
-                   device=dev)   # + early-fetch pad
-    _lib.check(lib.sphrt_csr_local_fill(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(tab),
-                                        stride, stream), 'sphrt_csr_local_fill')
+    tdt = tr.int16 if desc.tab_bytes == 2 else tr.int32
+    wide_bytes = nblocks * _lib.TAB_WIDE * desc.tab_bytes
+    one_pass = (os.environ.get('SPHRT_TABLES', 'onepass') != 'twopass' and
+                wide_bytes <= 0.3 * tr.cuda.mem_get_info(dev)[0])
+    if one_pass:
+        wide = tr.empty(nblocks * _lib.TAB_WIDE, dtype=tdt, device=dev)
+        _lib.check(lib.sphrt_csr_local_build(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(wide),
+                                             _lib.ptr(stats), stream), 'sphrt_csr_local_build')
+    else:
+        _lib.check(lib.sphrt_csr_local_count(desc, _lib.ptr(blocks), _lib.ptr(stats), stream),
+                   'sphrt_csr_local_count')
+    n_fallback, max_tab = stats.tolist()
+    stride = max(64, (max_tab + 63) // 64 * 64)
+    tab = tr.empty(nblocks * stride + 3 * 256, dtype=tdt, device=dev)   # + early-fetch pad
+    if one_pass:
+        _lib.check(lib.sphrt_csr_local_pack(desc, _lib.ptr(blocks), _lib.ptr(wide), _lib.ptr(tab),
+                                            stride, stream), 'sphrt_csr_local_pack')
+        del wide
+    else:
+        _lib.check(lib.sphrt_csr_local_fill(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(tab),
+                                            stride, stream), 'sphrt_csr_local_fill')
     desc.n_fallback, desc.tab_stride = n_fallback, stride
     desc.loc, desc.tab = loc.data_ptr(), tab.data_ptr()
     return loc, tab

@@ -580,3 +580,27 @@ def test_onepass_trace_full_size(kind, n_views, det, grid_shape, gpu, monkeypatc
     for k in ('row_ptr', 'vox', 'len'):
         assert tr.equal(ref[k][:ref['total'] if k != 'row_ptr' else None],
                         got[k][:got['total'] if k != 'row_ptr' else None]), k
+
+
+@pytest.mark.parametrize('grid_shape, staged', [((50, 50, 50), 'auto'), ((96, 80, 90), 'auto'),
+                                                ((30, 21, 26), '2,4,4')])
+def test_onepass_tables_equal_twopass(grid_shape, staged, gpu, monkeypatch):
+    """Granule tables built in one pass (wide tables + pack) equal the count + fill ones: block
+    records, loc, tables (bitmap build at 50^3, radix build above 2^19 voxels, brick-staged)."""
+    from sph_raytracer_amd import Operator
+    monkeypatch.setenv('SPHRT_BRICK', staged)
+    grid, geom = _orbit(6, (40, 64), grid_shape=grid_shape)
+    res = []
+    for mode in ('twopass', 'onepass'):
+        monkeypatch.setenv('SPHRT_TABLES', mode)
+        c = Operator(grid, geom, device=gpu)._csr
+        d = c['desc']
+        res.append((c['blocks'].cpu(), c['loc'][:c['total']].cpu(), d.tab_stride, d.n_fallback,
+                    c['tab'][:c['nblocks'] * d.tab_stride].cpu()))
+    (b0, l0, s0, f0, t0), (b1, l1, s1, f1, t1) = res
+    assert s0 == s1 and f0 == f1
+    assert tr.equal(b0, b1) and tr.equal(l0, l1)
+    n_tab = b0.reshape(-1, 6)[:, 5]
+    for b in range(len(n_tab)):      # entries past n_tab are unused (uninitialised)
+        k = int(n_tab[b])
+        assert tr.equal(t0[b * s0:b * s0 + k], t1[b * s1:b * s1 + k])
