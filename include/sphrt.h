@@ -161,8 +161,8 @@ int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const doubl
  * loc/tab/n_cols/tab_stride set, a static forward on a 16-byte-aligned density stages each
  * block's granules in LDS (4 * (tab_stride + 1) elements, up to 64 KB) instead of gathering per
  * segment.
- * Per-segment arrays (vox, len, len32, loc) are read in aligned 8-entry chunks: allocate
- * them to round_up(n_segments, 8) entries (the entries past n_segments are never used).  `len32` is
+ * Per-segment arrays (vox, len, len32, loc) are read in aligned 8- or 16-entry chunks: allocate
+ * them to round_up(n_segments, 16) entries (the entries past n_segments are never used).  `len32` is
  * the float32 copy of `len` used by the float32 forward (sphrt_f64_to_f32). */
 #define SPHRT_ROW_HEAD 0x80000000u
 #define SPHRT_BLOCK_FIELDS 6   /* int64 per entry of blocks */

@@ -28,6 +28,20 @@ constexpr int kThreads = 256;
 #ifndef SPHRT_FWD_MINB32
 #define SPHRT_FWD_MINB32 6   // the same for float32
 #endif
+// Segments per forward thread (8: 256-thread workgroups, 16: 128-thread ones — half the waves,
+// so half the per-wave scan / close / address instructions for the same segments), per density
+// dtype, and the waves per SIMD the 16-segment kernels' registers aim for.  Measured with 16 for
+// float32: C2 6.7 -> 7.7 us, C5 34.4 -> 37.6 us, C3 236 -> 241 us (the longer serial chain per
+// thread costs more than the saved issue slots), so 8 everywhere.
+#ifndef SPHRT_FWD_P32
+#define SPHRT_FWD_P32 8
+#endif
+#ifndef SPHRT_FWD_P64
+#define SPHRT_FWD_P64 8
+#endif
+#ifndef SPHRT_FWD_MINW16
+#define SPHRT_FWD_MINW16 5
+#endif
 // 64-bit min/max as plain selects (HIP's min<int64_t>/max<int64_t> went through double
 // conversions on VALU even for uniform operands).
 __host__ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
@@ -217,7 +231,7 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <bool kDrain>   // kDrain: a full barrier (also retires LDS-DMA granule loads)
+template <bool kDrain, int W = 4>   // kDrain: a full barrier (also retires LDS-DMA granule loads)
 __device__ __forceinline__ int block_excl_count1(int v, int& total, int (&cnt)[4]) {
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -226,11 +240,16 @@ __device__ __forceinline__ int block_excl_count1(int v, int& total, int (&cnt)[4
     if (kDrain) __syncthreads();
     else lds_barrier();
     const int4 c = *reinterpret_cast<const int4*>(cnt);     // one LDS read, no per-wave loop
+    if constexpr (W == 2) {                                 // (slots 2, 3 unused)
+        total = c.x + c.y;
+        return (wid > 0 ? c.x : 0) + inc - v;
+    }
     total = c.x + c.y + c.z + c.w;
     const int base = (wid > 0 ? c.x : 0) + (wid > 1 ? c.y : 0) + (wid > 2 ? c.z : 0);
     return base + inc - v;
 }
 
+template <int W = 4>
 __device__ __forceinline__ double block_excl_segsum1(bool has, double tail, bool& tot_has,
                                                      double& tot_sum, int (&hs)[4],
                                                      double (&sm)[4]) {
@@ -254,15 +273,15 @@ __device__ __forceinline__ double block_excl_segsum1(bool has, double tail, bool
     const int4 hv = *reinterpret_cast<const int4*>(hs);   // vector LDS reads, no per-wave loop
     const double2 s01 = *reinterpret_cast<const double2*>(sm);
     const double2 s23 = *reinterpret_cast<const double2*>(sm + 2);
-    const int hw[4] = {hv.x, hv.y, hv.z, hv.w};
-    const double sw[4] = {s01.x, s01.y, s23.x, s23.y};
+    const int hw[4] = {hv.x, hv.y, W > 2 ? hv.z : 0, W > 2 ? hv.w : 0};   // (W = 2: 2, 3 unused)
+    const double sw[4] = {s01.x, s01.y, W > 2 ? s23.x : 0.0, W > 2 ? s23.y : 0.0};
     double t[4];                                   // segmented prefix through wave w
     t[0] = sw[0];
 #pragma unroll
     for (int w = 1; w < 4; ++w) t[w] = hw[w] ? sw[w] : t[w - 1] + sw[w];
     const double cs = wid == 0 ? 0.0 : wid == 1 ? t[0] : wid == 2 ? t[1] : t[2];
     tot_sum = t[3];
-    tot_has = (hv.x | hv.y | hv.z | hv.w) != 0;
+    tot_has = (hw[0] | hw[1] | hw[2] | hw[3]) != 0;
     return eh ? es : cs + es;
 }
 
@@ -616,13 +635,15 @@ __global__ __launch_bounds__(kThreads) void table_pack_kernel(const int64_t* __r
 // round r of wave w covers table entries gran_entry(r, w, lane) (64/G granules, G lanes each).
 template <typename T>
 constexpr int kGranLanes = (int)sizeof(T) / 4;        // 16-byte DMA lanes per granule
-template <typename T>   // early rounds: kGranEarly chunks of 256 granules
-constexpr int kEarlyRounds = kGranEarly * kGranLanes<T>;
+// Early rounds cover kGranEarly chunks of 256 table entries whatever the workgroup size (THR
+// threads: a round moves THR / G granules).
+template <typename T, int THR = kThreads>
+constexpr int kEarlyRounds = kGranEarly * (256 / THR) * kGranLanes<T>;
 
-template <typename T>
+template <typename T, int THR = kThreads>
 __device__ __forceinline__ int gran_entry0(int r, int w) {    // first entry of round r (uniform)
     constexpr int G = kGranLanes<T>;
-    return (r / G) * kThreads + w * 64 + (r % G) * (64 / G);
+    return (r / G) * THR + w * 64 + (r % G) * (64 / G);
 }
 
 template <typename T>
@@ -644,11 +665,11 @@ __device__ __forceinline__ void stage_one(const T* __restrict__ rho, int32_t g, 
 
 // The volume's last granule, if partial (voxel count not a multiple of 4), can only be the
 // table's last entry: the DMA skips it (no read past the volume) and one lane copies it here.
-template <typename T, typename TabT>
+template <typename T, typename TabT, int THR = kThreads>
 __device__ __forceinline__ void stage_partial_tail(const T* __restrict__ rho,
                                                    const TabT* __restrict__ tab_b, int n_tab,
                                                    int64_t n_cols, T* dens) {
-    if ((n_cols & 3) != 0 && n_tab > 0 && (int)threadIdx.x == (n_tab - 1) % kThreads) {
+    if ((n_cols & 3) != 0 && n_tab > 0 && (int)threadIdx.x == (n_tab - 1) % THR) {
         const int j = n_tab - 1;
         const int64_t v0 = 4 * (int64_t)tab_b[j];
         if (v0 + 4 > n_cols)
@@ -657,15 +678,15 @@ __device__ __forceinline__ void stage_partial_tail(const T* __restrict__ rho,
 }
 
 // DMA rounds [r0, ..) of the table, entries read from memory one round at a time.
-template <typename T, typename TabT>
+template <typename T, typename TabT, int THR = kThreads>
 __device__ __forceinline__ void stage_granules_late(const T* __restrict__ rho,
                                                     const TabT* __restrict__ tab_b, int r0,
                                                     int n_tab, int32_t g_full, T* dens) {
     constexpr int G = kGranLanes<T>;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int r = r0; (r / G) * kThreads < n_tab; ++r) {
-        const int e0 = gran_entry0<T>(r, w);
+    for (int r = r0; (r / G) * THR < n_tab; ++r) {
+        const int e0 = gran_entry0<T, THR>(r, w);
         const int e = e0 + lane / G;
         if (e < n_tab) {
             const int32_t g = (int32_t)tab_b[e];
@@ -678,110 +699,163 @@ __device__ __forceinline__ void stage_granules_late(const T* __restrict__ rho,
 // (large tables) are fetched here.  When the volume's voxel count is not a multiple of 4 its
 // last granule is partial: only the table's last entry can be, it is skipped by the DMA (no read
 // past the volume) and copied lane by lane at the end.  Writes the zero granule.
-template <typename T, typename TabT>
+template <typename T, typename TabT, int THR = kThreads>
 __device__ __forceinline__ void stage_granules(const T* __restrict__ rho,
-                                               const int32_t (&ti)[kEarlyRounds<T>],
+                                               const int32_t (&ti)[kEarlyRounds<T, THR>],
                                                const TabT* __restrict__ tab_b, int n_tab,
                                                int32_t g_full, int64_t n_cols, T* dens) {
     constexpr int G = kGranLanes<T>;
+    constexpr int R = kEarlyRounds<T, THR>;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < 4) dens[threadIdx.x] = (T)0;
     // every early table entry is consumed before the first DMA goes out (one wait, not one per
     // DMA: the wait-count model serialises VMEM results read after an LDS-DMA)
 #pragma unroll
-    for (int r = 0; r < kEarlyRounds<T>; ++r) asm volatile("" ::"v"(ti[r]));
+    for (int r = 0; r < R; ++r) asm volatile("" ::"v"(ti[r]));
 #pragma unroll
-    for (int r = 0; r < kEarlyRounds<T>; ++r) {
-        const int e0 = gran_entry0<T>(r, w);
+    for (int r = 0; r < R; ++r) {
+        const int e0 = gran_entry0<T, THR>(r, w);
         if (e0 + lane / G < n_tab && ti[r] < g_full) stage_one<T>(rho, ti[r], e0, lane, dens);
     }
-    stage_granules_late<T, TabT>(rho, tab_b, kEarlyRounds<T>, n_tab, g_full, dens);
-    stage_partial_tail<T, TabT>(rho, tab_b, n_tab, n_cols, dens);
+    stage_granules_late<T, TabT, THR>(rho, tab_b, R, n_tab, g_full, dens);
+    stage_partial_tail<T, TabT, THR>(rho, tab_b, n_tab, n_cols, dens);
+}
+
+// Early DMA (forward_kernel<..., EDMA = true>): the early rounds go out as a fixed number of
+// unconditional LDS-DMAs right after the table entries arrive, before the first segment chunk is
+// decoded — every lane of every round issues (lanes past the table re-read granule 0 into slots
+// past the table, inside the LDS image), so the wait-count model knows exactly how many DMAs
+// follow the chunk's loads and waits for the chunk alone; the DMA round trip then overlaps the
+// chunk's arrival instead of following it.  Needs whole granules (columns % 4 == 0: no partial
+// tail granule) and an LDS image of at least kGranEarly * 256 granules.
+template <typename T, int THR = kThreads>
+__device__ __forceinline__ void stage_granules_early(const T* __restrict__ rho,
+                                                     const int32_t (&ti)[kEarlyRounds<T, THR>],
+                                                     int n_tab, T* dens) {
+    constexpr int G = kGranLanes<T>;
+    constexpr int R = kEarlyRounds<T, THR>;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < 4) dens[threadIdx.x] = (T)0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) asm volatile("" ::"v"(ti[r]));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e0 = gran_entry0<T, THR>(r, w);
+        const int32_t g = e0 + lane / G < n_tab ? ti[r] : 0;
+        stage_one<T>(rho, g, e0, lane, dens);
+    }
+}
+
+// Segment lengths of one chunk of P segments as aligned 16-byte vectors.
+template <typename L, int P>
+__device__ __forceinline__ void load_lens(const L* __restrict__ len, L (&l)[P]) {
+    constexpr int E = 16 / (int)sizeof(L);      // lengths per 16-byte vector
+    const uint4* lp = reinterpret_cast<const uint4*>(len);
+#pragma unroll
+    for (int k = 0; k < P / E; ++k) {
+        const uint4 f = lp[k];
+        const uint32_t w[4] = {f.x, f.y, f.z, f.w};
+        if constexpr (sizeof(L) == 4) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) l[4 * k + i] = __uint_as_float(w[i]);
+        } else {
+            l[2 * k] = __longlong_as_double((long long)(((uint64_t)w[1] << 32) | w[0]));
+            l[2 * k + 1] = __longlong_as_double((long long)(((uint64_t)w[3] << 32) | w[2]));
+        }
+    }
 }
 
 // The first pass's loads, issued before anything is known about the workgroup and decoded
-// later (raw registers keep the compiler from waiting on them early).
-template <typename L, bool LOCAL>
+// later (raw registers keep the compiler from waiting on them early).  P segments per thread:
+// loc half-words (8 per 16-byte vector) or vox words (4 per vector), and their lengths.
+template <typename L, bool LOCAL, int P = kPer>
 struct RawChunk {
-    uint4 ix[LOCAL ? 1 : 2];
-    L l[kPer];
+    uint4 ix[LOCAL ? P / 8 : P / 4];
+    L l[P];
 };
 
-template <typename L, bool LOCAL>
+template <typename L, bool LOCAL, int P = kPer>
 __device__ __forceinline__ void raw_load(const int32_t* __restrict__ vox,
                                          const uint16_t* __restrict__ loc,
                                          const L* __restrict__ len, int64_t a,
-                                         RawChunk<L, LOCAL>& r) {
+                                         RawChunk<L, LOCAL, P>& r) {
     // unconditional (the caller clamps `a` into the arrays; chunks outside the window are masked
     // by window_chunk): no branch, so no copy of a load result that would wait for it early
-    if constexpr (LOCAL) {
-        r.ix[0] = *reinterpret_cast<const uint4*>(loc + a);
-    } else {
-        const uint4* vp = reinterpret_cast<const uint4*>(vox + a);
-        r.ix[0] = vp[0];
-        r.ix[1] = vp[1];
-    }
-    load_len8(len + a, 0, r.l);
+    const uint4* ip = LOCAL ? reinterpret_cast<const uint4*>(loc + a)
+                            : reinterpret_cast<const uint4*>(vox + a);
+#pragma unroll
+    for (int k = 0; k < (LOCAL ? P / 8 : P / 4); ++k) r.ix[k] = ip[k];
+    load_lens<L, P>(len + a, r.l);
 }
 
-// Bits [first, end) of a chunk (chunk-relative segment window).
+// Bits [first, end) of a chunk of P segments (chunk-relative segment window).
+template <int P = kPer>
 __device__ __forceinline__ uint32_t window_bits(int first, int end) {
-    const int a = max(first, 0), b = min(end, kPer);
-    return a < b ? ((1u << b) - 1u) & ~((1u << a) - 1u) : 0u;
+    const int a = max(first, 0), b = min(end, P);
+    return a < b ? (uint32_t)(((1ull << b) - 1ull) & ~((1ull << a) - 1ull)) : 0u;
 }
 
 // A chunk's segment columns: table mode keeps the loc half-words packed two per register (head
 // bits cleared; slot k = LDS byte offset of its voxel, vslot()), otherwise the vox words.
-template <bool LOCAL>
-constexpr int kVW = LOCAL ? kPer / 2 : kPer;
+template <bool LOCAL, int P = kPer>
+constexpr int kVW = LOCAL ? P / 2 : P;
 
-template <bool LOCAL>
-__device__ __forceinline__ uint32_t vslot(const uint32_t (&v)[kVW<LOCAL>], int k) {
+template <bool LOCAL, int P = kPer>
+__device__ __forceinline__ uint32_t vslot(const uint32_t (&v)[kVW<LOCAL, P>], int k) {
     if constexpr (LOCAL) return (v[k >> 1] >> (16 * (k & 1))) & 0xffffu;
     else return v[k];
 }
 
 // Decode a raw chunk; returns the row heads of the chunk (bit k = segment k).
-template <typename L, bool LOCAL>
-__device__ __forceinline__ uint32_t decode(const RawChunk<L, LOCAL>& r, uint32_t (&v)[kVW<LOCAL>],
-                                           L (&l)[kPer]) {
+template <typename L, bool LOCAL, int P = kPer>
+__device__ __forceinline__ uint32_t decode(const RawChunk<L, LOCAL, P>& r,
+                                           uint32_t (&v)[kVW<LOCAL, P>], L (&l)[P]) {
     uint32_t hmask = 0;
     if constexpr (LOCAL) {
-        const uint32_t w[4] = {r.ix[0].x, r.ix[0].y, r.ix[0].z, r.ix[0].w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = w[j] & 0x7ffc7ffcu;
-        // bit 15 of half-word k -> bit k: even k to bits 0,2,4,6, odd k to 16,18,20,22, folded
-        const uint32_t h = ((w[0] >> 15) & 0x10001u) | ((w[1] >> 13) & 0x40004u) |
-                           ((w[2] >> 11) & 0x100010u) | ((w[3] >> 9) & 0x400040u);
-        hmask = (h | (h >> 15)) & 0xffu;
+        for (int q = 0; q < P / 8; ++q) {
+            const uint32_t w[4] = {r.ix[q].x, r.ix[q].y, r.ix[q].z, r.ix[q].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * q + j] = w[j] & 0x7ffc7ffcu;
+            // bit 15 of half-word k -> bit k: even k to bits 0,2,4,6, odd k to 16,18,20,22,
+            // folded
+            const uint32_t h = ((w[0] >> 15) & 0x10001u) | ((w[1] >> 13) & 0x40004u) |
+                               ((w[2] >> 11) & 0x100010u) | ((w[3] >> 9) & 0x400040u);
+            hmask |= ((h | (h >> 15)) & 0xffu) << (8 * q);
+        }
     } else {
-        v[0] = r.ix[0].x; v[1] = r.ix[0].y; v[2] = r.ix[0].z; v[3] = r.ix[0].w;
-        v[4] = r.ix[1].x; v[5] = r.ix[1].y; v[6] = r.ix[1].z; v[7] = r.ix[1].w;
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) hmask |= (v[k] >> 31) << k;
+        for (int q = 0; q < P / 4; ++q) {
+            v[4 * q] = r.ix[q].x; v[4 * q + 1] = r.ix[q].y;
+            v[4 * q + 2] = r.ix[q].z; v[4 * q + 3] = r.ix[q].w;
+        }
+#pragma unroll
+        for (int k = 0; k < P; ++k) hmask |= (v[k] >> 31) << k;
     }
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) l[k] = r.l[k];
+    for (int k = 0; k < P; ++k) l[k] = r.l[k];
     return hmask;
 }
 
-// Load, decode and window one chunk [p0, p0 + kPer) of a pass (pass-relative window [lo, hi)):
+// Load, decode and window one chunk [p0, p0 + P) of a pass (pass-relative window [lo, hi)):
 // masked slots read the zero granule / voxel 0 with length 0 and carry no head.
-template <typename L, bool LOCAL>
-__device__ __forceinline__ uint32_t window_chunk(const RawChunk<L, LOCAL>& r, int p0, int lo,
-                                                 int hi, uint32_t (&v)[kVW<LOCAL>], L (&l)[kPer]) {
-    uint32_t hmask = decode<L, LOCAL>(r, v, l);
-    if (p0 < lo || p0 + kPer > hi) {                // edge chunks only
+template <typename L, bool LOCAL, int P = kPer>
+__device__ __forceinline__ uint32_t window_chunk(const RawChunk<L, LOCAL, P>& r, int p0, int lo,
+                                                 int hi, uint32_t (&v)[kVW<LOCAL, P>],
+                                                 L (&l)[P]) {
+    uint32_t hmask = decode<L, LOCAL, P>(r, v, l);
+    if (p0 < lo || p0 + P > hi) {                   // edge chunks only
         const int first = lo - p0, end = hi - p0;
 #pragma unroll
-        for (int k = 0; k < kPer; ++k)
+        for (int k = 0; k < P; ++k)
             if (k < first || k >= end) {
                 if constexpr (LOCAL) v[k >> 1] &= ~(0xffffu << (16 * (k & 1)));
                 else v[k] = 0u;
                 l[k] = (L)0;
             }
-        hmask &= window_bits(first, end);
+        hmask &= window_bits<P>(first, end);
     }
     return hmask;
 }
@@ -816,14 +890,17 @@ enum FwdMode { kFwdTable = 0, kFwdGather = 1, kFwdDynamic = 2 };
 
 // Resident workgroups per CU the register allocation aims for: 6 (<= 80 VGPRs) lets a C2-sized
 // launch (~1500 workgroups) be resident at once; float64 stops at 5 (no spills).
-template <typename T, int MODE>
-constexpr int fwd_min_blocks() { return sizeof(T) == 8 ? SPHRT_FWD_MINB64 : SPHRT_FWD_MINB32; }
+template <typename T, int P>
+constexpr int fwd_min_blocks() {
+    return P == kPer ? (sizeof(T) == 8 ? SPHRT_FWD_MINB64 : SPHRT_FWD_MINB32) : SPHRT_FWD_MINW16;
+}
 
 template <typename T>
 using AccumOf = typename std::conditional<sizeof(T) == 4, float, double>::type;
 
-template <typename T, typename L, int MODE, typename TabT = int32_t>
-__global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward_kernel(
+template <typename T, typename L, int MODE, typename TabT = int32_t, bool EDMA = false,
+          int P = kPer>
+__global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_kernel(
     const int64_t* __restrict__ blocks, const int32_t* __restrict__ vox,
     const uint16_t* __restrict__ loc, const TabT* __restrict__ tab, const L* __restrict__ len,
     const int32_t* __restrict__ row_ray, const int32_t* __restrict__ empty_ray,
@@ -834,10 +911,12 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
     extern __shared__ __attribute__((aligned(16))) unsigned char fwd_dyn_lds[];
     T* dens = reinterpret_cast<T*>(fwd_dyn_lds);   // 4 * tab_stride entries (table mode)
     constexpr bool local = MODE == kFwdTable;
+    constexpr int THR = kPass / P;                  // threads (P segments each per pass)
+    constexpr int W = THR / 64;
     using A = AccumOf<T>;
     int par = 0;                                    // scan slot parity
     const int tid = threadIdx.x;
-    const int o = tid * kPer;                       // this thread's chunk within a pass
+    const int o = tid * P;                          // this thread's chunk within a pass
     const int64_t nc = MODE == kFwdDynamic ? 1 : n_chan;
     // Everything addressed by the workgroup index alone goes out before the block record
     // arrives: the first pass (rows of block b start in [b*kSegPerBlock, (b+1)*kSegPerBlock),
@@ -845,19 +924,21 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
     const int64_t blk = block_of(xcd_chunk);
     FWD_STAMP(0);
     const int64_t base0 = blk * kSegPerBlock;
-    const int64_t last_chunk = imax64((n_seg + kPer - 1) / kPer, 1) - 1;   // clamp for loads
-    RawChunk<L, local> raw;
-    raw_load<L, local>(vox, loc, len, imin64(base0 + o, last_chunk * kPer), raw);
+    const int64_t last_chunk = imax64((n_seg + P - 1) / P, 1) - 1;   // clamp for loads
+    RawChunk<L, local, P> raw;
+    if (!EDMA) raw_load<L, local, P>(vox, loc, len, imin64(base0 + o, last_chunk * P), raw);
     // table chunks beyond the stride read the next workgroup's entries (tab is padded by
     // kGranEarly*kThreads entries); they are never staged (j >= n_tab)
     const TabT* tab_b = tab + blk * tab_stride;
-    int32_t ti[kEarlyRounds<T>];
+    int32_t ti[kEarlyRounds<T, THR>];
     if (local) {
         const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
-        for (int r = 0; r < kEarlyRounds<T>; ++r)
-            ti[r] = (int32_t)tab_b[gran_entry0<T>(r, w) + (tid & 63) / kGranLanes<T>];
+        for (int r = 0; r < kEarlyRounds<T, THR>; ++r)
+            ti[r] = (int32_t)tab_b[gran_entry0<T, THR>(r, w) + (tid & 63) / kGranLanes<T>];
     }
+    // early DMA: the table entries first, so waiting for them does not wait for the chunk
+    if (EDMA) raw_load<L, local, P>(vox, loc, len, imin64(base0 + o, last_chunk * P), raw);
     __builtin_amdgcn_sched_barrier(0);
     const int64_t* m = blocks + kBlockFields * blk;
     const int64_t s0 = m[2], k0 = m[4], n_tab = m[5];
@@ -875,7 +956,7 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
         asm volatile("" : "+v"(r_empty));     // keep every use (and its wait) down here
         if (tid < e_n)
             for (int64_t c = 0; c < nc; ++c) out[c * ocs + r_empty] = (T)0;
-        for (int j = tid + kThreads; j < e_n; j += kThreads) {
+        for (int j = tid + THR; j < e_n; j += THR) {
             const int64_t r = empty_ray[e_lo + j];
             for (int64_t c = 0; c < nc; ++c) out[c * ocs + r] = (T)0;
         }
@@ -885,20 +966,35 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
         return;
     }
     const int32_t g_full = (int32_t)imin64(n_cols >> 2, INT32_MAX);   // whole granules
-    if (local) stage_granules<T, TabT>(density, ti, tab_b, (int)n_tab, g_full, n_cols, dens);
+    if (local && EDMA) stage_granules_early<T, THR>(density, ti, (int)n_tab, dens);
+    else if (local)
+        stage_granules<T, TabT, THR>(density, ti, tab_b, (int)n_tab, g_full, n_cols, dens);
     // pass-relative segment window [lo, hi) of this workgroup (32-bit lane arithmetic)
     auto window = [&](int64_t base, int& lo, int& hi) {
         lo = (int)imax64(s0 - base, -1);
         hi = (int)imin64(s1 - base, (int64_t)kPass + 1);
     };
-    uint32_t v[kVW<local>];
-    L l[kPer];
+    uint32_t v[kVW<local, P>];
+    L l[P];
     uint32_t hmask;
+    if constexpr (local && EDMA) {
+        // Loads complete in issue order: the chunk is in once at most the empty-list load and the
+        // early DMAs issued after it are outstanding.  Said explicitly: the compiler's model
+        // treats LDS-DMA as another event type and would wait for every DMA (vmcnt(0)).
+        constexpr int after = 1 + kEarlyRounds<T, THR>;
+        static_assert(after < 16, "vmcnt field");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt((after & 15) | (7 << 4) | (15 << 8));
+        __builtin_amdgcn_sched_barrier(0);
+    }
     {
         int lo, hi;
         window(base0, lo, hi);
-        hmask = window_chunk<L, local>(raw, o, lo, hi, v, l);
+        hmask = window_chunk<L, local, P>(raw, o, lo, hi, v, l);
     }
+    if (local && EDMA)        // rounds past the early ones (tables of more than 768 granules)
+        stage_granules_late<T, TabT, THR>(density, tab_b, kEarlyRounds<T, THR>, (int)n_tab, g_full,
+                                          dens);
     int64_t rbase = 0;                            // rows started in earlier passes
     FWD_STAMP(1);
 #pragma clang loop unroll(disable)   // (also no peeling: one copy of the pass body)
@@ -906,8 +1002,8 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
         const T* rho = density + c * cs;
         T* oc = out + c * ocs;
         if (local && c > 0) {
-            stage_granules_late<T, TabT>(rho, tab_b, 0, (int)n_tab, g_full, dens);
-            stage_partial_tail<T, TabT>(rho, tab_b, (int)n_tab, n_cols, dens);
+            stage_granules_late<T, TabT, THR>(rho, tab_b, 0, (int)n_tab, g_full, dens);
+            stage_partial_tail<T, TabT, THR>(rho, tab_b, (int)n_tab, n_cols, dens);
         }
         FWD_STAMP(2);
         double carry = 0.0;                 // open run entering the pass
@@ -919,20 +1015,20 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             // later channels of a one-pass block reuse the decoded first chunk: the segments
             // are streamed once, only the granules are staged per channel
             if (base != base0 || (c != 0 && s1 > base0 + kPass)) {
-                RawChunk<L, local> rc;
-                raw_load<L, local>(vox, loc, len, imin64(base + o, last_chunk * kPer), rc);
-                hmask = window_chunk<L, local>(rc, o, lo, hi, v, l);
+                RawChunk<L, local, P> rc;
+                raw_load<L, local, P>(vox, loc, len, imin64(base + o, last_chunk * P), rc);
+                hmask = window_chunk<L, local, P>(rc, o, lo, hi, v, l);
             }
             const int hcount = __builtin_popcount(hmask);
-            T rv[kPer];
+            T rv[P];
             if constexpr (MODE == kFwdGather) {   // per-segment gathers go out before any scan
 #pragma unroll
-                for (int k = 0; k < kPer; ++k)
-                    rv[k] = l[k] != (L)0 ? rho[vslot<local>(v, k) & ~kHead] : (T)0;
+                for (int k = 0; k < P; ++k)
+                    rv[k] = l[k] != (L)0 ? rho[vslot<local, P>(v, k) & ~kHead] : (T)0;
             }
             int pass_heads;
             // (table mode: the full barrier also retires the granule LDS-DMA)
-            const int hb = block_excl_count1<local>(hcount, pass_heads, sh.cnt[par]);
+            const int hb = block_excl_count1<local, W>(hcount, pass_heads, sh.cnt[par]);
             FWD_STAMP(3);
             pass_heads = __builtin_amdgcn_readfirstlane(pass_heads);
             // rows this thread closes: the run open at its start (row hb-1) and its first own row
@@ -949,18 +1045,18 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             };
             if constexpr (local) {
 #pragma unroll
-                for (int k = 0; k < kPer; ++k)
-                    rv[k] = lds_at<T>(dens, vslot<local>(v, k));   // masked: the zero granule
+                for (int k = 0; k < P; ++k)
+                    rv[k] = lds_at<T>(dens, vslot<local, P>(v, k));   // masked: the zero granule
             }
             if constexpr (MODE == kFwdDynamic) {   // time slice of each segment's ray
                 int rank = 0;
 #pragma unroll
-                for (int k = 0; k < kPer; ++k) {
+                for (int k = 0; k < P; ++k) {
                     rank += (hmask >> k) & 1;
                     T x = (T)0;
                     if (l[k] != (L)0) {
                         const int64_t ray = row_of(rank - 1);
-                        x = density[(ray / div) * cs + (vslot<local>(v, k) & ~kHead)];
+                        x = density[(ray / div) * cs + (vslot<local, P>(v, k) & ~kHead)];
                     }
                     rv[k] = x;
                 }
@@ -968,9 +1064,9 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             // Products and thread-local runs in A (float for a float density: the reference's own
             // precision, 4-cycle VALU ops instead of 8-cycle f64 ones); runs that cross threads are
             // stitched in double.
-            A p[kPer];
+            A p[P];
 #pragma unroll
-            for (int k = 0; k < kPer; ++k) p[k] = (A)rv[k] * (A)l[k];
+            for (int k = 0; k < P; ++k) p[k] = (A)rv[k] * (A)l[k];
             // Row closes: at every head except the workgroup's first segment, and at position kPer
             // in the thread holding the workgroup's last segment when this pass reaches it (masked
             // slots carry no head and zero length, so no per-slot window test is needed).  With
@@ -979,22 +1075,22 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             // start, in double), v1 and v2 (the runs [h1,h2), [h2,h3)) to rows hb-1, hb and hb+1;
             // closes past h3 (chunks of 3+ heads) take a second walk.  One walk gives the runs and
             // the thread's tail (its last run, the scan's input).
-            const uint32_t hm0 = hmask | (1u << kPer);
+            const uint32_t hm0 = hmask | (1u << P);
             const uint32_t hm1 = hm0 & (hm0 - 1), hm2 = hm1 & (hm1 - 1);
             const int h1 = __builtin_ctz(hm0);
-            const int h2 = __builtin_ctz(hm1 | (1u << kPer));
-            const int h3 = __builtin_ctz(hm2 | (1u << kPer));
+            const int h2 = __builtin_ctz(hm1 | (1u << P));
+            const int h3 = __builtin_ctz(hm2 | (1u << P));
             A tail = (A)0, qa = (A)0, v1 = (A)0, v2 = (A)0;
 #pragma unroll
-            for (int k = 0; k <= kPer; ++k) {
+            for (int k = 0; k <= P; ++k) {
                 qa = k == h1 ? tail : qa;
                 v1 = k == h2 ? tail : v1;
                 v2 = k == h3 ? tail : v2;
-                if (k < kPer) tail = ((hmask >> k) & 1 ? (A)0 : tail) + p[k];
+                if (k < P) tail = ((hmask >> k) & 1 ? (A)0 : tail) + p[k];
             }
             bool tot_has;
             double tot_sum;
-            const double ex = block_excl_segsum1(hmask != 0, (double)tail, tot_has, tot_sum,
+            const double ex = block_excl_segsum1<W>(hmask != 0, (double)tail, tot_has, tot_sum,
                                                  sh.has[par], sh.sum[par]);
             par ^= 1;
             FWD_STAMP(4);
@@ -1004,8 +1100,8 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
             uint32_t cmask = hmask;
             {
                 const int first = lo - o, end = hi - o;
-                if (base == base0 && first >= 0 && first < kPer) cmask &= ~(1u << first);
-                if (base + kPass >= s1 && end > 0 && end <= kPer) cmask |= 1u << kPer;
+                if (base == base0 && first >= 0 && first < P) cmask &= ~(1u << first);
+                if (base + kPass >= s1 && end > 0 && end <= P) cmask |= 1u << P;
             }
             if ((cmask >> h1) & 1) oc[r_prev] = (T)(run0 + (double)qa);
             if (h2 != h1 && ((cmask >> h2) & 1)) oc[r_first] = (T)v1;
@@ -1014,9 +1110,9 @@ __global__ __launch_bounds__(kThreads, (fwd_min_blocks<T, MODE>())) void forward
                 A q = (A)0;
                 int rank = 0;
 #pragma unroll
-                for (int k = 0; k <= kPer; ++k) {
+                for (int k = 0; k <= P; ++k) {
                     if (k > h3 && ((cmask >> k) & 1)) oc[rows[rank - 1]] = (T)q;
-                    if (k < kPer) {
+                    if (k < P) {
                         const bool h = (hmask >> k) & 1;
                         rank += h;
                         q = (h ? (A)0 : q) + p[k];
@@ -1296,6 +1392,16 @@ static int check_csr(const sphrt_csr* c, int64_t n_chan, int64_t div) {
 #endif
 constexpr size_t kTableLdsMax = SPHRT_TABLE_LDS_MAX;   // dynamic LDS for the staged granules, per workgroup
 
+// Early granule DMA (forward_kernel EDMA) needs whole granules only: no partial last granule.
+// SPHRT_FWD_EDMA=0 at build time keeps the chunk-first order everywhere (A/B studies).
+#ifndef SPHRT_FWD_EDMA
+#define SPHRT_FWD_EDMA 1
+#endif
+static bool early_dma(const sphrt_csr* c) {
+    return SPHRT_FWD_EDMA && table_cols(c) % 4 == 0 &&
+           (size_t)(kGranEarly * kThreads + 1) * 4 * 8 <= kTableLdsMax;
+}
+
 template <typename T>
 static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int64_t chan_stride,
                        int64_t div) {
@@ -1322,7 +1428,8 @@ static int fwd_chunk(const sphrt_csr* c, size_t elem) {
 template <typename T, typename L>
 static int launch_forward(const sphrt_csr* c, const L* len, const T* density, int64_t n_chan,
                           int64_t chan_stride, int64_t div, T* out, int64_t ocs, void* stream) {
-    const dim3 grid((unsigned)c->n_blocks), block(kThreads);
+    constexpr int P = sizeof(T) == 4 ? SPHRT_FWD_P32 : SPHRT_FWD_P64;   // segments per thread
+    const dim3 grid((unsigned)c->n_blocks), block(kPass / P);
     StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     const int chunk = fwd_chunk(c, sizeof(T));
@@ -1334,7 +1441,7 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
     const T* td = sm.on ? (const T*)c->stage : density;      // what the table kernel gathers
     const int64_t tcs = sm.on ? c->stage_cols : chan_stride;
     if (div > 0) {
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic>), grid, block, 0, st,
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic, int32_t, false, P>), grid, block, 0, st,
                            SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0);
     } else if (use_tables(c, td, n_chan, tcs, div)) {
         if (sm.on) {   // natural -> brick layout, every channel
@@ -1346,20 +1453,27 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
                                n_chan, (uint32_t)c->stage_shape[0], sm, c->stage_cols, (T*)c->stage);
             if (int e = check_launch("stage_pack_kernel")) return e;
         }
-        const size_t lds = (size_t)(c->tab_stride + 1) * 4 * sizeof(T);   // + zero granule
-        if (c->tab_bytes == 2)
-            hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, uint16_t>), grid, block, lds, st,
-                               SPHRT_FWD_ARGS(uint16_t, td, tcs, table_cols(c)), 0);
-        else
-            hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, int32_t>), grid, block, lds, st,
-                               SPHRT_FWD_ARGS(int32_t, td, tcs, table_cols(c)), 0);
+        const bool edma = early_dma(c);
+        const size_t lds = (size_t)((edma ? imax64(c->tab_stride, kGranEarly * kThreads)
+                                          : c->tab_stride) + 1) * 4 * sizeof(T);   // + zero granule
+#define SPHRT_FWD_TABLE(TabT, E)                                                                  \
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, TabT, E, P>), grid, block, lds, st,   \
+                           SPHRT_FWD_ARGS(TabT, td, tcs, table_cols(c)), 0)
+        if (c->tab_bytes == 2) {
+            if (edma) SPHRT_FWD_TABLE(uint16_t, true);
+            else SPHRT_FWD_TABLE(uint16_t, false);
+        } else {
+            if (edma) SPHRT_FWD_TABLE(int32_t, true);
+            else SPHRT_FWD_TABLE(int32_t, false);
+        }
+#undef SPHRT_FWD_TABLE
         if (c->n_fallback > 0) {   // (natural vox, natural density)
             if (int e = check_launch("forward_kernel<table>")) return e;
-            hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather>), grid, block, 0, st,
-                               SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 1);
+            hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0,
+                               st, SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 1);
         }
     } else {
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather>), grid, block, 0, st,
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0, st,
                            SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0);
     }
 #undef SPHRT_FWD_ARGS

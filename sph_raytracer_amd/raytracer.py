@@ -274,9 +274,9 @@ except AttributeError:   # pragma: no cover - older torch
 
 
 def _seg_alloc(total):
-    """Per-segment arrays are allocated to a multiple of 8 entries (the apply kernels read whole
-    aligned 8-segment chunks; entries past the total are masked, never used)."""
-    return max((total + 7) // 8 * 8, 8)
+    """Per-segment arrays are allocated to a multiple of 16 entries (the apply kernels read whole
+    aligned 8- or 16-segment chunks; entries past the total are masked, never used)."""
+    return max((total + 15) // 16 * 16, 16)
 
 
 def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
