@@ -236,21 +236,25 @@ def main():
 
     # cold path again in a warm process (the reference's 34k rays/s was also taken after
     # warm-up): new geometry objects + Operator (trace) + first forward
-    colds = []
+    colds, op_colds = [], []
     for _ in range(3):
         barrier()
         t0 = time.perf_counter()
         grid2, geom2 = build_geometry(cfg, rank, world)
+        t1 = time.perf_counter()
         op2 = Operator(grid2, geom2, device=dev, dynamic=grid2.dynamic)
         op2(x)
         torch.cuda.synchronize(dev)
-        colds.append(time.perf_counter() - t0)
+        t2 = time.perf_counter()
+        colds.append(t2 - t0)
+        op_colds.append(t2 - t1)     # the reference's cold: Operator init + first call
         del op2
     t_warm_cold = sorted(colds)[1]
+    t_op_cold = sorted(op_colds)[1]
     if dist is not None:
-        tt = torch.tensor([t_warm_cold], dtype=torch.float64, device=dev)
+        tt = torch.tensor([t_warm_cold, t_op_cold], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_warm_cold = tt.item()
+        t_warm_cold, t_op_cold = tt.tolist()
 
     # drop-in use with host tensors (the reference's device='cpu' default): H2D density, D2H image
     x_host = x.cpu()
@@ -300,9 +304,11 @@ def main():
         'pcie_inclusive': {'rays_per_s': n_rays / t_host, 'ms_per_call': t_host * 1e3,
                            'what': 'op(x) with x and the result in host memory (per rank)'},
         'cold': {'rays_per_s': n_rays * world / t_warm_cold, 'seconds': t_warm_cold,
+                 'operator_rays_per_s': n_rays * world / t_op_cold, 'operator_seconds': t_op_cold,
                  'first_in_process_seconds': t_cold,
                  'what': 'geometry + Operator trace + first forward (median of 3, warm process; '
-                         'first_in_process includes HIP/torch initialisation)'},
+                         'operator_*: Operator init + first forward only, the reference\'s cold '
+                         'definition; first_in_process includes HIP/torch initialisation)'},
         'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                      'achieved_basis': 'algorithmic bytes (SURVEY 8(d): s_y + 4 + S*(4 + s_len + '

@@ -648,9 +648,12 @@ class Operator:
         aligned = d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0)
         table = (c.loc and div == 0 and 0 < c.tab_stride and (c.tab_stride + 1) * 4 * es <= 64 * 1024
                  and (c.stage_shape[0] > 0 or aligned))
-        if table:
-            return f'forward_kernel<{t}, 0, {"unsigned short" if c.tab_bytes == 2 else "int"}>'
-        return f'forward_kernel<{t}, {2 if div else 1}, int>'
+        if table:   # early granule DMA whenever the table columns are whole granules
+            cols = c.stage_cols if c.stage_shape[0] > 0 else c.n_cols
+            edma = 'true' if cols % 4 == 0 else 'false'
+            tabt = 'unsigned short' if c.tab_bytes == 2 else 'int'
+            return f'forward_kernel<{t}, 0, {tabt}, {edma}, 8>'
+        return f'forward_kernel<{t}, {2 if div else 1}, int, false, 8>'
 
     def _apply_forward(self, density):
         with tr.cuda.device(self._cdev):      # launches and allocations on the operator's GPU

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/round
 mkdir -p $OUT
-TAG=${1:-r01}
+TAG=${1:-r02}
 STEPS=${STEPS:-tests,pmc,bench,prof,configs,apply}
 if [[ $STEPS == *tests* ]]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1

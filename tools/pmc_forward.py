@@ -46,7 +46,7 @@ def run_pass(counters, workdir, config, reps, kernel):
     cmd = ['rocprofv3', '--pmc', *counters, '-d', d, '-o', 'pmc', '--output-format', 'csv', '--',
            sys.executable, os.path.join(ROOT, 'tools', 'prof_forward.py'), '--only', '--reps',
            str(reps), '--config', config]
-    subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.DEVNULL)
+    subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.DEVNULL, timeout=90)
     files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
     if not files:
         raise RuntimeError(f'no counter_collection.csv under {d}')
