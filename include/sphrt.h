@@ -122,7 +122,9 @@ int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64
  *     not fit; if it is non-zero the staging is incomplete and the caller runs sphrt_trace_fill
  *     instead of step 3 (the counts are exact either way).
  *  3. after sphrt_scan_counts(counts) -> row_ptr: sphrt_trace_compact moves the rows into the
- *     tight CSR (vox, len: row_ptr[n] entries). */
+ *     tight CSR (vox, len: row_ptr[n] entries).  Either pair (svox, vox) or (slen, len) may be
+ *     NULL to move the other one alone: moving them in two calls, freeing each staging array
+ *     after its call, caps the peak footprint at staging + 12 B per segment. */
 int sphrt_trace_bound(const sphrt_plan *plan, const sphrt_rays *rays, int32_t *bounds,
                       void *workspace, size_t workspace_size, void *stream);
 int sphrt_trace_emit(const sphrt_plan *plan, const sphrt_rays *rays, const int64_t *bound_ptr,

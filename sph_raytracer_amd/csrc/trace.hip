@@ -1190,8 +1190,10 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
 }
 
 // ---- one-pass trace: staging slots -> tight CSR ---------------------------------------------
-// Every wave moves the rows of 64 consecutive rays: lane i reads ray i's slot and row pointers,
-// then the wave copies the rows one after the other (rows average 10-60 segments).
+// Every wave moves the rows of 64 consecutive rays, whose destination is one contiguous range
+// [row_ptr[r0], row_ptr[r0 + 64]): lane i holds ray r0 + i's row pointer and slot, and every lane
+// copies segments lane, lane + 64, ... of the range, finding its ray by a 6-step binary search
+// over the lanes' row pointers — independent loads and stores, no per-row serial loop.
 __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* __restrict__ slot,
                                                       const int64_t* __restrict__ row_ptr,
                                                       const int32_t* __restrict__ svox,
@@ -1203,17 +1205,44 @@ __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* 
     const int64_t nw = (int64_t)gridDim.x * 4;
     for (int64_t r0 = wave * 64; r0 < n; r0 += nw * 64) {
         const int64_t r = r0 + lane;
-        const bool in = r < n;
-        const int64_t a = in ? row_ptr[r] : 0, c = in ? row_ptr[r + 1] - a : 0;
-        const int64_t b = in ? slot[r] : 0;
-        uint64_t todo = __ballot(c > 0);
-        while (todo) {
-            const int i = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const int64_t ai = __shfl(a, i), ci = __shfl(c, i), bi = __shfl(b, i);
-            for (int64_t q = lane; q < ci; q += 64) {
-                vox[ai + q] = svox[bi + q];
-                len[ai + q] = slen[bi + q];
+        const int64_t a = row_ptr[r < n ? r : n];             // rays past n: empty, at the end
+        const int64_t b = r < n ? slot[r] : 0;
+        const int64_t a0 = __shfl(a, 0);
+        const int64_t end = row_ptr[r0 + 64 < n ? r0 + 64 : n];
+        const int32_t rel = (int32_t)(a - a0);                // < 2^31: 64 rows of <= K segments
+        // uniform trip count: every lane takes part in every shuffle (a shuffle from a lane that
+        // left a divergent loop would read nothing); 4 chunks of 64 per step, their loads issued
+        // before any store (one memory round trip per 256 segments, not per 64)
+        const int32_t total = (int32_t)(end - a0);
+        const int64_t dl = b - a;                             // slot - row start of lane's ray
+        for (int32_t q0 = 0; q0 < total; q0 += 256) {
+            int64_t src[4];
+            int32_t vv[4];
+            double ll[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int32_t pos = q0 + 64 * u + lane;
+                int lo = 0;
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1) {
+                    const int32_t x = __shfl(rel, lo + step);
+                    if (x <= pos) lo += step;                 // last lane with rel <= pos
+                }
+                src[u] = a0 + pos + __shfl(dl, lo);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool in = q0 + 64 * u + lane < total;
+                if (vox && in) vv[u] = svox[src[u]];
+                if (len && in) ll[u] = slen[src[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int32_t pos = q0 + 64 * u + lane;
+                if (pos < total) {
+                    if (vox) vox[a0 + pos] = vv[u];
+                    if (len) len[a0 + pos] = ll[u];
+                }
             }
         }
     }
@@ -1363,7 +1392,8 @@ extern "C" int sphrt_trace_compact(int64_t n, const int64_t* bound_ptr, const in
                                    double* len, void* stream) {
     if (n < 0) return fail("negative ray count");
     if (n == 0) return 0;
-    if (!bound_ptr || !svox || !slen || !row_ptr || !vox || !len) return fail("null compact argument");
+    if (!bound_ptr || !row_ptr || (!vox && !len) || (vox && !svox) || (len && !slen))
+        return fail("null compact argument");
     StreamGuard guard(stream);
     const int64_t waves = (n + 63) / 64;
     const int64_t blocks = (waves + 3) / 4 < 8192 ? (waves + 3) / 4 : 8192;

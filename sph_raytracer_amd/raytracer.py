@@ -434,12 +434,18 @@ def _trace_csr(lib, plan, batch, dev, stream):
             scan(counts, row_ptr)
             total, n_over = tr.stack((row_ptr[n], over[0])).tolist()   # host sync 2
             if n_over == 0:
+                del tws, counts, over
+                # vox, then lengths, each staging array freed after its move: peak = staging
+                # + 12 B per segment (the caching allocator reuses svox's block for seg_len)
                 vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+                _lib.check(lib.sphrt_trace_compact(n, _lib.ptr(bound_ptr), _lib.ptr(svox), None,
+                                                   _lib.ptr(row_ptr), _lib.ptr(vox), None,
+                                                   stream), 'sphrt_trace_compact')
+                del svox
                 seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
-                _lib.check(lib.sphrt_trace_compact(n, _lib.ptr(bound_ptr), _lib.ptr(svox),
-                                                   _lib.ptr(slen), _lib.ptr(row_ptr),
-                                                   _lib.ptr(vox), _lib.ptr(seg_len), stream),
-                           'sphrt_trace_compact')
+                _lib.check(lib.sphrt_trace_compact(n, _lib.ptr(bound_ptr), None, _lib.ptr(slen),
+                                                   _lib.ptr(row_ptr), None, _lib.ptr(seg_len),
+                                                   stream), 'sphrt_trace_compact')
                 return row_ptr, vox, seg_len, total
             del svox, slen
             return (row_ptr,) + fill(total) + (total,)
@@ -544,6 +550,7 @@ class Operator:
         n = batch.n
         stream = _lib.stream_of(dev)
         row_ptr, vox, seg_len, total = _trace_csr(lib, self._plan, batch, dev, stream)
+        batch.rays = None        # device ray directions: trace input only (24 B per ray)
         # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
         nblocks = lib.sphrt_csr_blocks(total)
         row_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
