@@ -117,6 +117,18 @@ def test_granule_tables_radix_build(gpu):
     _check_granule_tables(grid, geom, Operator(grid, geom, device=gpu), gpu, tab_bytes=4)
 
 
+def test_granule_tables_partial_last_granule(gpu):
+    """Voxel and ray counts that are not multiples of 4 (the last granule is partial): the table
+    forward / transposed adjoint take the chunk-first order with the partial tail copied lane by
+    lane (no early DMA) and still equal the per-segment gathers bitwise."""
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(6, (23, 29), grid_shape=(21, 17, 23))
+    assert math.prod(grid.shape) % 4 == 3 and math.prod(geom.shape) % 4 == 2
+    op = Operator(grid, geom, device=gpu)
+    assert 'false' in op._forward_kernel_name(tr.rand(grid.shape, device=gpu))
+    _check_granule_tables(grid, geom, op, gpu, tab_bytes=2)
+
+
 def _stage_col(v, shape, brick):
     """Natural voxel -> brick-staged column (apply.hip stage_col), numpy."""
     (nr, ne, na), (br, be, ba) = shape, brick
