@@ -199,6 +199,9 @@ typedef struct sphrt_csr {
     int64_t stage_cols;    /* prod over dims of ceil(shape / brick) * brick */
     void *stage;
     int64_t stage_bytes;
+    /* (optional, sphrt_csr_runs) per block SPHRT_RUN_FIELDS int32: its rows' rays and its share
+     * of the empty rays as ranges; NULL: the forward reads row_ray / empty_ray instead. */
+    const int32_t *runs;
 } sphrt_csr;
 
 int64_t sphrt_csr_blocks(int64_t n_segments);
@@ -223,6 +226,20 @@ int sphrt_csr_local_build(const sphrt_csr *csr, int64_t *blocks, uint16_t *loc, 
                           int64_t *stats, void *stream);
 int sphrt_csr_local_pack(const sphrt_csr *csr, const int64_t *blocks, const void *tab_wide,
                          void *tab, int64_t tab_stride, void *stream);
+/* Row runs (optional).  Block b's rows map to rays in runs of consecutive rays, and its share of
+ * the empty rays (empty_ray[empty_lo .. empty_hi)) to ranges of consecutive rays; when both fit
+ * in SPHRT_MAX_RUNS entries for every block, the table-mode forward takes them from one 128-byte
+ * record per block instead of loading row_ray / empty_ray entries (no dependent row loads, and
+ * the empty rays are zeroed by contiguous stores).  runs: n_blocks x SPHRT_RUN_FIELDS int32
+ *   [0] row runs, [1] empty ranges (-1: more than SPHRT_MAX_RUNS),
+ *   [2 + 2i], [3 + 2i]  run i: first row (relative to the block's row_lo), its ray,
+ *   [16 + 2i], [17 + 2i] empty range i: first ray, ray count.
+ * Writes one device int64 to stats: the number of blocks with more than SPHRT_MAX_RUNS runs or
+ * ranges (the caller sets csr->runs only when it is 0).  Needs row_ray, empty_ray and blocks. */
+#define SPHRT_RUN_FIELDS 32
+#define SPHRT_MAX_RUNS 7
+int sphrt_csr_runs(const sphrt_csr *csr, int32_t *runs, int64_t *stats, void *stream);
+
 /* Time-paired columns for a dynamic operator whose view i sees time slice i (ray r reads slice
  * r / div): vox_out[s] = (r / div) * vol + voxel, head bit kept, for every segment of ray r.  A
  * CSR with these columns (and its own blocks / tables, n_cols = T * vol) is a static CSR over the

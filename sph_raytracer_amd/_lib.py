@@ -41,13 +41,15 @@ class CSR(ctypes.Structure):
                 ('n_fallback', c_i64), ('empty_ray', c_vp), ('tab_stride', c_i64),
                 ('tab_bytes', c_i64), ('stage_shape', ctypes.c_int32 * 3),
                 ('stage_brick', ctypes.c_int32 * 3), ('stage_cols', c_i64), ('stage', c_vp),
-                ('stage_bytes', c_i64)]
+                ('stage_bytes', c_i64), ('runs', c_vp)]
 
 
 ROW_HEAD = 0x80000000
 BLOCK_FIELDS = 6           # SPHRT_BLOCK_FIELDS
 LOC_HEAD = 0x8000          # SPHRT_LOC_HEAD
 TAB_WIDE = 2048            # SPHRT_TAB_WIDE
+RUN_FIELDS = 32            # SPHRT_RUN_FIELDS
+MAX_RUNS = 7               # SPHRT_MAX_RUNS
 
 # (name, restype, argtypes) — mirrors include/sphrt.h one to one
 _SIGNATURES = [
@@ -73,6 +75,7 @@ _SIGNATURES = [
     ('sphrt_csr_blocks', c_i64, [c_i64]),
     ('sphrt_csr_index_workspace_bytes', ctypes.c_size_t, [c_i64]),
     ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    ('sphrt_csr_runs', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp]),
     ('sphrt_csr_local_count', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp]),
     ('sphrt_csr_local_fill', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp]),
     ('sphrt_csr_local_build', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_vp, c_vp]),

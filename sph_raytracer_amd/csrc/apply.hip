@@ -127,6 +127,66 @@ __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
     m[5] = -1;                                  // no granule table until sphrt_csr_local
 }
 
+// Row runs and empty ranges of block b (sphrt_csr_runs): one thread per block walks its rows'
+// rays (row_ray[k0 .. k1)) and its share of the empty list, splitting both where the ray ids stop
+// being consecutive.  More than kMaxRuns of either -> -1 and the block counts in stats.
+constexpr int kRunFields = SPHRT_RUN_FIELDS;
+constexpr int kMaxRuns = SPHRT_MAX_RUNS;
+constexpr int kRunEmpty = 2 + 2 * kMaxRuns;           // first empty-range field
+static_assert(kRunEmpty + 2 * kMaxRuns <= kRunFields, "run record layout");
+
+__global__ __launch_bounds__(256) void block_runs_kernel(const int64_t* __restrict__ blocks,
+                                                         const int32_t* __restrict__ row_ray,
+                                                         const int32_t* __restrict__ empty_ray,
+                                                         int64_t n_rays, int64_t nblocks,
+                                                         int32_t* __restrict__ runs,
+                                                         unsigned long long* stats) {
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= nblocks) return;
+    const int64_t* m = blocks + kBlockFields * b;
+    const int64_t n_rows = n_rays - blocks[kBlockFields * (nblocks - 1) + 1];   // all rows
+    const int64_t k0 = m[4];
+    const int64_t k1 = b + 1 < nblocks ? blocks[kBlockFields * (b + 1) + 4] : n_rows;
+    int32_t* r = runs + kRunFields * b;
+    bool over = false;
+    int n = 0;
+    for (int64_t k = k0; k < k1 && !over; ++k) {
+        const int32_t ray = row_ray[k];
+        if (k == k0 || ray != row_ray[k - 1] + 1) {
+            if (n == kMaxRuns) { over = true; break; }
+            r[2 + 2 * n] = (int32_t)(k - k0);
+            r[3 + 2 * n] = ray;
+            ++n;
+        }
+    }
+    r[0] = over ? -1 : n;
+    bool over_e = false;
+    int ne = 0;
+    int32_t start = 0, cnt = 0;
+    for (int64_t j = m[0]; j < m[1]; ++j) {
+        const int32_t ray = empty_ray[j];
+        if (cnt > 0 && ray == start + cnt) { ++cnt; continue; }
+        if (cnt > 0) {
+            if (ne == kMaxRuns) { over_e = true; break; }
+            r[kRunEmpty + 2 * ne] = start;
+            r[kRunEmpty + 2 * ne + 1] = cnt;
+            ++ne;
+        }
+        start = ray;
+        cnt = 1;
+    }
+    if (!over_e && cnt > 0) {
+        if (ne == kMaxRuns) over_e = true;
+        else {
+            r[kRunEmpty + 2 * ne] = start;
+            r[kRunEmpty + 2 * ne + 1] = cnt;
+            ++ne;
+        }
+    }
+    r[1] = over_e ? -1 : ne;
+    if (over || over_e) atomicAdd(stats, 1ull);
+}
+
 // ---- block-level scans (256 threads = 4 waves) -----------------------------------------------
 struct ScanShared {
     int cnt[4];
@@ -653,10 +713,15 @@ __device__ __forceinline__ T lds_at(const T* dens, uint32_t x) {
 
 // One DMA lane: granule g (its index in the channel; the byte offset is 32-bit: volumes under
 // 4 GiB per channel), into the round whose first table entry is e0.
+// SPHRT_FWD_ABL_GRAN=m (diagnostic builds only, wrong results): granule indices masked with m, so
+// the DMA reads a volume of (m+1) granules — the forward without density misses.
 template <typename T>
 __device__ __forceinline__ void stage_one(const T* __restrict__ rho, int32_t g, int e0, int lane,
                                           T* dens) {
     constexpr int G = kGranLanes<T>;
+#ifdef SPHRT_FWD_ABL_GRAN
+    g &= SPHRT_FWD_ABL_GRAN;
+#endif
     const char* src = reinterpret_cast<const char*>(rho) + (uint32_t)g * (16u * G) +
                       16 * (lane % G);
     __builtin_amdgcn_global_load_lds((const void*)src,
@@ -748,6 +813,20 @@ __device__ __forceinline__ void stage_granules_early(const T* __restrict__ rho,
     }
 }
 
+// Segment-stream loads (read once per launch).  SPHRT_FWD_NT=1: non-temporal (A/B study).
+#ifndef SPHRT_FWD_NT
+#define SPHRT_FWD_NT 0
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 stream_load(const uint4* p) {
+    if constexpr (SPHRT_FWD_NT) {
+        const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+
 // Segment lengths of one chunk of P segments as aligned 16-byte vectors.
 template <typename L, int P>
 __device__ __forceinline__ void load_lens(const L* __restrict__ len, L (&l)[P]) {
@@ -755,7 +834,7 @@ __device__ __forceinline__ void load_lens(const L* __restrict__ len, L (&l)[P]) 
     const uint4* lp = reinterpret_cast<const uint4*>(len);
 #pragma unroll
     for (int k = 0; k < P / E; ++k) {
-        const uint4 f = lp[k];
+        const uint4 f = stream_load(lp + k);
         const uint32_t w[4] = {f.x, f.y, f.z, f.w};
         if constexpr (sizeof(L) == 4) {
 #pragma unroll
@@ -786,7 +865,7 @@ __device__ __forceinline__ void raw_load(const int32_t* __restrict__ vox,
     const uint4* ip = LOCAL ? reinterpret_cast<const uint4*>(loc + a)
                             : reinterpret_cast<const uint4*>(vox + a);
 #pragma unroll
-    for (int k = 0; k < (LOCAL ? P / 8 : P / 4); ++k) r.ix[k] = ip[k];
+    for (int k = 0; k < (LOCAL ? P / 8 : P / 4); ++k) r.ix[k] = stream_load(ip + k);
     load_lens<L, P>(len + a, r.l);
 }
 
@@ -898,15 +977,18 @@ constexpr int fwd_min_blocks() {
 template <typename T>
 using AccumOf = typename std::conditional<sizeof(T) == 4, float, double>::type;
 
+// RUNS (table mode, sphrt_csr.runs set): the rows' rays and the empty rays come from the block's
+// run record (one dword per lane, loaded with the table entries) instead of row_ray / empty_ray.
 template <typename T, typename L, int MODE, typename TabT = int32_t, bool EDMA = false,
-          int P = kPer>
+          int P = kPer, bool RUNS = false>
 __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_kernel(
     const int64_t* __restrict__ blocks, const int32_t* __restrict__ vox,
     const uint16_t* __restrict__ loc, const TabT* __restrict__ tab, const L* __restrict__ len,
     const int32_t* __restrict__ row_ray, const int32_t* __restrict__ empty_ray,
     const T* __restrict__ density, int64_t n_chan, int64_t cs, int64_t div, T* __restrict__ out,
     int64_t ocs, int64_t n_rays, int64_t n_seg, int64_t n_cols, int64_t tab_stride,
-    int xcd_chunk, int fallback_only) {
+    int xcd_chunk, int fallback_only, const int32_t* __restrict__ runs) {
+    static_assert(!RUNS || MODE == kFwdTable, "run records serve the table mode");
     __shared__ FwdShared sh;
     extern __shared__ __attribute__((aligned(16))) unsigned char fwd_dyn_lds[];
     T* dens = reinterpret_cast<T*>(fwd_dyn_lds);   // 4 * tab_stride entries (table mode)
@@ -937,6 +1019,10 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
         for (int r = 0; r < kEarlyRounds<T, THR>; ++r)
             ti[r] = (int32_t)tab_b[gran_entry0<T, THR>(r, w) + (tid & 63) / kGranLanes<T>];
     }
+    // the run record goes out with the table entries, before the chunk (the early-DMA wait below
+    // counts only the loads issued after the chunk; issued after the chunk it measured the same)
+    int32_t rrec = 0;
+    if constexpr (RUNS) rrec = runs[blk * kRunFields + (tid & 31)];
     // early DMA: the table entries first, so waiting for them does not wait for the chunk
     if (EDMA) raw_load<L, local, P>(vox, loc, len, imin64(base0 + o, last_chunk * P), raw);
     __builtin_amdgcn_sched_barrier(0);
@@ -948,11 +1034,41 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     // Empty rays integrate to zero: this workgroup's share of the list is fetched now and
     // written at the very end, off the critical path.
     const int64_t e_lo = m[0];
-    const int e_n = fallback_only ? 0 : (int)(m[1] - e_lo);
+#ifdef SPHRT_FWD_ABL_EMPTY
+    const int e_n = 0;
+#else
+    const int e_n = (fallback_only || RUNS) ? 0 : (int)(m[1] - e_lo);
+#endif
     // (unconditional load: empty_ray holds n_rays + 1 entries; a predicated load would make
     // the wait-count model drain every load before the granule DMA)
-    int32_t r_empty = empty_ray[e_lo + min(tid, max(e_n - 1, 0))];
+#ifdef SPHRT_FWD_ABL_EMPTY   // diagnostic builds only: no empty-ray zeroing (wrong results)
+    constexpr int kEmptyLoads = 0;
+    int32_t r_empty = 0;
+#else
+    constexpr int kEmptyLoads = RUNS ? 0 : 1;
+    int32_t r_empty = 0;
+    if constexpr (!RUNS) r_empty = empty_ray[e_lo + min(tid, max(e_n - 1, 0))];
+#endif
     auto zero_empty = [&]() {
+        if constexpr (RUNS) {      // empty j of the share -> its ray through the ranges
+            const int ne = __builtin_amdgcn_readlane(rrec, 1);
+            int e_tot = 0;
+            for (int i = 0; i < ne; ++i) e_tot += __builtin_amdgcn_readlane(rrec, kRunEmpty + 2 * i + 1);
+            for (int j = tid; j < e_tot; j += THR) {   // (one round for shares of <= 256)
+                int rem = j;
+                int32_t ray = 0;
+                for (int i = 0; i < ne; ++i) {
+                    const int32_t r0 = __builtin_amdgcn_readlane(rrec, kRunEmpty + 2 * i);
+                    const int cnt = __builtin_amdgcn_readlane(rrec, kRunEmpty + 2 * i + 1);
+                    ray = (rem >= 0 && rem < cnt) ? r0 + rem : ray;
+                    rem -= cnt;
+                }
+                if (nc == 1) out[ray] = (T)0;
+                else
+                    for (int64_t c = 0; c < nc; ++c) out[c * ocs + ray] = (T)0;
+            }
+            return;
+        }
         asm volatile("" : "+v"(r_empty));     // keep every use (and its wait) down here
         if (tid < e_n)
             for (int64_t c = 0; c < nc; ++c) out[c * ocs + r_empty] = (T)0;
@@ -961,7 +1077,11 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             for (int64_t c = 0; c < nc; ++c) out[c * ocs + r] = (T)0;
         }
     };
-    if (s0 >= s1) {
+    // A block without rows (or left to the fallback launch) zeroes its empty share and leaves.
+    // With run records the table kernel runs on instead (its passes are skipped): as a separate
+    // exit path, the compiler sank the table-entry and chunk loads below the block record's
+    // arrival, serialising one more round trip in front of every workgroup.
+    if (!RUNS && s0 >= s1) {
         zero_empty();
         return;
     }
@@ -981,7 +1101,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
         // Loads complete in issue order: the chunk is in once at most the empty-list load and the
         // early DMAs issued after it are outstanding.  Said explicitly: the compiler's model
         // treats LDS-DMA as another event type and would wait for every DMA (vmcnt(0)).
-        constexpr int after = 1 + kEarlyRounds<T, THR>;
+        constexpr int after = kEmptyLoads + kEarlyRounds<T, THR>;
         static_assert(after < 16, "vmcnt field");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt((after & 15) | (7 << 4) | (15 << 8));
@@ -1037,10 +1157,45 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             // unconditional loads (clamped into row_ray's n_rays entries): no branch, so nothing
             // waits for them before the first store
             const int64_t ri = k0 + rbase + hb;
-            const int32_t r_prev = row_ray[imax64(ri - 1, 0)];
-            const int32_t r_first = row_ray[imin64(ri, n_rays - 1)];
-            const int32_t r_second = row_ray[imin64(ri + 1, n_rays - 1)];
+            // RUNS: the ray of block-relative row q from the record's runs (run 0 starts at row 0)
+            const int qb = (int)(rbase + hb);
+            auto ray_of_row = [&](int q) -> int32_t {
+                int32_t r = __builtin_amdgcn_readlane(rrec, 3) + q;
+                const int nr = __builtin_amdgcn_readlane(rrec, 0);
+                for (int i = 1; i < nr; ++i) {
+                    const int off = __builtin_amdgcn_readlane(rrec, 2 + 2 * i);
+                    const int32_t ray = __builtin_amdgcn_readlane(rrec, 3 + 2 * i);
+                    r = q >= off ? ray + (q - off) : r;
+                }
+                return r;
+            };
+            int32_t r_prev, r_first, r_second;
+#ifdef SPHRT_FWD_ABL_ROWS    // diagnostic builds only: rows' rays without loads (wrong results)
+            r_prev = (int32_t)imax64(ri - 1, 0);
+            r_first = (int32_t)imin64(ri, n_rays - 1);
+            r_second = (int32_t)imin64(ri + 1, n_rays - 1);
+#else
+            if constexpr (RUNS) {
+                const int32_t r0 = __builtin_amdgcn_readlane(rrec, 3);
+                r_prev = r0 + qb - 1;
+                r_first = r0 + qb;
+                r_second = r0 + qb + 1;
+                const int nr = __builtin_amdgcn_readlane(rrec, 0);
+                for (int i = 1; i < nr; ++i) {   // uniform: usually 1 or 2 runs
+                    const int off = __builtin_amdgcn_readlane(rrec, 2 + 2 * i);
+                    const int32_t d = __builtin_amdgcn_readlane(rrec, 3 + 2 * i) - off;
+                    r_prev = qb - 1 >= off ? d + qb - 1 : r_prev;
+                    r_first = qb >= off ? d + qb : r_first;
+                    r_second = qb + 1 >= off ? d + qb + 1 : r_second;
+                }
+            } else {
+                r_prev = row_ray[imax64(ri - 1, 0)];
+                r_first = row_ray[imin64(ri, n_rays - 1)];
+                r_second = row_ray[imin64(ri + 1, n_rays - 1)];
+            }
+#endif
             auto row_of = [&](int i) -> int64_t {     // ray of the row after i own heads
+                if constexpr (RUNS) return i < 0 ? r_prev : i == 0 ? r_first : ray_of_row(qb + i);
                 return i < 0 ? r_prev : i == 0 ? r_first : rows[i];
             };
             if constexpr (local) {
@@ -1111,7 +1266,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
                 int rank = 0;
 #pragma unroll
                 for (int k = 0; k <= P; ++k) {
-                    if (k > h3 && ((cmask >> k) & 1)) oc[rows[rank - 1]] = (T)q;
+                    if (k > h3 && ((cmask >> k) & 1)) oc[row_of(rank - 1)] = (T)q;
                     if (k < P) {
                         const bool h = (hmask >> k) & 1;
                         rank += h;
@@ -1237,6 +1392,22 @@ extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* 
     hipLaunchKernelGGL(block_meta_kernel, dim3((unsigned)((n_blocks + 255) / 256)), dim3(256), 0,
                        st, row_ptr, pre, n_rays, n_blocks, blocks);
     return check_launch("block_meta");
+}
+
+extern "C" int sphrt_csr_runs(const sphrt_csr* c, int32_t* runs, int64_t* stats, void* stream) {
+    if (!c || !c->row_ray || !c->empty_ray || !c->blocks || !runs || !stats)
+        return fail("incomplete CSR for the run records");
+    if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
+    if (c->n_rays > 0x7fffffff) return fail("run records need ray ids < 2^31");
+    StreamGuard guard(stream);
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(stats, 0, sizeof(int64_t), st) != hipSuccess)
+        return fail("hipMemsetAsync failed");
+    if (c->n_rays == 0) return 0;
+    hipLaunchKernelGGL(block_runs_kernel, dim3((unsigned)((c->n_blocks + 255) / 256)), dim3(256),
+                       0, st, c->blocks, c->row_ray, c->empty_ray, c->n_rays, c->n_blocks, runs,
+                       (unsigned long long*)stats);
+    return check_launch("block_runs");
 }
 
 #ifdef SPHRT_FWD_STAMPS
@@ -1442,7 +1613,7 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
     const int64_t tcs = sm.on ? c->stage_cols : chan_stride;
     if (div > 0) {
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic, int32_t, false, P>), grid, block, 0, st,
-                           SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0);
+                           SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, nullptr);
     } else if (use_tables(c, td, n_chan, tcs, div)) {
         if (sm.on) {   // natural -> brick layout, every channel
             if (!c->stage || (int64_t)sizeof(T) * n_chan * c->stage_cols > c->stage_bytes)
@@ -1454,27 +1625,35 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
             if (int e = check_launch("stage_pack_kernel")) return e;
         }
         const bool edma = early_dma(c);
-        const size_t lds = (size_t)((edma ? imax64(c->tab_stride, kGranEarly * kThreads)
-                                          : c->tab_stride) + 1) * 4 * sizeof(T);   // + zero granule
-#define SPHRT_FWD_TABLE(TabT, E)                                                                  \
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, TabT, E, P>), grid, block, lds, st,   \
-                           SPHRT_FWD_ARGS(TabT, td, tcs, table_cols(c)), 0)
+        size_t lds = (size_t)((edma ? imax64(c->tab_stride, kGranEarly * kThreads)
+                                    : c->tab_stride) + 1) * 4 * sizeof(T);   // + zero granule
+#ifdef SPHRT_FWD_LDS_MIN
+        lds = lds < (size_t)SPHRT_FWD_LDS_MIN ? (size_t)SPHRT_FWD_LDS_MIN : lds;
+#endif
+#define SPHRT_FWD_TABLE(TabT, E, R)                                                               \
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, TabT, E, P, R>), grid, block, lds,    \
+                           st, SPHRT_FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
+#define SPHRT_FWD_TABLE_R(TabT, E)                                                                \
+        if (c->runs) SPHRT_FWD_TABLE(TabT, E, true);                                              \
+        else SPHRT_FWD_TABLE(TabT, E, false)
         if (c->tab_bytes == 2) {
-            if (edma) SPHRT_FWD_TABLE(uint16_t, true);
-            else SPHRT_FWD_TABLE(uint16_t, false);
+            if (edma) SPHRT_FWD_TABLE_R(uint16_t, true);
+            else SPHRT_FWD_TABLE_R(uint16_t, false);
         } else {
-            if (edma) SPHRT_FWD_TABLE(int32_t, true);
-            else SPHRT_FWD_TABLE(int32_t, false);
+            if (edma) SPHRT_FWD_TABLE_R(int32_t, true);
+            else SPHRT_FWD_TABLE_R(int32_t, false);
         }
+#undef SPHRT_FWD_TABLE_R
 #undef SPHRT_FWD_TABLE
         if (c->n_fallback > 0) {   // (natural vox, natural density)
             if (int e = check_launch("forward_kernel<table>")) return e;
             hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0,
-                               st, SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 1);
+                               st, SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 1,
+                               nullptr);
         }
     } else {
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0, st,
-                           SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0);
+                           SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, nullptr);
     }
 #undef SPHRT_FWD_ARGS
     return check_launch(sizeof(T) == 4 ? "forward_kernel<f32>" : "forward_kernel<f64>");

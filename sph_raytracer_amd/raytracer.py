@@ -280,11 +280,28 @@ def _seg_alloc(total):
 
 
 def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
-    """Per-workgroup granule tables of a CSR; sets desc.loc/.tab/.tab_stride/.n_fallback.  One
-    host sync (the largest table decides the stride).  One pass (sphrt_csr_local_build into
-    SPHRT_TAB_WIDE-strided tables, then _pack to the stride) unless the wide tables would not fit
-    comfortably in free memory or SPHRT_TABLES=twopass (sphrt_csr_local_count, then _fill)."""
-    stats = tr.empty(2, dtype=tr.int64, device=dev)
+    """Per-workgroup granule tables and run records of a CSR; sets desc.loc/.tab/.tab_stride/
+    .n_fallback/.runs and returns (loc, tab, runs).  One host sync (the largest table decides
+    the stride; the run-record overflow count decides desc.runs).  One pass
+    (sphrt_csr_local_build into SPHRT_TAB_WIDE-strided tables, then _pack to the stride) unless
+    the wide tables would not fit comfortably in free memory or SPHRT_TABLES=twopass
+    (sphrt_csr_local_count, then _fill).  Run records (sphrt_csr_runs) replace the forward's
+    row_ray / empty_ray loads in grids of more than one wave of workgroups (SPHRT_RUNS=auto;
+    =on: every grid, =off: none).  Measured on MI355X (forward / transposed adjoint, us): C3 f32
+    234.4 -> 227.6 / 226.4 -> 225.2, f64 370.3 -> 360.5 / 317.5 -> 305.0; C5 f32 34.8 -> 34.1,
+    f64 63.8 -> 63.3; but the single-wave C2 f32 forward 6.90 -> 7.06 (its dependent loads are
+    hidden under the one wave's latency chain), so single-wave grids keep the loads."""
+    stats = tr.empty(3, dtype=tr.int64, device=dev)
+    desc.runs = None
+    runs = None
+    mode = os.environ.get('SPHRT_RUNS', 'auto')
+    want = mode == 'on' or (mode == 'auto' and nblocks > _SINGLE_WAVE_BLOCKS)
+    if want and desc.n_rays < 2 ** 31:
+        runs = tr.empty(_lib.RUN_FIELDS * nblocks, dtype=tr.int32, device=dev)
+        _lib.check(lib.sphrt_csr_runs(desc, _lib.ptr(runs), _lib.ptr(stats[2:]), stream),
+                   'sphrt_csr_runs')
+    else:
+        stats[2:].fill_(1)
     loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
     # 16-bit entries when every granule index fits (<= 2^18 columns): half the table bytes the
     # forward streams
@@ -301,7 +318,9 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
     else:
         _lib.check(lib.sphrt_csr_local_count(desc, _lib.ptr(blocks), _lib.ptr(stats), stream),
                    'sphrt_csr_local_count')
-    n_fallback, max_tab = stats.tolist()
+    n_fallback, max_tab, runs_over = stats.tolist()
+    if runs_over:
+        runs = None
     stride = max(64, (max_tab + 63) // 64 * 64)
     tab = tr.empty(nblocks * stride + 3 * 256, dtype=tdt, device=dev)   # + early-fetch pad
     if one_pass:
@@ -313,10 +332,12 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
                                             stride, stream), 'sphrt_csr_local_fill')
     desc.n_fallback, desc.tab_stride = n_fallback, stride
     desc.loc, desc.tab = loc.data_ptr(), tab.data_ptr()
-    return loc, tab
+    desc.runs = runs.data_ptr() if runs is not None else None
+    return loc, tab, runs
 
 
 _BRICK = (2, 4, 4)   # (r, e, a) voxels per staging brick: 32 = one 128-byte float line
+_SINGLE_WAVE_BLOCKS = 256 * 6   # forward workgroups resident at once (256 CUs x 6)
 
 
 # Transposed CSRs (columns = rays) are not staged by default: detector tiles of (1, 4, 8) rays
@@ -338,7 +359,7 @@ def _stage_brick(nblocks, env_name='SPHRT_BRICK', brick=_BRICK):
         return None
     if env != 'auto':
         return tuple(int(v) for v in env.split(','))
-    return brick if brick is not None and nblocks > 256 * 6 else None
+    return brick if brick is not None and nblocks > _SINGLE_WAVE_BLOCKS else None
 
 
 def _set_stage(desc, shape, brick):
@@ -569,10 +590,10 @@ class Operator:
         c.n_cols = math.prod(self.grid.shape[-3:])
         shape3 = tuple(int(v) for v in self.grid.shape[-3:])
         _set_stage(c, shape3, _stage_brick(nblocks))
-        loc, tab = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
+        loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
         self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, row_ray=row_ray,
-                         empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, nblocks=nblocks,
-                         n=n, total=total, desc=c)
+                         empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, runs=runs,
+                         nblocks=nblocks, n=n, total=total, desc=c)
         self._batch = batch
 
     # -- shape logic of raytracer.py:703-712 -----------------------------------------------------
@@ -659,8 +680,9 @@ class Operator:
             cols = c.stage_cols if c.stage_shape[0] > 0 else c.n_cols
             edma = 'true' if cols % 4 == 0 else 'false'
             tabt = 'unsigned short' if c.tab_bytes == 2 else 'int'
-            return f'forward_kernel<{t}, 0, {tabt}, {edma}, 8>'
-        return f'forward_kernel<{t}, {2 if div else 1}, int, false, 8>'
+            runs = 'true' if c.runs else 'false'
+            return f'forward_kernel<{t}, 0, {tabt}, {edma}, 8, {runs}>'
+        return f'forward_kernel<{t}, {2 if div else 1}, int, false, 8, false>'
 
     def _apply_forward(self, density):
         with tr.cuda.device(self._cdev):      # launches and allocations on the operator's GPU
@@ -754,9 +776,9 @@ class Operator:
         shape3 = self._ray_shape3()
         _set_stage(c, shape3, _stage_brick(nblocks, 'SPHRT_BRICK_T', _BRICK_RAYS)
                    if shape3 else None)
-        loc, tab = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
+        loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
         return dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, empty_vox, blocks,
-                                  loc, tab))
+                                  loc, tab, runs))
 
     def _paired(self, T, div):
         """The trace with time-paired columns (ray r reads slice r // div: column
@@ -782,8 +804,8 @@ class Operator:
         _clear_stage(c)                             # time-paired columns are not bricked
         c.vox, c.blocks, c.n_cols = vox_p.data_ptr(), blocks_p.data_ptr(), T * vol
         c.loc, c.tab, c.tab_stride, c.n_fallback = None, None, 0, 0
-        loc, tab = _local_tables(lib, c, blocks_p, nblocks, total, dev, stream)
-        csr[key] = dict(desc=c, keep=(vox_p, blocks_p, loc, tab), n_t=T)
+        loc, tab, runs = _local_tables(lib, c, blocks_p, nblocks, total, dev, stream)
+        csr[key] = dict(desc=c, keep=(vox_p, blocks_p, loc, tab, runs), n_t=T)
         return csr[key]
 
     def _apply_adjoint(self, y, dshape, ddtype, ddevice):

@@ -125,7 +125,7 @@ def test_granule_tables_partial_last_granule(gpu):
     grid, geom = _orbit(6, (23, 29), grid_shape=(21, 17, 23))
     assert math.prod(grid.shape) % 4 == 3 and math.prod(geom.shape) % 4 == 2
     op = Operator(grid, geom, device=gpu)
-    assert 'false' in op._forward_kernel_name(tr.rand(grid.shape, device=gpu))
+    assert ', false, 8,' in op._forward_kernel_name(tr.rand(grid.shape, device=gpu))
     _check_granule_tables(grid, geom, op, gpu, tab_bytes=2)
 
 
@@ -616,3 +616,99 @@ def test_onepass_tables_equal_twopass(grid_shape, staged, gpu, monkeypatch):
     for b in range(len(n_tab)):      # entries past n_tab are unused (uninitialised)
         k = int(n_tab[b])
         assert tr.equal(t0[b * s0:b * s0 + k], t1[b * s1:b * s1 + k])
+
+
+def _expected_runs(csr, n_blocks_fields):
+    """Host restatement of block_runs_kernel: per block, the runs of consecutive rays of its rows
+    and of its share of the empty list (None for more than MAX_RUNS)."""
+    from sph_raytracer_amd import _lib
+    blocks = csr['blocks'].cpu().numpy().reshape(-1, n_blocks_fields)
+    row_ray = csr['row_ray'].cpu().numpy()
+    empty = csr['empty_ray'].cpu().numpy()
+    n_rows = csr['n'] - blocks[-1, 1]
+
+    def runs(v):
+        if len(v) == 0:
+            return []
+        cut = np.nonzero(np.diff(v) != 1)[0] + 1
+        starts = np.concatenate(([0], cut))
+        ends = np.concatenate((cut, [len(v)]))
+        return [(int(a), int(v[a]), int(b - a)) for a, b in zip(starts, ends)]
+
+    out = []
+    for b in range(len(blocks)):
+        k0 = blocks[b, 4]
+        k1 = blocks[b + 1, 4] if b + 1 < len(blocks) else n_rows
+        rr = runs(row_ray[k0:k1])
+        er = runs(empty[blocks[b, 0]:blocks[b, 1]])
+        out.append((rr if len(rr) <= _lib.MAX_RUNS else None,
+                    er if len(er) <= _lib.MAX_RUNS else None))
+    return out
+
+
+def test_run_records(c2, gpu, monkeypatch):
+    """Row runs / empty ranges (sphrt_csr_runs, forced on at C2): the records equal a numpy
+    restatement on the C2 trace and its transpose, the forward and the transposed adjoint with records equal the ones
+    reading row_ray / empty_ray bitwise (f32, f64, 3 channels), and a trace whose rows are too
+    fragmented for the records (random rays, every other one missing) leaves desc.runs unset and
+    still matches the oracle."""
+    from sph_raytracer_amd import Operator, ViewGeom, _lib
+    grid, geom, op_auto = c2
+    assert not op_auto._csr['desc'].runs       # auto: a single-wave grid keeps the loads
+    monkeypatch.setenv('SPHRT_RUNS', 'on')
+    op = Operator(grid, geom, device=gpu)
+    for csr in (op._csr, dict(op._transposed(), n=math.prod(grid.shape))):
+        if 'keep' in csr:      # transposed: row_ptr, t_ray, len, len32, vox_list, empty, blocks..
+            k = csr['keep']
+            csr = dict(n=csr['n'], blocks=k[6], row_ray=k[4], empty_ray=k[5], runs=k[9],
+                       desc=csr['desc'])
+        assert csr['desc'].runs, 'run records expected at C2'
+        rec = csr['runs'].cpu().numpy().reshape(-1, _lib.RUN_FIELDS)
+        for b, (rr, er) in enumerate(_expected_runs(csr, _lib.BLOCK_FIELDS)):
+            assert rr is not None and er is not None
+            assert rec[b, 0] == len(rr) and rec[b, 1] == len(er)
+            for i, (off, ray, _) in enumerate(rr):
+                assert (rec[b, 2 + 2 * i], rec[b, 3 + 2 * i]) == (off, ray)
+            for i, (_, ray, cnt) in enumerate(er):
+                assert (rec[b, 16 + 2 * i], rec[b, 17 + 2 * i]) == (ray, cnt)
+    g = tr.Generator(device=gpu).manual_seed(11)
+    descs = [op._csr['desc'], op._transposed()['desc']]
+    for dt in (tr.float32, tr.float64):
+        x = tr.rand((3,) + tuple(grid.shape), dtype=dt, device=gpu, generator=g)
+        y = tr.rand(geom.shape, dtype=dt, device=gpu, generator=g)
+        a, at = op(x), op.T(y)
+        assert tr.equal(op_auto(x), a) and tr.equal(op_auto.T(y), at)
+        saved = [d.runs for d in descs]
+        try:
+            for d in descs:
+                d.runs = None
+            op._fast.clear()
+            op._fastc = None
+            assert tr.equal(op(x), a) and tr.equal(op.T(y), at)
+        finally:
+            for d, r in zip(descs, saved):
+                d.runs = r
+            op._fast.clear()
+            op._fastc = None
+    # fragmented rows: random directions from inside the grid's bounding box, half of them
+    # pointed away from a tiny grid -> more than MAX_RUNS runs per block
+    rng = np.random.default_rng(5)
+    n = 40000
+    d = rng.normal(size=(n, 3))
+    d[1::2] = np.array([0.0, 0.0, 1.0])                     # every other ray: straight up ...
+    xs = np.tile(np.array([0.0, 0.0, 3.0]), (n, 1))          # ... from above the grid: misses
+    xs[0::2] = rng.uniform(-0.4, 0.4, size=(n // 2, 3))      # the others start inside
+    geom_f = ViewGeom(tr.from_numpy(xs), tr.from_numpy(d))
+    from sph_raytracer_amd import SphericalGrid
+    grid_f = SphericalGrid(shape=(6, 5, 8))
+    op_f = Operator(grid_f, geom_f, device=gpu)
+    assert not op_f._csr['desc'].runs
+    xf = tr.rand(grid_f.shape, dtype=tr.float64, device=gpu, generator=g)
+    yf = op_f(xf).cpu().numpy().reshape(-1)
+    from oracle import oracle
+    from sph_raytracer_amd.raytracer import find_starts
+    og = oracle.Grid.from_boundaries(grid_f.r_b.numpy(), grid_f.e_b.numpy(), grid_f.a_b.numpy())
+    ptr, vox, seg = oracle.trace_segments(og, geom_f.ray_starts.numpy(), geom_f.rays.numpy(),
+                                          find_starts(grid_f, geom_f.ray_starts).numpy())
+    ref = oracle.forward(ptr, vox, seg, xf.cpu().numpy(), math.prod(grid_f.shape))[0]
+    assert np.allclose(yf, ref, rtol=1e-10, atol=1e-12)
