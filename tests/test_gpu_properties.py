@@ -712,3 +712,41 @@ def test_run_records(c2, gpu, monkeypatch):
                                           find_starts(grid_f, geom_f.ray_starts).numpy())
     ref = oracle.forward(ptr, vox, seg, xf.cpu().numpy(), math.prod(grid_f.shape))[0]
     assert np.allclose(yf, ref, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize('lams, meas_dtype', [((1, 1), tr.float64), ((0.5, 2), tr.float64),
+                                              ((1, None), tr.float32)])
+def test_gd_direct_matches_autograd(lams, meas_dtype, gpu, monkeypatch):
+    """The static_retrieval.py loop without autograd (retrieval._gd_direct: forward, residual,
+    adjoint, -lam/N on negative voxels, Adam) gives the autograd loop's iterates bitwise: the
+    same loss history, coefficients and reconstruction, for unit and non-unit weights, with and
+    without the regulariser, and a float32 measurement."""
+    from sph_raytracer_amd import Operator, retrieval
+    from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
+    from sph_raytracer_amd.model import FullyDenseModel
+    grid, geom = _orbit(12, (20, 16), kind='circ', grid_shape=(16, 16, 16))
+    x = tr.zeros(grid.shape, dtype=tr.float64, device=gpu)
+    x[:, 8:, :8] = 1
+    x[:, :8, 8:] = 1
+    op = Operator(grid, geom, device=gpu)
+    meas = op(x).to(meas_dtype)
+    calls = []
+    direct = retrieval._gd_direct
+
+    def spy(*a, **k):
+        calls.append(1)
+        return direct(*a, **k)
+
+    monkeypatch.setattr(retrieval, '_gd_direct', spy)
+    runs = []
+    for use_direct in (True, False):
+        if not use_direct:
+            monkeypatch.setattr(retrieval, '_direct_plan', lambda *a: None)
+        fns = [lams[0] * SquareLoss()] + ([lams[1] * NegRegularizer()] if lams[1] else [])
+        c, yh, hist = retrieval.gd(op, meas.clone(), FullyDenseModel(grid), lr=1e-1,
+                                   num_iterations=25, loss_fns=fns, progress_bar=False)
+        runs.append((c.detach().clone(), yh.detach().clone(), list(hist.values())))
+    assert len(calls) == 1
+    (ca, ya, ha), (cb, yb, hb) = runs
+    assert ha == hb and len(ha[0]) == 25 and ha[0][-1] < 0.3 * ha[0][0]
+    assert tr.equal(ca, cb) and tr.equal(ya, yb)

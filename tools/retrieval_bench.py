@@ -2,8 +2,8 @@
 """The C5 retrieval (BASELINE configs[4], examples/static_retrieval.py shape): 64^3 grid, 64-view
 ConeCirc (100,50) orbit, FullyDenseModel, SquareLoss + NegRegularizer, Adam lr 0.1, float64
 coefficients, `gd` unchanged.  Reports the Operator construction, the measurement forward and the
-per-iteration time of `gd` (forward + autograd adjoint + Adam on the GPU; `gd` reads the loss
-values back every iteration, as the reference's progress bar does).
+per-iteration time of `gd` (forward + adjoint + Adam on the GPU), both the autograd-free loop gd
+takes for this configuration and the same loop through autograd (the iterates are compared).
 
     python tools/retrieval_bench.py [--iters 100] [--out profiles/r01_retrieval_c5.json]
 """
@@ -44,19 +44,28 @@ def main():
     y = op(truth)
     model = FullyDenseModel(grid)
     losses = [SquareLoss(), NegRegularizer()]
-    retrieval.gd(op, y, model, num_iterations=3, loss_fns=losses, lr=1e-1, progress_bar=False)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    coeffs, y_hat, hist = retrieval.gd(op, y, model, num_iterations=args.iters, loss_fns=losses,
-                                       lr=1e-1, progress_bar=False)
-    torch.cuda.synchronize()
-    t_gd = time.perf_counter() - t0
+    def run():
+        retrieval.gd(op, y, model, num_iterations=3, loss_fns=losses, lr=1e-1, progress_bar=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = retrieval.gd(op, y, model, num_iterations=args.iters, loss_fns=losses, lr=1e-1,
+                           progress_bar=False)
+        torch.cuda.synchronize()
+        return out, time.perf_counter() - t0
+
+    (coeffs, y_hat, hist), t_gd = run()          # the autograd-free loop (retrieval._gd_direct)
+    plan = retrieval._direct_plan
+    retrieval._direct_plan = lambda *a: None     # the same loop through autograd
+    (c_ag, _, hist_ag), t_ag = run()
+    retrieval._direct_plan = plan
     fid = hist[losses[0]]
     rec = {'config': 'C5 retrieval: 64^3 grid, 64-view ConeCirc (100,50) orbit, FullyDenseModel, '
                      'SquareLoss + NegRegularizer, Adam lr 0.1, float64',
            'rays': op._csr['n'], 'segments': op._csr['total'], 'iterations': args.iters,
            'operator_init_ms': t_init * 1e3, 'gd_total_ms': t_gd * 1e3,
            'ms_per_iteration': t_gd / args.iters * 1e3,
+           'ms_per_iteration_autograd': t_ag / args.iters * 1e3,
+           'direct_equals_autograd': bool(torch.equal(coeffs, c_ag)) and hist_ag == hist,
            'fidelity_first': fid[0], 'fidelity_last': fid[-1],
            'reference_cpu_s_per_iteration': 1.64,
            'speedup_vs_reference_cpu': 1.64 / (t_gd / args.iters),
