@@ -1030,6 +1030,9 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     const int64_t s0 = m[2], k0 = m[4], n_tab = m[5];
     int64_t s1 = m[3];
     if (MODE == kFwdTable && n_tab < 0) s1 = s0;      // left to the kFwdGather fallback launch
+    // RUNS has no early exit for blocks without rows (below): an empty pass range instead, so
+    // no pass runs (a pass over an empty window would still close "the last row" at its end)
+    if (RUNS && s0 >= s1) s1 = base0;
     if (MODE == kFwdGather && fallback_only && n_tab >= 0) return;
     // Empty rays integrate to zero: this workgroup's share of the list is fetched now and
     // written at the very end, off the critical path.

@@ -215,15 +215,19 @@ def _check_granule_tables(grid, geom, op, gpu, tab_bytes):
                 d.loc, d.tab = lc, tb
 
 
-def test_long_rows_fall_back_to_per_segment_gather(gpu):
+@pytest.mark.parametrize('runs', ['auto', 'on'])
+def test_long_rows_fall_back_to_per_segment_gather(runs, gpu, monkeypatch):
     """Rays of ~3300 segments through 1650 shells: their workgroups exceed the granule table
-    (n_tab = -1) and use the per-segment gather; results against the C oracle's trace + forward."""
+    (n_tab = -1) and use the per-segment gather, and the workgroups inside a long row own no
+    row; results against the C oracle's trace + forward, with and without run records."""
     from oracle import oracle
     from sph_raytracer_amd import ConeRectGeom, Operator, SphericalGrid, _lib
     from sph_raytracer_amd.raytracer import find_starts
+    monkeypatch.setenv('SPHRT_RUNS', runs)
     grid = SphericalGrid(shape=(1650, 2, 3))
     geom = ConeRectGeom((4, 5), pos=(3, 0.01, 0.02), fov=(2, 2))
     op = Operator(grid, geom, device=gpu)
+    assert bool(op._csr['desc'].runs) == (runs == 'on')
     blocks = op._csr['blocks'].cpu().numpy().reshape(-1, _lib.BLOCK_FIELDS)
     assert (blocks[:, 5] == -1).any()
     assert op._csr['desc'].n_fallback == int((blocks[:, 5] == -1).sum())
@@ -654,7 +658,8 @@ def test_run_records(c2, gpu, monkeypatch):
     still matches the oracle."""
     from sph_raytracer_amd import Operator, ViewGeom, _lib
     grid, geom, op_auto = c2
-    assert not op_auto._csr['desc'].runs       # auto: a single-wave grid keeps the loads
+    if os.environ.get('SPHRT_RUNS', 'auto') == 'auto':
+        assert not op_auto._csr['desc'].runs   # auto: a single-wave grid keeps the loads
     monkeypatch.setenv('SPHRT_RUNS', 'on')
     op = Operator(grid, geom, device=gpu)
     for csr in (op._csr, dict(op._transposed(), n=math.prod(grid.shape))):
