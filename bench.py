@@ -261,12 +261,18 @@ def main():
     for _ in range(3):
         op(x_host)
     t0 = time.perf_counter()
-    reps_h = 50
+    reps_h = 20
     for _ in range(reps_h):
         op(x_host)
     t_host = (time.perf_counter() - t0) / reps_h
 
-    k_ms, k_method = kernel_time_ms(op, x)
+    k_reps = 50
+    k_ms, k_method = kernel_time_ms(op, x, reps=k_reps)
+    # launch order of the forward kernel in this process, for tools/rocprof_legs.py (splits a
+    # rocprofv3 kernel trace of this command into these legs)
+    log('legs ' + json.dumps([['first', 1], ['warmup', args.warmup], ['steps', args.steps]] +
+                             ([['final_gather_fwd', 1]] if dist is not None else []) +
+                             [['cold', 3], ['pcie', 3 + reps_h], ['graph', 1 + 4 * k_reps]]))
     kname = op._forward_kernel_name(x)
     traffic, traffic_src = None, None
     # HBM bytes per launch from the newest committed rocprofv3 --pmc passes of this kernel

@@ -120,7 +120,29 @@ __device__ __forceinline__ void sphere_solve(const GridDev& G, const RayGeo& g, 
     if (__builtin_isnan(t_out)) t_out = kInf;
 }
 
+// False exactly when sphere_solve(j) yields no finite distance: R*R - dd*dd < 0 (or NaN) makes
+// both square roots NaN, i.e. +inf crossings that nothing lists.  (The trace skips such shells.)
+__device__ __forceinline__ bool sphere_may_cross(const GridDev& G, const RayGeo& g, int j) {
+    const double R = G.r_b[j];
+    return R * R - g.dd * g.dd >= 0.0;
+}
+
 // ---- cones (e_torch, raytracer.py:373-466) --------------------------------------------------
+// False exactly when cone_solve(j) yields two +inf roots through a NaN square root: the
+// (snapped) discriminant is negative or NaN and the ray is not parallel to a generator (the only
+// override that makes a root finite).  The coefficients repeat cone_solve's operations.
+__device__ __forceinline__ bool cone_may_cross(const GridDev& G, const RayGeo& g, int j) {
+    const double th = G.close_tol;
+    const double c2 = G.c2_e()[j];
+    double aa = g.w2 * g.w2 - c2;
+    const double bb = 2.0 * (g.w2 * g.x2 - g.wx * c2);
+    const double cc = g.x2 * g.x2 - g.nx2 * c2;
+    if (__builtin_fabs(aa) < th) aa = 0.0;
+    double delta = bb * bb - (4.0 * aa) * cc;
+    if (__builtin_fabs(delta) < th) delta = 0.0;
+    const bool parallel = __builtin_fabs(aa) < th && !(__builtin_fabs(bb) < th);
+    return delta >= 0.0 || parallel;
+}
 // Distance/region fix-up of one root t of cone j (region -2 = glancing, keep current region).
 __device__ __forceinline__ void cone_root(const GridDev& G, const RayGeo& g, int j,
                                           double& t, int& reg, int& neg) {

@@ -371,6 +371,17 @@ __device__ __forceinline__ void load_ray(const RaysDev& R, int64_t i, double* x,
     s[0] = sp[0]; s[1] = sp[1]; s[2] = sp[2];
 }
 
+// First boundary j < n with ok(j) (n when none), wave-uniform.
+template <typename Ok>
+__device__ __forceinline__ int first_may_cross(int n, int lane, Ok ok) {
+    for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
+        const uint64_t m = __ballot(j < n && ok(j));
+        if (m) return j0 + __builtin_ctzll(m);
+    }
+    return n;
+}
+
 // Trace ray `ray` (wave-uniform) with the whole wave.  keys/pays: this wave's LDS list.
 template <int MODE, typename T>
 __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const int se,
@@ -420,9 +431,17 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     };
 
     const int nbr = G.nbr, nbe = G.nbe, nba = G.nba;
-    for (int j0 = 0; j0 < nbr; j0 += 64) {
+    // Families of more than 64 boundaries solve only the 64-wide chunks that can list something:
+    // from the first boundary whose solve can give a finite crossing (sphere_may_cross /
+    // cone_may_cross: exact, the skipped solves would yield +inf only), and chunks without such a
+    // boundary are skipped.  (C5: 65 shells / cones, one chunk instead of two; C3: 129, ~2
+    // instead of 3.)  Families of <= 64 boundaries keep the single chunk (no pre-pass).
+    auto sph_ok = [&](int j) { return sphere_may_cross(G, g, j); };
+    auto cone_ok = [&](int j) { return cone_may_cross(G, g, j); };
+    for (int j0 = nbr > 64 ? first_may_cross(nbr, lane, sph_ok) : 0; j0 < nbr; j0 += 64) {
         const int j = j0 + lane;
         const bool v = j < nbr;
+        if (nbr > 64 && __ballot(v && sph_ok(j)) == 0) continue;
         double ti = kInf, to = kInf;
         int ri = 0, ro = 0, ni, no;
         if (v) sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
@@ -435,9 +454,10 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         push(v && keep(to) && !(to == ti && ro == ri), to, nbr + j, ro);
     }
     const int ce0 = 2 * nbr;
-    for (int j0 = 0; j0 < nbe; j0 += 64) {
+    for (int j0 = nbe > 64 ? first_may_cross(nbe, lane, cone_ok) : 0; j0 < nbe; j0 += 64) {
         const int j = j0 + lane;
         const bool v = j < nbe;
+        if (nbe > 64 && __ballot(v && cone_ok(j)) == 0) continue;
         double ta = kInf, tb = kInf;
         int ra = 0, rb = 0, na_, nb_;
         if (v) cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);

@@ -310,6 +310,44 @@ def test_c5_geometry_vs_oracle_sample(gpu):
     assert msg is None, msg
 
 
+@pytest.mark.parametrize('case', ['c3_orbit', 'inside_starts', 'hemisphere'])
+def test_wide_families_vs_oracle(case, gpu):
+    """Grids of more than 64 boundaries per family, where the trace solves only the chunks whose
+    boundaries can cross (sphere_may_cross / cone_may_cross): the C3 grid (129 per family) seen
+    by an orbit, random rays starting inside a (100, 90, 130) grid (every family listed behind
+    the start), and a hemisphere / half-azimuth grid of 97 x 70 x 80 — every ray against the C
+    oracle (IEEE sqrt), segments and f64 line integrals."""
+    from oracle import oracle
+    from sph_raytracer_amd import ConeRectGeom, Operator, SphericalGrid, ViewGeom
+    from sph_raytracer_amd.raytracer import find_starts
+    if case == 'c3_orbit':
+        grid, geom = _orbit(6, (32, 64), grid_shape=(128, 128, 128))
+    elif case == 'inside_starts':
+        grid = SphericalGrid(shape=(100, 90, 130))
+        gen = tr.Generator().manual_seed(7)
+        xs = (tr.rand((4000, 3), generator=gen, dtype=tr.float64) - 0.5) * 1.2
+        d = tr.randn((4000, 3), generator=gen, dtype=tr.float64)
+        geom = ViewGeom(xs, d / d.norm(dim=-1, keepdim=True))
+    else:
+        grid = SphericalGrid(shape=(97, 70, 80), size_e=(0, tr.pi / 2), size_a=(0, tr.pi))
+        geom = sum(ConeRectGeom((24, 40), pos=p, fov=(40, 40))
+                   for p in ((3, 1, 2), (-2, 2.5, 0.5), (0.3, -4, -1)))
+    op = Operator(grid, geom, device=gpu)
+    xs = np.broadcast_to(geom.ray_starts.numpy(), geom.rays.shape).reshape(-1, 3).copy()
+    rays = geom.rays.numpy().reshape(-1, 3).copy()
+    starts = find_starts(grid, tr.from_numpy(xs)).numpy()
+    oracle.use_mkl_sqrt(False)
+    g = oracle.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy())
+    ref = oracle.trace_segments(g, xs, rays, starts)
+    got = tuple(t.cpu().numpy() for t in op.segments())
+    msg = gc.compare_segments(ref, got, 1.0, case)
+    assert msg is None, msg
+    x = tr.rand(grid.shape, dtype=tr.float64, generator=tr.Generator().manual_seed(3))
+    want = np.asarray(oracle.forward(*ref, x.numpy(), math.prod(grid.shape))).reshape(-1)
+    have = op(x.to(gpu)).cpu().numpy().reshape(-1)
+    assert np.allclose(have, want, rtol=1e-10, atol=1e-12)
+
+
 def test_gd_retrieval_decreases_loss(gpu):
     """static_retrieval.py's loop (FullyDenseModel, SquareLoss + NegRegularizer, Adam) on a small
     grid: runs unchanged on the HIP operator and the fidelity loss drops."""

@@ -38,7 +38,7 @@ def main():
         fn()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        buf = (ctypes.c_ulonglong * 8)()
+        buf = (ctypes.c_ulonglong * 16)()
         lib.sphrt_diag_trace_cycles(ctypes.cast(buf, ctypes.c_void_p), 0)
         n = max(buf[5], 1)
         rec[name] = {'rays_traced': buf[5], 'mean_F': buf[6] / n, 'wall_ms': wall * 1e3,
