@@ -159,37 +159,60 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     """`gd` for `_direct_plan` loops: the same arithmetic as autograd's, op by op, so the
     iterates are the same (the Operator forward, the adjoint of the SquareLoss residual, the
     NegRegularizer's -lam/N on negative voxels, the optimiser step), without building and walking
-    a graph every iteration: one forward, one adjoint and ~10 elementwise launches.
+    a graph every iteration: one forward, one adjoint, the two fused loss tails
+    of csrc/loss.hip, two means and the optimiser step.
 
     Gradient of lam * mean((y - f(d))^2): autograd's chain gives (lam / N) * (2 * (y - f(d)))
     negated, i.e. (f(d) - y) * (2 * (lam / N)) exactly (scaling by 2 and negation are exact).
     Gradient of lam * mean(|clip(d, max=0)|): -(lam / N) where d < 0, else 0 (sign(0) = 0).
     The two are summed (IEEE addition commutes, so the order autograd accumulates them in does
     not matter) and handed to the optimiser as coeffs.grad."""
+    from . import _lib
     sq, neg = plan
     losses = {fn: [] for fn in loss_fns}
     y.requires_grad_()                 # (the reference's own side effect on y)
-    yd = y.detach().to(coeffs.dtype)   # (y - f(d) promotes a float32 y exactly, the same)
+    # y as measured: a float32 y is promoted inside the residual kernel (exactly, as y - f(d)
+    # promotes it); anything else is converted to float64 once
+    yd = y.detach()
+    if yd.dtype not in (t.float32, t.float64):
+        yd = yd.to(coeffs.dtype)
+    yd = yd.contiguous()
     c_sq = sq.lam / yd.numel()
     c_neg = neg.lam / coeffs.numel() if neg is not None else 0.0
     pending = {fn: [] for fn in loss_fns}
     step = _split_fused_adam(opt, coeffs)
     bar = _Bar(range(num_iterations), progress_bar)
+    lib = _lib.load()
+    n_meas, n_vox = yd.numel(), coeffs.numel()
     try:
         with t.no_grad():
             for _ in bar:
                 opt.zero_grad()
                 d = coeffs.detach()
-                r = f(d) - yd
-                sq_val = t.mean(r * r)
+                stream = _lib.stream_of(d.device)
+                yhat = f(d)
+                if yhat.shape != yd.shape:
+                    raise ValueError(f'measurements {tuple(yd.shape)} do not match the operator '
+                                     f'output {tuple(yhat.shape)}')
+                # r = f(d) - y, r * r (the loss value) and r * (2 lam / N) (the adjoint's input)
+                # in one launch (csrc/loss.hip)
+                r_scaled, r_sq = t.empty_like(yhat), t.empty_like(yhat)
+                _lib.check(lib.sphrt_sq_residual_f64(
+                    _lib.ptr(yhat), _lib.ptr(yd), int(yd.dtype == t.float64), n_meas,
+                    2 * c_sq, _lib.ptr(r_scaled), _lib.ptr(r_sq), stream), 'sphrt_sq_residual_f64')
+                sq_val = t.mean(r_sq)
                 if not _unit(sq.lam):
                     sq_val = sq.lam * sq_val
-                g = f._apply_adjoint(r * (2 * c_sq), tuple(d.shape), d.dtype, d.device)
+                g = f._apply_adjoint(r_scaled, tuple(d.shape), d.dtype, d.device)
                 vals = {sq: sq_val}
                 if neg is not None:
-                    neg_val = t.mean(t.abs(d.clamp(max=0)))
+                    # |clamp(d, max=0)| (the loss value) and g -= lam/N where d < 0, one launch
+                    abs_neg = t.empty_like(d)
+                    _lib.check(lib.sphrt_neg_reg_f64(_lib.ptr(d), n_vox, c_neg, _lib.ptr(g),
+                                                     _lib.ptr(abs_neg), stream),
+                               'sphrt_neg_reg_f64')
+                    neg_val = t.mean(abs_neg)
                     vals[neg] = neg_val if _unit(neg.lam) else neg.lam * neg_val
-                    g.sub_(d.lt(0).to(g.dtype), alpha=c_neg)
                 for fn in loss_fns:
                     pending[fn].append(vals[fn])
                 if progress_bar:
