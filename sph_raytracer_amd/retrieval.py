@@ -3,7 +3,7 @@
 Every iteration is one Operator forward per fidelity loss plus one backward, i.e. the forward
 and adjoint HIP kernels on the cached trace; the optimiser step is plain PyTorch.  The
 examples/static_retrieval.py loop (FullyDenseModel, SquareLoss + NegRegularizer) runs the same
-arithmetic without autograd (_gd_direct): the same iterates, a third of the launches.
+arithmetic without autograd (_gd_direct): the same iterates, a quarter of the launches.
 """
 import math
 
@@ -159,8 +159,9 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     """`gd` for `_direct_plan` loops: the same arithmetic as autograd's, op by op, so the
     iterates are the same (the Operator forward, the adjoint of the SquareLoss residual, the
     NegRegularizer's -lam/N on negative voxels, the optimiser step), without building and walking
-    a graph every iteration: one forward, one adjoint, the two fused loss tails
-    of csrc/loss.hip, two means and the optimiser step.
+    a graph every iteration: one forward, one adjoint, the two fused loss tails of
+    csrc/loss.hip (each ending in its loss value: deterministic means, within rounding of the
+    autograd loop's torch.mean) and the optimiser step.
 
     Gradient of lam * mean((y - f(d))^2): autograd's chain gives (lam / N) * (2 * (y - f(d)))
     negated, i.e. (f(d) - y) * (2 * (lam / N)) exactly (scaling by 2 and negation are exact).
@@ -184,6 +185,9 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     bar = _Bar(range(num_iterations), progress_bar)
     lib = _lib.load()
     n_meas, n_vox = yd.numel(), coeffs.numel()
+    # partials + counter of the fused means (zeroed once; each launch re-arms its counter)
+    ws = t.zeros(lib.sphrt_loss_workspace_bytes(), dtype=t.uint8, device=coeffs.device)
+    wsp, wsn = _lib.ptr(ws), ws.numel()
     try:
         with t.no_grad():
             for _ in bar:
@@ -194,24 +198,24 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                 if yhat.shape != yd.shape:
                     raise ValueError(f'measurements {tuple(yd.shape)} do not match the operator '
                                      f'output {tuple(yhat.shape)}')
-                # r = f(d) - y, r * r (the loss value) and r * (2 lam / N) (the adjoint's input)
+                # r = f(d) - y, r * (2 lam / N) (the adjoint's input) and mean(r * r) (the loss)
                 # in one launch (csrc/loss.hip)
-                r_scaled, r_sq = t.empty_like(yhat), t.empty_like(yhat)
+                r_scaled = t.empty_like(yhat)
+                sq_val = t.empty((), dtype=t.float64, device=d.device)
                 _lib.check(lib.sphrt_sq_residual_f64(
                     _lib.ptr(yhat), _lib.ptr(yd), int(yd.dtype == t.float64), n_meas,
-                    2 * c_sq, _lib.ptr(r_scaled), _lib.ptr(r_sq), stream), 'sphrt_sq_residual_f64')
-                sq_val = t.mean(r_sq)
+                    2 * c_sq, _lib.ptr(r_scaled), _lib.ptr(sq_val), wsp, wsn, stream),
+                    'sphrt_sq_residual_f64')
                 if not _unit(sq.lam):
                     sq_val = sq.lam * sq_val
                 g = f._apply_adjoint(r_scaled, tuple(d.shape), d.dtype, d.device)
                 vals = {sq: sq_val}
                 if neg is not None:
-                    # |clamp(d, max=0)| (the loss value) and g -= lam/N where d < 0, one launch
-                    abs_neg = t.empty_like(d)
+                    # g -= lam/N where d < 0 and mean(|clamp(d, max=0)|), one launch
+                    neg_val = t.empty((), dtype=t.float64, device=d.device)
                     _lib.check(lib.sphrt_neg_reg_f64(_lib.ptr(d), n_vox, c_neg, _lib.ptr(g),
-                                                     _lib.ptr(abs_neg), stream),
+                                                     _lib.ptr(neg_val), wsp, wsn, stream),
                                'sphrt_neg_reg_f64')
-                    neg_val = t.mean(abs_neg)
                     vals[neg] = neg_val if _unit(neg.lam) else neg.lam * neg_val
                 for fn in loss_fns:
                     pending[fn].append(vals[fn])

@@ -762,8 +762,9 @@ def test_run_records(c2, gpu, monkeypatch):
 def test_gd_direct_matches_autograd(lams, meas_dtype, gpu, monkeypatch):
     """The static_retrieval.py loop without autograd (retrieval._gd_direct: forward, residual,
     adjoint, -lam/N on negative voxels, Adam) gives the autograd loop's iterates bitwise: the
-    same loss history, coefficients and reconstruction, for unit and non-unit weights, with and
-    without the regulariser, and a float32 measurement."""
+    same coefficients and reconstruction, for unit and non-unit weights, with and without the
+    regulariser, and a float32 measurement.  Its loss values are the fused kernels' own
+    deterministic means: equal to torch.mean's within 1e-13 relative."""
     from sph_raytracer_amd import Operator, retrieval
     from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
     from sph_raytracer_amd.model import FullyDenseModel
@@ -791,5 +792,7 @@ def test_gd_direct_matches_autograd(lams, meas_dtype, gpu, monkeypatch):
         runs.append((c.detach().clone(), yh.detach().clone(), list(hist.values())))
     assert len(calls) == 1
     (ca, ya, ha), (cb, yb, hb) = runs
-    assert ha == hb and len(ha[0]) == 25 and ha[0][-1] < 0.3 * ha[0][0]
+    assert len(ha) == len(hb) and len(ha[0]) == 25 and ha[0][-1] < 0.3 * ha[0][0]
+    for la, lb in zip(ha, hb):
+        assert np.allclose(la, lb, rtol=1e-13, atol=0), (la, lb)
     assert tr.equal(ca, cb) and tr.equal(ya, yb)

@@ -65,7 +65,9 @@ def main():
            'operator_init_ms': t_init * 1e3, 'gd_total_ms': t_gd * 1e3,
            'ms_per_iteration': t_gd / args.iters * 1e3,
            'ms_per_iteration_autograd': t_ag / args.iters * 1e3,
-           'direct_equals_autograd': bool(torch.equal(coeffs, c_ag)) and hist_ag == hist,
+           'direct_iterates_equal_autograd': bool(torch.equal(coeffs, c_ag)),
+           'direct_loss_max_rel_diff': max(
+               abs(a - b) / max(abs(b), 1e-300) for k in hist for a, b in zip(hist[k], hist_ag[k])),
            'fidelity_first': fid[0], 'fidelity_last': fid[-1],
            'reference_cpu_s_per_iteration': 1.64,
            'speedup_vs_reference_cpu': 1.64 / (t_gd / args.iters),
