@@ -16,6 +16,8 @@
 // whatever the row lengths, ~3 dependent global round trips per workgroup, deterministic order.
 #include <hipcub/hipcub.hpp>
 
+#include <stdlib.h>
+
 #include "common.hpp"
 
 namespace sphrt {
@@ -724,8 +726,12 @@ __device__ __forceinline__ void stage_one(const T* __restrict__ rho, int32_t g, 
 #endif
     const char* src = reinterpret_cast<const char*>(rho) + (uint32_t)g * (16u * G) +
                       16 * (lane % G);
+#ifndef SPHRT_FWD_ABL_NODMA      // diagnostic builds only: no granule DMA (wrong results)
     __builtin_amdgcn_global_load_lds((const void*)src,
         (__attribute__((address_space(3))) void*)(dens + 4 * (e0 + 1)), 16, 0, 0);
+#else
+    (void)src;
+#endif
 }
 
 // The volume's last granule, if partial (voxel count not a multiple of 4), can only be the
@@ -1248,8 +1254,14 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             }
             bool tot_has;
             double tot_sum;
+#ifdef SPHRT_FWD_ABL_SEGSCAN   // diagnostic builds only: no segmented scan (wrong results)
+            const double ex = 0.0;
+            tot_has = true;
+            tot_sum = (double)tail;
+#else
             const double ex = block_excl_segsum1<W>(hmask != 0, (double)tail, tot_has, tot_sum,
                                                  sh.has[par], sh.sum[par]);
+#endif
             par ^= 1;
             FWD_STAMP(4);
             // the run open at this thread's start: the segmented prefix of the earlier threads,
@@ -1594,6 +1606,11 @@ static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int
 // 7.0 -> 6.7 us); otherwise (the array fits every L2, several waves) dispatch order is as fast or
 // faster (C5 f64 64 vs 68 us with runs of 64).
 static int fwd_chunk(const sphrt_csr* c, size_t elem) {
+    static const int forced = [] {     // SPHRT_XCD_CHUNK=k: runs of k blocks (A/B studies)
+        const char* e = getenv("SPHRT_XCD_CHUNK");
+        return e ? atoi(e) : -1;
+    }();
+    if (forced >= 0) return forced;
     if (c->n_cols * (int64_t)elem > (int64_t)(4 << 20)) return 64;
     if (c->n_blocks <= 256 * 6) return INT32_MAX;
     return 0;
