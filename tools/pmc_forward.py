@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""rocprofv3 PMC passes over the bare float32 forward (tools/prof_forward.py --only) and the
+"""rocprofv3 PMC passes over the bare forward (the bench config's dtype) (tools/prof_forward.py --only) and the
 per-launch numbers the bench roofline uses.  Runs rocprofv3 as a child process (this driver never
 touches the GPU itself); one counter group per pass (MI355X_MICROARCH.md § rocprofv3 PMC slots).
 
@@ -28,24 +28,25 @@ PASSES = [
 ]
 
 
-def kernel_name(config):
-    """The f32 forward instantiation for a config, from a child process (this driver never
+def kernel_name(config, dtype='f32'):
+    """The forward instantiation for a config and dtype, from a child process (this driver never
     touches the GPU itself)."""
     code = ('import sys, torch; sys.path.insert(0, %r); sys.path.insert(0, %r); import bench; '
             'from sph_raytracer_amd import Operator; cfg = bench.CONFIGS[%r]; '
             'g, v = bench.build_geometry(cfg, 0, 1); op = Operator(g, v, device=torch.device("cuda", 0)); '
-            'x = torch.rand(cfg[0], device="cuda"); print(op._forward_kernel_name(x))'
-            % (ROOT, os.path.join(ROOT, 'tools'), config))
+            'x = torch.rand(cfg[0], device="cuda", dtype=torch.%s); print(op._forward_kernel_name(x))'
+            % (ROOT, os.path.join(ROOT, 'tools'), config,
+               'float32' if dtype == 'f32' else 'float64'))
     out = subprocess.run([sys.executable, '-c', code], check=True, capture_output=True, text=True)
     return out.stdout.strip().splitlines()[-1]
 
 
-def run_pass(counters, workdir, config, reps, kernel):
+def run_pass(counters, workdir, config, reps, kernel, dtype='f32'):
     d = os.path.join(workdir, '_'.join(c.lower() for c in counters[:2]))
     shutil.rmtree(d, ignore_errors=True)
     cmd = ['rocprofv3', '--pmc', *counters, '-d', d, '-o', 'pmc', '--output-format', 'csv', '--',
            sys.executable, os.path.join(ROOT, 'tools', 'prof_forward.py'), '--only', '--reps',
-           str(reps), '--config', config]
+           str(reps), '--config', config, '--dtype', dtype]
     subprocess.run(cmd, check=True, cwd=ROOT, stdout=subprocess.DEVNULL, timeout=90)
     files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
     if not files:
@@ -67,29 +68,39 @@ def main():
     ap.add_argument('--out', required=True)
     ap.add_argument('--config', default='c2')
     ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--dtype', default=None, choices=['f32', 'f64'],
+                    help='forward dtype (default: the bench config\'s)')
     ap.add_argument('--kernel', default=None,
                     help='kernel name substring (default: the instantiation the f32 forward runs)')
     ap.add_argument('--workdir', default=os.path.join(ROOT, 'gpurun_out', 'pmc'))
     ap.add_argument('--extra', action='append', default=[],
                     help='one more counter group (space-separated names) per use')
     args = ap.parse_args()
+    if args.dtype is None:
+        sys.path.insert(0, ROOT)
+        import bench
+        import torch
+        args.dtype = 'f64' if bench.CONFIGS[args.config][4] == torch.float64 else 'f32'
     if args.kernel is None:
-        args.kernel = kernel_name(args.config)
+        args.kernel = kernel_name(args.config, args.dtype)
     per_launch, dispatches, raw = {}, {}, []
     passes = PASSES + [e.split() for e in args.extra]
     for counters in passes:
-        v, n, files = run_pass(counters, args.workdir, args.config, args.reps, args.kernel)
+        v, n, files = run_pass(counters, args.workdir, args.config, args.reps, args.kernel,
+                               args.dtype)
         per_launch.update(v)
         dispatches.update(n)
         raw += files
     rec = {
-        'kernel': args.kernel, 'config': args.config, 'dispatches': dispatches,
+        'kernel': args.kernel, 'config': args.config, 'dtype': args.dtype,
+        'dispatches': dispatches,
         'per_launch': per_launch,
         'correction': 'MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of wide streaming reads on '
                       'gfx950 -> doubled; WRITE_SIZE exact; KB = 1024 B; one counter group per pass',
         'traffic_bytes_per_launch': (2 * per_launch['FETCH_SIZE'] + per_launch['WRITE_SIZE']) * 1024,
         'commands': [f'rocprofv3 --pmc {" ".join(c)} -d ... -- python tools/prof_forward.py --only '
-                     f'--reps {args.reps} --config {args.config}' for c in passes],
+                     f'--reps {args.reps} --config {args.config} --dtype {args.dtype}'
+                     for c in passes],
     }
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with open(args.out, 'w') as f:

@@ -4,7 +4,7 @@ adjoint, from HIP events around graph-replayed launches, interleaved rounds in o
 (guide §5.4 rule 24).
 
     python tools/prof_forward.py [--config c2] [--rounds 5] [--reps 50]
-    python tools/prof_forward.py --only [--reps 20]     # bare f32 forwards, for rocprofv3 --pmc
+    python tools/prof_forward.py --only [--reps 20] [--dtype f64]   # bare forwards, for rocprofv3 --pmc
 """
 import argparse
 import json
@@ -44,6 +44,7 @@ def main():
     ap.add_argument('--reps', type=int, default=50)
     ap.add_argument('--config', default='c2')
     ap.add_argument('--only', action='store_true')
+    ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'], help='--only: forward dtype')
     args = ap.parse_args()
     import bench
     from sph_raytracer_amd import Operator, _lib
@@ -57,8 +58,9 @@ def main():
     o32 = torch.empty(n, dtype=torch.float32, device=dev)
     o64 = torch.empty(n, dtype=torch.float64, device=dev)
     if args.only:
+        xo, oo = (x32, o32) if args.dtype == 'f32' else (x64, o64)
         for _ in range(args.reps):
-            op._launch_forward(x32, o32, 1, 0)
+            op._launch_forward(xo, oo, 1, 0)
         torch.cuda.synchronize()
         return
     y = torch.rand(n, dtype=torch.float64, device=dev)
