@@ -985,8 +985,15 @@ using AccumOf = typename std::conditional<sizeof(T) == 4, float, double>::type;
 
 // RUNS (table mode, sphrt_csr.runs set): the rows' rays and the empty rays come from the block's
 // run record (one dword per lane, loaded with the table entries) instead of row_ray / empty_ray.
+// HALF (float64 table mode with early DMA, tables of kHalfTab < n <= 2 kHalfTab granules): the LDS
+// image holds half a table — entries [0, kHalfTab), then [kHalfTab, n_tab) — so a workgroup
+// reserves 24.6 KB instead of up to 49 KB and five workgroups fit a CU instead of three (C5).
+// Every segment reads its density in the phase that holds its granule (the other phase reads
+// the zero granule) and keeps that value: the sums are unchanged, bit for bit.
+constexpr int kHalfTab = kGranEarly * kThreads;   // = the early DMA rounds' entries (768)
+
 template <typename T, typename L, int MODE, typename TabT = int32_t, bool EDMA = false,
-          int P = kPer, bool RUNS = false>
+          int P = kPer, bool RUNS = false, bool HALF = false>
 __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_kernel(
     const int64_t* __restrict__ blocks, const int32_t* __restrict__ vox,
     const uint16_t* __restrict__ loc, const TabT* __restrict__ tab, const L* __restrict__ len,
@@ -995,6 +1002,8 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     int64_t ocs, int64_t n_rays, int64_t n_seg, int64_t n_cols, int64_t tab_stride,
     int xcd_chunk, int fallback_only, const int32_t* __restrict__ runs) {
     static_assert(!RUNS || MODE == kFwdTable, "run records serve the table mode");
+    static_assert(!HALF || (MODE == kFwdTable && EDMA && P == kPer && kPass / P == kThreads),
+                  "half tables: table mode, early DMA, 256-thread workgroups");
     __shared__ FwdShared sh;
     extern __shared__ __attribute__((aligned(16))) unsigned char fwd_dyn_lds[];
     T* dens = reinterpret_cast<T*>(fwd_dyn_lds);   // 4 * tab_stride entries (table mode)
@@ -1121,7 +1130,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
         window(base0, lo, hi);
         hmask = window_chunk<L, local, P>(raw, o, lo, hi, v, l);
     }
-    if (local && EDMA)        // rounds past the early ones (tables of more than 768 granules)
+    if (local && EDMA && !HALF)   // rounds past the early ones (tables of more than 768 granules)
         stage_granules_late<T, TabT, THR>(density, tab_b, kEarlyRounds<T, THR>, (int)n_tab, g_full,
                                           dens);
     int64_t rbase = 0;                            // rows started in earlier passes
@@ -1130,7 +1139,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     for (int64_t c = 0; c < nc; ++c) {
         const T* rho = density + c * cs;
         T* oc = out + c * ocs;
-        if (local && c > 0) {
+        if (local && c > 0 && !HALF) {
             stage_granules_late<T, TabT, THR>(rho, tab_b, 0, (int)n_tab, g_full, dens);
             stage_partial_tail<T, TabT, THR>(rho, tab_b, (int)n_tab, n_cols, dens);
         }
@@ -1156,6 +1165,14 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
                     rv[k] = l[k] != (L)0 ? rho[vslot<local, P>(v, k) & ~kHead] : (T)0;
             }
             int pass_heads;
+            // HALF: the first half is staged again for each channel, and for every later pass of
+            // a two-phase block (its LDS then holds the second half); the previous pass's reads
+            // all precede its segmented-scan barrier
+            if constexpr (HALF) {
+                if ((c > 0 && base == base0) || (n_tab > kHalfTab && base != base0))
+                    stage_granules_late<T, TabT, THR>(rho, tab_b, 0, (int)imin64(n_tab, kHalfTab),
+                                                      g_full, dens);
+            }
             // (table mode: the full barrier also retires the granule LDS-DMA)
             const int hb = block_excl_count1<local, W>(hcount, pass_heads, sh.cnt[par]);
             FWD_STAMP(3);
@@ -1207,10 +1224,32 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
                 if constexpr (RUNS) return i < 0 ? r_prev : i == 0 ? r_first : ray_of_row(qb + i);
                 return i < 0 ? r_prev : i == 0 ? r_first : rows[i];
             };
-            if constexpr (local) {
+            if constexpr (local && !HALF) {
 #pragma unroll
                 for (int k = 0; k < P; ++k)
                     rv[k] = lds_at<T>(dens, vslot<local, P>(v, k));   // masked: the zero granule
+            }
+            if constexpr (HALF) {
+                // slots of entries < kHalfTab lie below `lim` (float-unit offsets 16 (r+1) + 4 i);
+                // the rest read the zero granule (x & 15) in this phase
+                constexpr uint32_t lim = 16u * (kHalfTab + 1);
+#pragma unroll
+                for (int k = 0; k < P; ++k) {
+                    const uint32_t x = vslot<local, P>(v, k);
+                    rv[k] = lds_at<T>(dens, x < lim ? x : (x & 15u));
+                }
+                if (n_tab > kHalfTab) {             // (block-uniform)
+                    lds_barrier();                  // every first-half read is done
+                    stage_granules_late<T, TabT, THR>(rho, tab_b + kHalfTab, 0,
+                                                      (int)n_tab - kHalfTab, g_full, dens);
+                    __syncthreads();                // retires the DMA
+#pragma unroll
+                    for (int k = 0; k < P; ++k) {
+                        const uint32_t x = vslot<local, P>(v, k);
+                        const T r1 = lds_at<T>(dens, x < lim ? (x & 15u) : x - 16u * kHalfTab);
+                        rv[k] = x < lim ? rv[k] : r1;
+                    }
+                }
             }
             if constexpr (MODE == kFwdDynamic) {   // time slice of each segment's ray
                 int rank = 0;
@@ -1583,6 +1622,16 @@ constexpr size_t kTableLdsMax = SPHRT_TABLE_LDS_MAX;   // dynamic LDS for the st
 #ifndef SPHRT_FWD_EDMA
 #define SPHRT_FWD_EDMA 1
 #endif
+// SPHRT_FWD_HALF=0 (build time, or the environment at launch) keeps whole float64 tables (A/B
+// studies, tests).
+#ifndef SPHRT_FWD_HALF
+#define SPHRT_FWD_HALF 1
+#endif
+static bool half_tables_on() {
+    const char* e = getenv("SPHRT_FWD_HALF");
+    return SPHRT_FWD_HALF != 0 && !(e && e[0] == '0');
+}
+
 static bool early_dma(const sphrt_csr* c) {
     return SPHRT_FWD_EDMA && table_cols(c) % 4 == 0 &&
            (size_t)(kGranEarly * kThreads + 1) * 4 * 8 <= kTableLdsMax;
@@ -1645,24 +1694,35 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
             if (int e = check_launch("stage_pack_kernel")) return e;
         }
         const bool edma = early_dma(c);
-        size_t lds = (size_t)((edma ? imax64(c->tab_stride, kGranEarly * kThreads)
-                                    : c->tab_stride) + 1) * 4 * sizeof(T);   // + zero granule
+        // float64 tables that leave fewer than 4 workgroups per CU (over 40 KB of LDS): half
+        // tables, 5 per CU (C5 forward f64 62.1 -> 53.0 us, transposed adjoint 58.8 -> 53.7 us).
+        // Not below: C3's 34.8 KB tables (4 per CU) measured 364 -> 383 us with halves (more
+        // resident workgroups, more L2 misses; few of its tables even need the second phase).
+        const bool half = sizeof(T) == 8 && edma && (size_t)(c->tab_stride + 1) * 32 > 40 * 1024 &&
+                          c->tab_stride <= 2 * kHalfTab && half_tables_on();
+        size_t lds = (size_t)((half ? kHalfTab
+                               : edma ? imax64(c->tab_stride, kGranEarly * kThreads)
+                                      : c->tab_stride) + 1) * 4 * sizeof(T);   // + zero granule
 #ifdef SPHRT_FWD_LDS_MIN
         lds = lds < (size_t)SPHRT_FWD_LDS_MIN ? (size_t)SPHRT_FWD_LDS_MIN : lds;
 #endif
-#define SPHRT_FWD_TABLE(TabT, E, R)                                                               \
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, TabT, E, P, R>), grid, block, lds,    \
+#define SPHRT_FWD_TABLE(TabT, E, R, H)                                                            \
+        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, TabT, E, P, R, H>), grid, block, lds, \
                            st, SPHRT_FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
-#define SPHRT_FWD_TABLE_R(TabT, E)                                                                \
-        if (c->runs) SPHRT_FWD_TABLE(TabT, E, true);                                              \
-        else SPHRT_FWD_TABLE(TabT, E, false)
+#define SPHRT_FWD_TABLE_R(TabT, E, H)                                                             \
+        if (c->runs) SPHRT_FWD_TABLE(TabT, E, true, H);                                           \
+        else SPHRT_FWD_TABLE(TabT, E, false, H)
+#define SPHRT_FWD_TABLE_E(TabT)                                                                   \
+        if (half) {                                                                               \
+            if constexpr (sizeof(T) == 8 && P == kPer) SPHRT_FWD_TABLE_R(TabT, true, true);       \
+        } else if (edma) SPHRT_FWD_TABLE_R(TabT, true, false);                                    \
+        else SPHRT_FWD_TABLE_R(TabT, false, false)
         if (c->tab_bytes == 2) {
-            if (edma) SPHRT_FWD_TABLE_R(uint16_t, true);
-            else SPHRT_FWD_TABLE_R(uint16_t, false);
+            SPHRT_FWD_TABLE_E(uint16_t);
         } else {
-            if (edma) SPHRT_FWD_TABLE_R(int32_t, true);
-            else SPHRT_FWD_TABLE_R(int32_t, false);
+            SPHRT_FWD_TABLE_E(int32_t);
         }
+#undef SPHRT_FWD_TABLE_E
 #undef SPHRT_FWD_TABLE_R
 #undef SPHRT_FWD_TABLE
         if (c->n_fallback > 0) {   // (natural vox, natural density)

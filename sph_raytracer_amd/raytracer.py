@@ -668,7 +668,8 @@ class Operator:
 
     def _forward_kernel_name(self, d):
         """The forward kernel instantiation a launch on `d` runs (sphrt_forward_*'s choice, for
-        reports): 0 = granule tables staged in LDS, 1 = per-segment gathers, 2 = time slices."""
+        reports): 0 = granule tables staged in LDS, 1 = per-segment gathers, 2 = time slices;
+        the last flag: float64 half tables."""
         t = 'float, float' if d.dtype == tr.float32 else 'double, double'
         n_chan, div, _ = self._layout(d.shape)
         c, n_chan, _, div = self._launch_args(d, n_chan, div)
@@ -681,8 +682,11 @@ class Operator:
             edma = 'true' if cols % 4 == 0 else 'false'
             tabt = 'unsigned short' if c.tab_bytes == 2 else 'int'
             runs = 'true' if c.runs else 'false'
-            return f'forward_kernel<{t}, 0, {tabt}, {edma}, 8, {runs}>'
-        return f'forward_kernel<{t}, {2 if div else 1}, int, false, 8, false>'
+            # float64 half tables (apply.hip kHalfTab = 768 granules per phase)
+            half = (es == 8 and edma == 'true' and (c.tab_stride + 1) * 32 > 40 * 1024
+                    and c.tab_stride <= 1536 and os.environ.get('SPHRT_FWD_HALF', '1') != '0')
+            return f'forward_kernel<{t}, 0, {tabt}, {edma}, 8, {runs}, {"true" if half else "false"}>'
+        return f'forward_kernel<{t}, {2 if div else 1}, int, false, 8, false, false>'
 
     def _apply_forward(self, density):
         with tr.cuda.device(self._cdev):      # launches and allocations on the operator's GPU

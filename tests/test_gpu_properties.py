@@ -348,6 +348,35 @@ def test_wide_families_vs_oracle(case, gpu):
     assert np.allclose(have, want, rtol=1e-10, atol=1e-12)
 
 
+def test_half_tables_float64(gpu, monkeypatch):
+    """C5 geometry (granule tables of up to 1512 entries: float64 forwards stage them in two
+    halves, apply.hip HALF): float64 forward and transposed adjoint against the C oracle on the
+    GPU's own trace, bitwise equal to whole tables (SPHRT_FWD_HALF=0), and two channels (the
+    first half staged again per channel) equal to one channel each."""
+    from oracle import oracle
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(64, (100, 50), kind='circ', grid_shape=(64, 64, 64))
+    op = Operator(grid, geom, device=gpu)
+    assert 1279 < op._csr['desc'].tab_stride <= 1536
+    gen = tr.Generator().manual_seed(5)
+    x = tr.rand((2,) + tuple(grid.shape), dtype=tr.float64, generator=gen)
+    xg = x.to(gpu)
+    assert op._forward_kernel_name(xg[0]).endswith('true, true>')
+    y = op(xg[0])
+    rp, vx, ln = (t.cpu().numpy() for t in op.segments())
+    nv = math.prod(grid.shape)
+    ref = np.asarray(oracle.forward(rp, vx, ln, x[0].numpy(), nv)).reshape(-1)
+    assert np.allclose(y.cpu().numpy().reshape(-1), ref, rtol=1e-10, atol=1e-12)
+    y2 = op(xg)
+    assert tr.equal(y2[0], y) and tr.equal(y2[1], op(xg[1]))
+    yt = tr.rand(geom.shape, dtype=tr.float64, generator=gen)
+    a = op.T(yt.to(gpu))
+    aref = np.asarray(oracle.adjoint(rp, vx, ln, yt.numpy().reshape(-1), nv)).reshape(-1)
+    assert np.allclose(a.cpu().numpy().reshape(-1), aref, rtol=1e-10, atol=1e-12)
+    monkeypatch.setenv('SPHRT_FWD_HALF', '0')
+    assert tr.equal(op(xg[0]), y) and tr.equal(op(xg), y2) and tr.equal(op.T(yt.to(gpu)), a)
+
+
 def test_gd_retrieval_decreases_loss(gpu):
     """static_retrieval.py's loop (FullyDenseModel, SquareLoss + NegRegularizer, Adam) on a small
     grid: runs unchanged on the HIP operator and the fidelity loss drops."""
