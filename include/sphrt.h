@@ -284,18 +284,17 @@ int sphrt_csr_transpose(const sphrt_csr *csr, int64_t n_vox, int64_t *col_ptr, i
 int sphrt_f64_to_f32(const double *src, float *dst, int64_t n, void *stream);
 
 /* ---- retrieval loss tails (csrc/loss.hip; retrieval._gd_direct) ------------------------------
- * SquareLoss: r = yhat - y (y float32 or float64, promoted), r_scaled = r * scale, *mean =
- * mean(r * r).  NegRegularizer: g -= c_neg where d < 0, *mean = mean(|clamp(d, max=0)|).  The
- * elementwise values are single IEEE operations, the values torch's elementwise ops give
- * (reference loss.py:87-162); the means are deterministic, within rounding of torch.mean.
- * `mean` is one device double; the workspace (sphrt_loss_workspace_bytes, zeroed once before
- * its first use) may be reused by calls on one stream, one at a time. */
-size_t sphrt_loss_workspace_bytes(void);
+ * SquareLoss: r = yhat - y (y float32 or float64, promoted), r_scaled = r * scale, and the
+ * partial sums of r * r.  NegRegularizer: g -= c_neg where d < 0, and the partial sums of
+ * |clamp(d, max=0)|.  The elementwise values are single IEEE operations, the values torch's
+ * elementwise ops give (reference loss.py:87-162).  Each call writes sphrt_loss_partials(n)
+ * partial sums (fixed partition and order); the loss is their sum / n, within rounding of
+ * torch.mean. */
+int64_t sphrt_loss_partials(int64_t n);
 int sphrt_sq_residual_f64(const double *yhat, const void *y, int y_is_f64, int64_t n, double scale,
-                          double *r_scaled, double *mean, void *workspace, size_t workspace_size,
-                          void *stream);
-int sphrt_neg_reg_f64(const double *d, int64_t n, double c_neg, double *g, double *mean,
-                      void *workspace, size_t workspace_size, void *stream);
+                          double *r_scaled, double *partial_sums, void *stream);
+int sphrt_neg_reg_f64(const double *d, int64_t n, double c_neg, double *g, double *partial_sums,
+                      void *stream);
 
 /* ---- fused no-store mode: trace + integrate in one pass (nothing persisted) --------------- */
 int sphrt_trace_integrate_f32(const sphrt_plan *plan, const sphrt_rays *rays,

@@ -160,8 +160,9 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     iterates are the same (the Operator forward, the adjoint of the SquareLoss residual, the
     NegRegularizer's -lam/N on negative voxels, the optimiser step), without building and walking
     a graph every iteration: one forward, one adjoint, the two fused loss tails of
-    csrc/loss.hip (each ending in its loss value: deterministic means, within rounding of the
-    autograd loop's torch.mean) and the optimiser step.
+    csrc/loss.hip and the optimiser step.  The loss values are the fused kernels' partial sums,
+    summed for all iterations after the loop: deterministic, within rounding of the autograd
+    loop's torch.mean.
 
     Gradient of lam * mean((y - f(d))^2): autograd's chain gives (lam / N) * (2 * (y - f(d)))
     negated, i.e. (f(d) - y) * (2 * (lam / N)) exactly (scaling by 2 and negation are exact).
@@ -180,17 +181,25 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     yd = yd.contiguous()
     c_sq = sq.lam / yd.numel()
     c_neg = neg.lam / coeffs.numel() if neg is not None else 0.0
-    pending = {fn: [] for fn in loss_fns}
     step = _split_fused_adam(opt, coeffs)
     bar = _Bar(range(num_iterations), progress_bar)
     lib = _lib.load()
     n_meas, n_vox = yd.numel(), coeffs.numel()
-    # partials + counter of the fused means (zeroed once; each launch re-arms its counter)
-    ws = t.zeros(lib.sphrt_loss_workspace_bytes(), dtype=t.uint8, device=coeffs.device)
-    wsp, wsn = _lib.ptr(ws), ws.numel()
+    # every iteration's loss as the workgroup partial sums of its fused kernel, one row per
+    # iteration, summed once after the loop (no reduction launch, no host sync per iteration)
+    ps, pn = lib.sphrt_loss_partials(n_meas), lib.sphrt_loss_partials(n_vox)
+    rows = max(num_iterations, 1)
+    part_sq = t.empty((rows, ps), dtype=t.float64, device=coeffs.device)
+    part_neg = t.empty((rows, pn), dtype=t.float64, device=coeffs.device) if neg is not None else None
+    done = 0
+
+    def scaled(parts, n, lam):
+        val = parts.sum(-1) / n
+        return val if _unit(lam) else lam * val
+
     try:
         with t.no_grad():
-            for _ in bar:
+            for it in bar:
                 opt.zero_grad()
                 d = coeffs.detach()
                 stream = _lib.stream_of(d.device)
@@ -198,39 +207,34 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                 if yhat.shape != yd.shape:
                     raise ValueError(f'measurements {tuple(yd.shape)} do not match the operator '
                                      f'output {tuple(yhat.shape)}')
-                # r = f(d) - y, r * (2 lam / N) (the adjoint's input) and mean(r * r) (the loss)
-                # in one launch (csrc/loss.hip)
+                # r = f(d) - y, r * (2 lam / N) (the adjoint's input) and the partial sums of
+                # r * r (the loss) in one launch (csrc/loss.hip)
                 r_scaled = t.empty_like(yhat)
-                sq_val = t.empty((), dtype=t.float64, device=d.device)
                 _lib.check(lib.sphrt_sq_residual_f64(
                     _lib.ptr(yhat), _lib.ptr(yd), int(yd.dtype == t.float64), n_meas,
-                    2 * c_sq, _lib.ptr(r_scaled), _lib.ptr(sq_val), wsp, wsn, stream),
+                    2 * c_sq, _lib.ptr(r_scaled), _lib.ptr(part_sq[it]), stream),
                     'sphrt_sq_residual_f64')
-                if not _unit(sq.lam):
-                    sq_val = sq.lam * sq_val
                 g = f._apply_adjoint(r_scaled, tuple(d.shape), d.dtype, d.device)
-                vals = {sq: sq_val}
                 if neg is not None:
-                    # g -= lam/N where d < 0 and mean(|clamp(d, max=0)|), one launch
-                    neg_val = t.empty((), dtype=t.float64, device=d.device)
+                    # g -= lam/N where d < 0, and the partial sums of |clamp(d, max=0)|
                     _lib.check(lib.sphrt_neg_reg_f64(_lib.ptr(d), n_vox, c_neg, _lib.ptr(g),
-                                                     _lib.ptr(neg_val), wsp, wsn, stream),
+                                                     _lib.ptr(part_neg[it]), stream),
                                'sphrt_neg_reg_f64')
-                    vals[neg] = neg_val if _unit(neg.lam) else neg.lam * neg_val
-                for fn in loss_fns:
-                    pending[fn].append(vals[fn])
                 if progress_bar:
-                    bar.describe(f'F:{float(sq_val):.1e} '
-                                 f'R:{float(vals[neg]) if neg is not None else 0:.1e} O:0')
+                    fv = float(scaled(part_sq[it], n_meas, sq.lam))
+                    rv = float(scaled(part_neg[it], n_vox, neg.lam)) if neg is not None else 0
+                    bar.describe(f'F:{fv:.1e} R:{rv:.1e} O:0')
                 if step is not None:
                     step(g)
                 else:
                     coeffs.grad = g
                     opt.step()
+                done = it + 1
     except KeyboardInterrupt:
         pass
-    for fn, vals in pending.items():
-        losses[fn] = t.stack(vals).cpu().tolist() if vals else []
+    losses[sq] = scaled(part_sq[:done], n_meas, sq.lam).cpu().tolist()
+    if neg is not None:
+        losses[neg] = scaled(part_neg[:done], n_vox, neg.lam).cpu().tolist()
     # the reference's bookkeeping: the coefficients once some iteration's total was < inf
     totals = [sum(v) for v in zip(*(losses[fn] for fn in loss_fns))]
     best = coeffs if any(v < float('inf') for v in totals) else None
