@@ -1710,13 +1710,20 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, TabT, E, P, R, H>), grid, block, lds, \
                            st, SPHRT_FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
 #define SPHRT_FWD_TABLE_R(TabT, E, H)                                                             \
-        if (c->runs) SPHRT_FWD_TABLE(TabT, E, true, H);                                           \
-        else SPHRT_FWD_TABLE(TabT, E, false, H)
+        do {                                                                                      \
+            if (c->runs) SPHRT_FWD_TABLE(TabT, E, true, H);                                       \
+            else SPHRT_FWD_TABLE(TabT, E, false, H);                                              \
+        } while (0)
 #define SPHRT_FWD_TABLE_E(TabT)                                                                   \
-        if (half) {                                                                               \
-            if constexpr (sizeof(T) == 8 && P == kPer) SPHRT_FWD_TABLE_R(TabT, true, true);       \
-        } else if (edma) SPHRT_FWD_TABLE_R(TabT, true, false);                                    \
-        else SPHRT_FWD_TABLE_R(TabT, false, false)
+        do {                                                                                      \
+            if (half) {                                                                           \
+                if constexpr (sizeof(T) == 8 && P == kPer) { SPHRT_FWD_TABLE_R(TabT, true, true); } \
+            } else if (edma) {                                                                    \
+                SPHRT_FWD_TABLE_R(TabT, true, false);                                             \
+            } else {                                                                              \
+                SPHRT_FWD_TABLE_R(TabT, false, false);                                            \
+            }                                                                                     \
+        } while (0)
         if (c->tab_bytes == 2) {
             SPHRT_FWD_TABLE_E(uint16_t);
         } else {
