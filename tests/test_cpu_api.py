@@ -61,6 +61,41 @@ def test_find_starts():
         assert check(find_starts(SphericalGrid(shape=shape), x), exp)
 
 
+def test_find_starts_host():
+    """The trace's host start binning (_find_starts_host: numpy sums and binning, torch sqrt and
+    arctan2 on the reference's layouts) equals find_starts bitwise: random points inside and
+    outside, the origin, points on radius / elevation / azimuth boundaries, the known answers,
+    several grids and leading shapes."""
+    from sph_raytracer_amd import SphericalGrid
+    from sph_raytracer_amd.raytracer import _find_starts_host, find_starts
+    gen = tr.Generator().manual_seed(11)
+    grids = [SphericalGrid(shape=(50, 50, 50)), SphericalGrid(shape=(7, 9, 12), size_r=(0.2, 1.5),
+                                                                size_e=(0, tr.pi / 2), size_a=(0, tr.pi)),
+             SphericalGrid(shape=(20, 11, 13), size_r=(0.1, 1), spacing='log'),
+             SphericalGrid(shape=(3, 4, 5, 6))]
+    for grid in grids:
+        pts = [(tr.rand((400, 3), generator=gen, dtype=tr.float64) - 0.5) * 3.5,
+               tr.zeros((2, 3), dtype=tr.float64)]
+        r, e, a = (tr.as_tensor(b, dtype=tr.float64) for b in (grid.r_b, grid.e_b, grid.a_b))
+        for rb in r:                                     # on the spheres, the cones, half-planes
+            for eb in e[::3]:
+                for ab in a[::4]:
+                    pts.append(tr.stack([rb * tr.sin(eb) * tr.cos(ab), rb * tr.sin(eb) * tr.sin(ab),
+                                         rb * tr.cos(eb)])[None])
+        pts.append(tr.tensor([[1.0, 0.0, 0.0], [-1.0, 0.0, 0.0], [0.0, 0.0, 1.0], [0.0, 0.0, -0.5],
+                              [-0.3, -0.0, 0.1], [0.0, 0.5, 0.0]], dtype=tr.float64))
+        xs = tr.cat(pts)
+        for shaped in (xs, xs[:48].reshape(4, 2, 6, 3), xs[:1].reshape(1, 1, 1, 3)):
+            want = find_starts(grid, shaped)
+            got = _find_starts_host(grid, shaped.contiguous())
+            assert got.dtype == want.dtype and got.shape == want.shape
+            assert tr.equal(got, want), np.argwhere((got != want).numpy())[:5]
+    for shape, x, exp in START_CASES:
+        g = SphericalGrid(shape=shape)
+        xt = tr.as_tensor(x, dtype=tr.float64)
+        assert tr.equal(_find_starts_host(g, xt), find_starts(g, xt))
+
+
 def test_conerectgeom():
     from sph_raytracer_amd import ConeRectGeom
     g = ConeRectGeom((11, 11), (4, 0, 1), fov=(23, 45))
