@@ -206,9 +206,12 @@ typedef struct sphrt_csr {
 
 int64_t sphrt_csr_blocks(int64_t n_segments);
 size_t sphrt_csr_index_workspace_bytes(int64_t n_rays);
+/* ray_ids: NULL (row r is ray r), or the ray each row reports in row_ray / empty_ray — the
+ * output index of a trace made in another ray order than the geometry's (the Operator traces
+ * ConeCirc views in wedges of 5 azimuth columns, raytracer._trace_order). */
 int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_t *row_ray,
-                    int32_t *empty_ray, int64_t *blocks, int64_t n_blocks, void *workspace,
-                    void *stream);
+                    int32_t *empty_ray, int64_t *blocks, int64_t n_blocks, const int32_t *ray_ids,
+                    void *workspace, void *stream);
 /* Granule tables in two passes.  _count sets n_tab in blocks (-1: no table) and writes two
  * device int64 to stats: {blocks without a table, largest n_tab}; the caller copies the first to
  * csr->n_fallback, picks tab_stride >= the second (csr->tab_stride; tab holds n_blocks *

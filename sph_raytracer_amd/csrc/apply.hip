@@ -94,11 +94,13 @@ __global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* row_ptr, 
 
 __global__ __launch_bounds__(256) void row_list_kernel(const int64_t* row_ptr,
                                                        const int64_t* row_pre, int64_t n,
-                                                       int32_t* row_ray, int32_t* empty_ray) {
+                                                       const int32_t* ray_ids, int32_t* row_ray,
+                                                       int32_t* empty_ray) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= n) return;
-    if (row_ptr[r + 1] > row_ptr[r]) row_ray[row_pre[r]] = (int32_t)r;
-    else empty_ray[r - row_pre[r]] = (int32_t)r;
+    const int32_t id = ray_ids ? ray_ids[r] : (int32_t)r;   // the ray (output index) of row r
+    if (row_ptr[r + 1] > row_ptr[r]) row_ray[row_pre[r]] = id;
+    else empty_ray[r - row_pre[r]] = id;
 }
 
 __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
@@ -1426,7 +1428,7 @@ extern "C" size_t sphrt_csr_index_workspace_bytes(int64_t n_rays) {
 
 extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* vox,
                                int32_t* row_ray, int32_t* empty_ray, int64_t* blocks,
-                               int64_t n_blocks,
+                               int64_t n_blocks, const int32_t* ray_ids,
                                void* workspace, void* stream) {
     if (n_rays < 0 || n_blocks < 1) return fail("bad CSR index sizes");
     if (n_rays == 0) return 0;
@@ -1440,8 +1442,8 @@ extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* 
     hipLaunchKernelGGL(mark_rows_kernel, dim3(g), dim3(256), 0, st, row_ptr, n_rays, vox, flags);
     if (int e = check_launch("mark_rows")) return e;
     if (int e = sphrt_scan_counts(flags, n_rays, pre, scan_ws, stream)) return e;
-    hipLaunchKernelGGL(row_list_kernel, dim3(g), dim3(256), 0, st, row_ptr, pre, n_rays, row_ray,
-                       empty_ray);
+    hipLaunchKernelGGL(row_list_kernel, dim3(g), dim3(256), 0, st, row_ptr, pre, n_rays, ray_ids,
+                       row_ray, empty_ray);
     if (int e = check_launch("row_list")) return e;
     hipLaunchKernelGGL(block_meta_kernel, dim3((unsigned)((n_blocks + 255) / 256)), dim3(256), 0,
                        st, row_ptr, pre, n_rays, n_blocks, blocks);

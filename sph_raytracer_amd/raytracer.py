@@ -17,6 +17,7 @@ Differences from the reference, by design:
 - the caller's ``geom.rays`` tensor is never normalised in place.
 """
 import ctypes
+import functools
 import math
 import os
 
@@ -188,6 +189,52 @@ def _device_rays(geom, dev):
 def _geom_rays(geom, dev):
     rays = _device_rays(geom, dev)
     return geom.rays if rays is None else rays
+
+
+_WEDGE = 5    # azimuth columns per wedge of the ConeCirc trace order
+
+
+def _trace_order(geom, rays):
+    """Per-view order the trace visits a ConeCirc detector's pixels in, or None (geometry order).
+
+    ConeCirc pixels are (radius, azimuth) with the azimuth fastest: ~36 consecutive rays (one
+    workgroup block at C5) sweep most of a ring, whose rays part around the view axis.  Wedges of
+    _WEDGE azimuth columns, radius-major inside, keep a block's rays together: granules per
+    block 1105 -> 770 at C5 (oracle study), forward f32 33.5 -> 28.4 us, f64 53.7 -> 44.2 us,
+    transposed adjoint f64 56.1 -> 47.6 us (tools/exp studies; ConeRect rows are already
+    compact: strips beat every tiling measured).  Only the order of the CSR's rows changes: every
+    row reports its geometry ray (sphrt_csr_index ray_ids), outputs stay in geometry order.
+    SPHRT_RAY_ORDER=natural keeps the geometry order."""
+    if os.environ.get('SPHRT_RAY_ORDER', 'auto') == 'natural':
+        return None
+    from .geometry import ConeCircGeom
+    geoms = getattr(geom, 'geoms', [geom])
+    if not geoms or any(type(g) is not ConeCircGeom for g in geoms):
+        return None
+    shape = tuple(rays.shape[:-1])
+    if len(shape) not in (2, 3) or shape[-1] <= _WEDGE:
+        return None
+    return _wedge_order(shape[-2], shape[-1])
+
+
+@functools.lru_cache(maxsize=16)
+def _wedge_order(h, w):
+    """Pixel order of an (h, w) ConeCirc detector in wedges of _WEDGE azimuth columns."""
+    r = tr.arange(h).repeat_interleave(w)
+    a = tr.arange(w).repeat(h)
+    key = ((a // _WEDGE) * h + r) * _WEDGE + a % _WEDGE
+    return tr.argsort(key)
+
+
+def _permute_rays(rays, perm):
+    """Rays (V, H, W, 3) or (H, W, 3) with each view's pixels in trace order `perm` (a device
+    index) and the geometry ray of every trace row (int32, on the device)."""
+    shape = rays.shape
+    v = shape[0] if rays.dim() == 4 else 1
+    flat = rays.reshape(v, -1, 3).index_select(1, perm)
+    hw = perm.numel()
+    ray_id = (tr.arange(v, device=perm.device, dtype=tr.int32) * hw)[:, None] + perm.to(tr.int32)
+    return flat.reshape(shape), ray_id.reshape(-1)
 
 
 class _RayBatch:
@@ -594,7 +641,12 @@ class Operator:
     def _trace_on(self, dev):
         lib = _lib.load()
         self._plan = _Plan(self.grid, dev)
-        batch = _RayBatch(self.grid, self.geom.ray_starts, _geom_rays(self.geom, dev), dev)
+        rays = _geom_rays(self.geom, dev)
+        perm = _trace_order(self.geom, rays)
+        ray_id = None
+        if perm is not None:           # trace in wedges; rows report their geometry ray
+            rays, ray_id = _permute_rays(rays, perm.to(dev, non_blocking=True))
+        batch = _RayBatch(self.grid, self.geom.ray_starts, rays, dev)
         self._ray_shape = batch.shape
         n = batch.n
         stream = _lib.stream_of(dev)
@@ -608,7 +660,8 @@ class Operator:
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(row_ptr), n, _lib.ptr(vox), _lib.ptr(row_ray),
                                        _lib.ptr(empty_ray), _lib.ptr(blocks), nblocks,
-                                       _lib.ptr(iws), stream), 'sphrt_csr_index')
+                                       _lib.ptr(ray_id), _lib.ptr(iws), stream),
+                   'sphrt_csr_index')
         del iws
         c = _lib.CSR()
         c.n_rays, c.n_segments, c.n_blocks = n, total, nblocks
@@ -621,7 +674,7 @@ class Operator:
         loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
         self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, row_ray=row_ray,
                          empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, runs=runs,
-                         nblocks=nblocks, n=n, total=total, desc=c)
+                         nblocks=nblocks, n=n, total=total, desc=c, ray_id=ray_id)
         self._batch = batch
 
     # -- shape logic of raytracer.py:703-712 -----------------------------------------------------
@@ -794,7 +847,8 @@ class Operator:
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n_vox), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(col_ptr), n_vox, _lib.ptr(t_ray),
                                        _lib.ptr(vox_list), _lib.ptr(empty_vox), _lib.ptr(blocks),
-                                       nblocks, _lib.ptr(iws), stream), 'sphrt_csr_index(T)')
+                                       nblocks, None, _lib.ptr(iws), stream),
+                   'sphrt_csr_index(T)')
         t_len32 = tr.empty(t_len.shape, dtype=tr.float32, device=dev)
         _lib.check(lib.sphrt_f64_to_f32(_lib.ptr(t_len), _lib.ptr(t_len32), t_len.numel(), stream),
                    'sphrt_f64_to_f32')
@@ -805,7 +859,8 @@ class Operator:
         c.row_ray, c.blocks = vox_list.data_ptr(), blocks.data_ptr()
         c.empty_ray = empty_vox.data_ptr()
         c.n_cols = csr['n']
-        shape3 = self._ray_shape3()
+        # (columns are trace rows: detector tiles only when they are the geometry's rays)
+        shape3 = self._ray_shape3() if csr['ray_id'] is None else None
         _set_stage(c, shape3, _stage_brick(nblocks, 'SPHRT_BRICK_T', _BRICK_RAYS)
                    if shape3 else None)
         loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
@@ -858,6 +913,8 @@ class Operator:
         if self.adjoint_mode == 'transpose' and (div == 0 or paired is not None):
             cdt = ddtype if ddtype in (tr.float32, tr.float64) else tr.float32
             yv = yv.to(cdt)
+            if csr['ray_id'] is not None:   # the transpose's columns are trace rows
+                yv = yv.view(-1, n).index_select(1, self._ray_id_long()).reshape(-1)
             if paired is not None:      # columns of the flattened (T, vol) density
                 if 'transposed' not in paired:
                     paired['transposed'] = self._transpose_of(paired['desc'], paired['desc'].n_cols)
@@ -894,7 +951,7 @@ class Operator:
     # -- compatibility views -----------------------------------------------------------------------
     def _padded(self):
         csr = self._csr
-        row_ptr = csr['row_ptr']
+        row_ptr, seg_vox, seg_len = self.segments()      # geometry order
         counts = (row_ptr[1:] - row_ptr[:-1])
         smax = max(int(counts.max().item()) if csr['n'] else 0, 1)
         n, total = csr['n'], csr['total']
@@ -902,8 +959,8 @@ class Operator:
         pos = tr.arange(total, device=row_ptr.device) - row_ptr[:-1][ray]
         vox = tr.zeros((n, smax), dtype=tr.int64, device=row_ptr.device)
         lens = tr.zeros((n, smax), dtype=tr.float64, device=row_ptr.device)
-        vox[ray, pos] = csr['vox'][:total].to(tr.int64) & 0x7FFFFFFF
-        lens[ray, pos] = csr['len'][:total]
+        vox[ray, pos] = seg_vox.to(tr.int64)
+        lens[ray, pos] = seg_len
         _, ne, na = self.grid.shape[-3:]
         regs = tr.stack((vox // (ne * na), (vox // na) % ne, vox % na))
         R = tuple(self._ray_shape)
@@ -919,11 +976,33 @@ class Operator:
         """(*rays, S_max) segment lengths matching ``regs`` (zero padding)."""
         return self._padded()[1].to(device=self.device)
 
+    def _ray_id_long(self):
+        c = self._csr
+        if 'ray_id_long' not in c:
+            c['ray_id_long'] = c['ray_id'].long()
+        return c['ray_id_long']
+
     def segments(self):
         """The trace itself: (row_ptr int64 (n+1,), linear voxel int32, len float64) on the GPU;
-        segment s of ray i is row_ptr[i] <= s < row_ptr[i+1], voxel (r*ne + e)*na + a."""
+        segment s of ray i is row_ptr[i] <= s < row_ptr[i+1], voxel (r*ne + e)*na + a.  Rays in
+        geometry order (a trace made in another order is reordered here)."""
         c = self._csr
-        return c['row_ptr'], c['vox'][:c['total']] & 0x7FFFFFFF, c['len'][:c['total']]
+        row_ptr, vox = c['row_ptr'], c['vox'][:c['total']] & 0x7FFFFFFF
+        seg = c['len'][:c['total']]
+        if c['ray_id'] is None:
+            return row_ptr, vox, seg
+        rid = self._ray_id_long()                     # trace row k -> geometry ray rid[k]
+        counts = row_ptr[1:] - row_ptr[:-1]
+        g_counts = tr.empty_like(counts)
+        g_counts[rid] = counts
+        g_ptr = tr.zeros_like(row_ptr)
+        g_ptr[1:] = tr.cumsum(g_counts, 0)
+        # segment j of trace row k goes to g_ptr[rid[k]] + j
+        row = tr.repeat_interleave(tr.arange(c['n'], device=row_ptr.device), counts)
+        dst = g_ptr[rid][row] + (tr.arange(c['total'], device=row_ptr.device) - row_ptr[:-1][row])
+        g_vox, g_seg = tr.empty_like(vox), tr.empty_like(seg)
+        g_vox[dst], g_seg[dst] = vox, seg
+        return g_ptr, g_vox, g_seg
 
     def _debug_print(self, debug_los):
         R = tuple(self._ray_shape)

@@ -96,6 +96,23 @@ def test_find_starts_host():
         assert tr.equal(_find_starts_host(g, xt), find_starts(g, xt))
 
 
+def test_trace_order():
+    """ConeCirc detectors are traced in wedges of 5 azimuth columns, radius-major inside (a
+    permutation of each view's pixels); ConeRect and mixed geometries keep the geometry order."""
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom
+    from sph_raytracer_amd.raytracer import _trace_order, _wedge_order
+    p = _wedge_order(7, 12)
+    assert sorted(p.tolist()) == list(range(84))
+    assert p[:7].tolist() == [0, 1, 2, 3, 4, 12, 13]        # wedge 0: columns 0-4, radius 0, 1
+    assert p[35:38].tolist() == [5, 6, 7]                     # wedge 1 starts after 7 x 5 pixels
+    assert p[-2:].tolist() == [82, 83]                        # the last, 2-column wedge
+    circ = sum(ConeCircGeom((7, 12), pos=(3, 0, 1)) for _ in range(2))
+    assert tr.equal(_trace_order(circ, circ.rays), p)
+    rect = ConeRectGeom((7, 12), pos=(3, 0, 1))
+    assert _trace_order(rect, rect.rays) is None
+    assert _trace_order(rect + ConeCircGeom((7, 12), pos=(3, 0, 1)), circ.rays) is None
+
+
 def test_conerectgeom():
     from sph_raytracer_amd import ConeRectGeom
     g = ConeRectGeom((11, 11), (4, 0, 1), fov=(23, 45))
