@@ -14,7 +14,7 @@ if [[ $STEPS == *tests* ]]; then
   tail -3 $OUT/gpu_tests.log
 fi
 if [[ $STEPS == *pmc* ]]; then
-  for c in c2 c3 c5; do
+  for c in c2 c3 c4 c5; do
     timeout -k 10 300 python tools/pmc_forward.py --config $c --reps 5 --out $OUT/${TAG}_forward_${c}_pmc.json > $OUT/pmc_$c.log 2>&1
     cp $OUT/${TAG}_forward_${c}_pmc.json profiles/
     for p in fetch_size write_size sq_waves_sq_insts_valu sq_wait_any_sq_wait_inst_any; do

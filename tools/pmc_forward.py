@@ -33,7 +33,7 @@ def kernel_name(config, dtype='f32'):
     touches the GPU itself)."""
     code = ('import sys, torch; sys.path.insert(0, %r); sys.path.insert(0, %r); import bench; '
             'from sph_raytracer_amd import Operator; cfg = bench.CONFIGS[%r]; '
-            'g, v = bench.build_geometry(cfg, 0, 1); op = Operator(g, v, device=torch.device("cuda", 0)); '
+            'g, v = bench.build_geometry(cfg, 0, 1); op = Operator(g, v, device=torch.device("cuda", 0), dynamic=g.dynamic); '
             'x = torch.rand(cfg[0], device="cuda", dtype=torch.%s); print(op._forward_kernel_name(x))'
             % (ROOT, os.path.join(ROOT, 'tools'), config,
                'float32' if dtype == 'f32' else 'float64'))

@@ -51,17 +51,25 @@ def main():
     dev = torch.device('cuda', 0)
     cfg = bench.CONFIGS[args.config]
     grid, geom = bench.build_geometry(cfg, 0, 1)
-    op = Operator(grid, geom, device=dev)
+    op = Operator(grid, geom, device=dev, dynamic=grid.dynamic)
     n, total = op._csr['n'], op._csr['total']
     x32 = torch.rand(cfg[0], dtype=torch.float32, device=dev)
     x64 = x32.double()
-    o32 = torch.empty(n, dtype=torch.float32, device=dev)
-    o64 = torch.empty(n, dtype=torch.float64, device=dev)
+    n_chan, div, _ = op._layout(x32.shape)      # (a dynamic grid: view i <-> time slice i)
+    o32 = torch.empty(n * (n_chan if div == 0 else 1), dtype=torch.float32, device=dev)
+    o64 = torch.empty(o32.shape, dtype=torch.float64, device=dev)
     if args.only:
         xo, oo = (x32, o32) if args.dtype == 'f32' else (x64, o64)
         for _ in range(args.reps):
-            op._launch_forward(xo, oo, 1, 0)
+            op._launch_forward(xo, oo, n_chan, div)
         torch.cuda.synchronize()
+        return
+    if grid.dynamic:
+        for name, xo, oo in (('forward_f32', x32, o32), ('forward_f64', x64, o64)):
+            us = sorted(graph_time_us(lambda: op._launch_forward(xo, oo, n_chan, div), args.reps)
+                        for _ in range(args.rounds))
+            print(json.dumps({'kernel': name, 'rays': n, 'segments': total,
+                              'us_median': us[len(us) // 2], 'us_min': us[0]}))
         return
     y = torch.rand(n, dtype=torch.float64, device=dev)
     acc = torch.zeros(math.prod(cfg[0]), dtype=torch.float64, device=dev)
