@@ -74,6 +74,14 @@ typedef struct sphrt_rays {
 /* Replaces the per-call conversion of grid.r_b/e_b/a_b inside r_torch/e_torch/a_torch
  * (raytracer.py:271-277, 353-361, 493-501).  `device` is the HIP device ordinal. */
 int sphrt_plan_create(const sphrt_grid_desc *grid, int device, sphrt_plan **out);
+/* The same plan over caller-owned device tables (no hipMalloc, no hipFree: the device-wide sync
+ * hipFree implies is avoided): sphrt_plan_pack_tables writes sphrt_plan_table_bytes(grid) bytes
+ * into host memory, the caller copies them to an 8-byte-aligned device buffer that outlives the
+ * plan (stream-ordered before the plan's first use) and passes it here. */
+size_t sphrt_plan_table_bytes(const sphrt_grid_desc *grid);
+int sphrt_plan_pack_tables(const sphrt_grid_desc *grid, void *host_tables);
+int sphrt_plan_create_external(const sphrt_grid_desc *grid, int device, const void *dev_tables,
+                               sphrt_plan **out);
 int sphrt_plan_destroy(sphrt_plan *plan);
 /* Candidates per ray in the reference's concatenation (raytracer.py:92, 117-122):
  * K = 2(nr+1) + 2(ne+1) + (na+1) + 1. */

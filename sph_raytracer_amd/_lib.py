@@ -54,6 +54,10 @@ MAX_RUNS = 7               # SPHRT_MAX_RUNS
 # (name, restype, argtypes) — mirrors include/sphrt.h one to one
 _SIGNATURES = [
     ('sphrt_plan_create', c_int, [ctypes.POINTER(GridDesc), c_int, ctypes.POINTER(c_vp)]),
+    ('sphrt_plan_table_bytes', ctypes.c_size_t, [ctypes.POINTER(GridDesc)]),
+    ('sphrt_plan_pack_tables', c_int, [ctypes.POINTER(GridDesc), c_vp]),
+    ('sphrt_plan_create_external', c_int, [ctypes.POINTER(GridDesc), c_int, c_vp,
+                                           ctypes.POINTER(c_vp)]),
     ('sphrt_plan_destroy', c_int, [c_vp]),
     ('sphrt_plan_candidates', c_i64, [c_vp]),
     ('sphrt_last_error', ctypes.c_char_p, []),

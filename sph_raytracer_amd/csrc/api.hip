@@ -125,9 +125,9 @@ using namespace sphrt;
 extern "C" const char* sphrt_last_error(void) { return g_err; }
 extern "C" const char* sphrt_version(void) { return SPHRT_VERSION; }
 
-extern "C" int sphrt_plan_create(const sphrt_grid_desc* gd, int device, sphrt_plan** out) {
-    if (!gd || !out) return fail("null argument");
-    *out = nullptr;
+// Validate a grid description; K and the table block size on success.
+static int plan_check(const sphrt_grid_desc* gd, int64_t& K, size_t& bytes) {
+    if (!gd) return fail("null argument");
     // zero-voxel axes are legal for the per-family solves (a single boundary), not for traces
     if (gd->nr < 0 || gd->ne < 0 || gd->na < 0) return fail("grid shape must be non-negative");
     if (gd->nr > 32000 || gd->ne > 32000 || gd->na > 32000)
@@ -137,14 +137,27 @@ extern "C" int sphrt_plan_create(const sphrt_grid_desc* gd, int device, sphrt_pl
     const int nbr = gd->nr + 1, nbe = gd->ne + 1, nba = gd->na + 1;
     for (int j = 1; j < nbr; ++j)
         if (!(gd->r_b[j] >= gd->r_b[j - 1])) return fail("r_b must be ascending");
-    const int64_t K = 2LL * nbr + 2LL * nbe + nba + 1;
+    K = 2LL * nbr + 2LL * nbe + nba + 1;
     if (K >= 65535) return fail("too many boundaries (K=%lld)", (long long)K);
     // table layout: r_b | c2_e | cos_a | sin_a | e_b | a_b (doubles) | e_flags (bytes)
     const size_t nd = (size_t)nbr + 2 * (size_t)nbe + 3 * (size_t)nba;
-    const size_t bytes = nd * sizeof(double) + (size_t)nbe;
-    double* host = (double*)malloc(bytes);
-    if (!host) return fail("host allocation failed");
-    double* h_r = host;
+    bytes = nd * sizeof(double) + (size_t)nbe;
+    return 0;
+}
+
+extern "C" size_t sphrt_plan_table_bytes(const sphrt_grid_desc* gd) {
+    int64_t K;
+    size_t bytes;
+    return plan_check(gd, K, bytes) ? 0 : bytes;
+}
+
+extern "C" int sphrt_plan_pack_tables(const sphrt_grid_desc* gd, void* host_tables) {
+    int64_t K;
+    size_t bytes;
+    if (int e = plan_check(gd, K, bytes)) return e;
+    if (!host_tables) return fail("null table buffer");
+    const int nbr = gd->nr + 1, nbe = gd->ne + 1, nba = gd->na + 1;
+    double* h_r = (double*)host_tables;
     double* h_c2 = h_r + nbr;
     double* h_ca = h_c2 + nbe;
     double* h_sa = h_ca + nba;
@@ -157,15 +170,50 @@ extern "C" int sphrt_plan_create(const sphrt_grid_desc* gd, int device, sphrt_pl
     memcpy(h_sa, gd->sin_a, nba * sizeof(double));
     memcpy(h_eb, gd->e_b, nbe * sizeof(double));
     memcpy(h_ab, gd->a_b, nba * sizeof(double));
-    int e_asc = 1, a_asc = 1;
-    for (int j = 1; j < nbe; ++j) e_asc &= gd->e_b[j] > gd->e_b[j - 1] ? 1 : 0;
-    for (int j = 1; j < nba; ++j) a_asc &= gd->a_b[j] > gd->a_b[j - 1] ? 1 : 0;
     const double half_pi = 3.141592653589793 / 2;  // tr.pi / 2 (raytracer.py:457)
     for (int j = 0; j < nbe; ++j) {
         uint8_t f = 0;
         if (gd->cos_e[j] >= 0.0) f |= 1;
         if (fabs(half_pi - gd->e_b[j]) < gd->close_tol) f |= 2;
         h_fl[j] = f;
+    }
+    return 0;
+}
+
+// The plan over device tables `dmem` (packed by sphrt_plan_pack_tables); owns them if `own`.
+static sphrt_plan* plan_over(const sphrt_grid_desc* gd, int device, void* dmem, bool own,
+                             int64_t K) {
+    sphrt_plan* p = new sphrt_plan;
+    p->device = device;
+    p->table_mem = own ? dmem : nullptr;
+    GridDev& G = p->dev;
+    G.nr = gd->nr; G.ne = gd->ne; G.na = gd->na;
+    G.nbr = gd->nr + 1; G.nbe = gd->ne + 1; G.nba = gd->na + 1;
+    G.K = (int)K;
+    G.a_wrap = gd->a_wrap ? 1 : 0;
+    G.close_tol = gd->close_tol;
+    G.plane_par_tol = gd->plane_par_tol;
+    G.r_outer = gd->r_b[gd->nr];
+    int e_asc = 1, a_asc = 1;
+    for (int j = 1; j < G.nbe; ++j) e_asc &= gd->e_b[j] > gd->e_b[j - 1] ? 1 : 0;
+    for (int j = 1; j < G.nba; ++j) a_asc &= gd->a_b[j] > gd->a_b[j - 1] ? 1 : 0;
+    G.e_asc = e_asc;
+    G.a_asc = a_asc;
+    G.r_b = (const double*)dmem;   // the rest of the block follows it (GridDev accessors)
+    return p;
+}
+
+extern "C" int sphrt_plan_create(const sphrt_grid_desc* gd, int device, sphrt_plan** out) {
+    if (!out) return fail("null argument");
+    *out = nullptr;
+    int64_t K;
+    size_t bytes;
+    if (int e = plan_check(gd, K, bytes)) return e;
+    void* host = malloc(bytes);
+    if (!host) return fail("host allocation failed");
+    if (int e = sphrt_plan_pack_tables(gd, host)) {
+        free(host);
+        return e;
     }
     DeviceGuard guard(device);
     void* dmem = nullptr;
@@ -180,27 +228,29 @@ extern "C" int sphrt_plan_create(const sphrt_grid_desc* gd, int device, sphrt_pl
         (void)hipFree(dmem);
         return fail("hipMemcpy(plan tables) failed: %s", hipGetErrorString(e));
     }
-    sphrt_plan* p = new sphrt_plan;
-    p->device = device;
-    p->table_mem = dmem;
-    GridDev& G = p->dev;
-    G.nr = gd->nr; G.ne = gd->ne; G.na = gd->na;
-    G.nbr = nbr; G.nbe = nbe; G.nba = nba;
-    G.K = (int)K;
-    G.a_wrap = gd->a_wrap ? 1 : 0;
-    G.close_tol = gd->close_tol;
-    G.plane_par_tol = gd->plane_par_tol;
-    G.r_outer = gd->r_b[gd->nr];
-    G.e_asc = e_asc;
-    G.a_asc = a_asc;
-    double* d = (double*)dmem;
-    G.r_b = d;   // the rest of the block follows it (GridDev accessors)
-    *out = p;
+    *out = plan_over(gd, device, dmem, true, K);
+    return 0;
+}
+
+extern "C" int sphrt_plan_create_external(const sphrt_grid_desc* gd, int device,
+                                          const void* dev_tables, sphrt_plan** out) {
+    if (!out) return fail("null argument");
+    *out = nullptr;
+    int64_t K;
+    size_t bytes;
+    if (int e = plan_check(gd, K, bytes)) return e;
+    if (!dev_tables || (uintptr_t)dev_tables % 8 != 0)
+        return fail("device tables missing or not 8-byte aligned");
+    *out = plan_over(gd, device, const_cast<void*>(dev_tables), false, K);
     return 0;
 }
 
 extern "C" int sphrt_plan_destroy(sphrt_plan* plan) {
     if (!plan) return 0;
+    if (!plan->table_mem) {       // caller-owned tables (sphrt_plan_create_external): no hipFree
+        delete plan;
+        return 0;
+    }
     DeviceGuard guard(plan->device);
     hipError_t e = hipFree(plan->table_mem);
     delete plan;

@@ -113,10 +113,41 @@ def _find_starts_host(grid, xs):
 
 # ----- device plumbing ------------------------------------------------------------------------
 
-class _Plan:
-    """Owner of a libsphrt plan: the grid's boundary tables resident on one GPU."""
+class _Staging:
+    """Host byte blobs gathered for one host-to-device copy (the Operator's plan tables, ray
+    spec and start bins go over together instead of as three copies)."""
 
-    def __init__(self, grid, device, boundaries=None):
+    def __init__(self):
+        self._parts, self._offs, self._size = [], [], 0
+        self._dev = None
+
+    def add(self, t):
+        """Register a contiguous CPU tensor; returns its slot."""
+        b = t.contiguous().reshape(-1).view(tr.uint8)
+        self._offs.append(self._size)
+        self._parts.append(b)
+        self._size += -(-b.numel() // 16) * 16              # 16-byte aligned slots
+        if b.numel() % 16:
+            self._parts.append(tr.zeros(16 - b.numel() % 16, dtype=tr.uint8))
+        return len(self._offs) - 1
+
+    def upload(self, dev):
+        self._dev = tr.concat(self._parts).to(dev) if self._parts else None
+
+    def get(self, slot, like):
+        """The device copy of slot `slot` with the dtype and shape of host tensor `like`."""
+        o = self._offs[slot]
+        nb = like.numel() * like.element_size()
+        return self._dev[o:o + nb].view(like.dtype).view(like.shape)
+
+
+class _Plan:
+    """Owner of a libsphrt plan: the grid's boundary tables resident on one GPU.  With a
+    `staging`, the tables are packed on the host and go to the device with the staging's copy:
+    the plan is created by attach() after the upload, over the caller's device copy (no
+    hipMalloc, and no hipFree with its device-wide sync when the plan is destroyed)."""
+
+    def __init__(self, grid, device, boundaries=None, staging=None):
         lib = _lib.load()
         rb, eb, ab = boundaries if boundaries is not None else (grid.r_b, grid.e_b, grid.a_b)
         rb, eb, ab = (tr.asarray(b, dtype=tr.float64).contiguous() for b in (rb, eb, ab))
@@ -137,8 +168,26 @@ class _Plan:
         desc.plane_par_tol = res
         self.shape = (desc.nr, desc.ne, desc.na)
         self.device = device
+        self._desc = desc
+        self.handle = None
+        if staging is not None:
+            host = tr.empty(lib.sphrt_plan_table_bytes(desc), dtype=tr.uint8)
+            _lib.check(lib.sphrt_plan_pack_tables(desc, host.data_ptr()), 'sphrt_plan_pack_tables')
+            self._host, self._slot = host, staging.add(host)
+            return
         h = _lib.c_vp()
         _lib.check(lib.sphrt_plan_create(desc, device.index, h), 'sphrt_plan_create')
+        self.handle = h
+        self.K = lib.sphrt_plan_candidates(h)
+
+    def attach(self, staging):
+        """Create the plan over the staged tables' device copy (after staging.upload)."""
+        lib = _lib.load()
+        self._tables = staging.get(self._slot, self._host)
+        h = _lib.c_vp()
+        _lib.check(lib.sphrt_plan_create_external(self._desc, self.device.index,
+                                                  self._tables.data_ptr(), h),
+                   'sphrt_plan_create_external')
         self.handle = h
         self.K = lib.sphrt_plan_candidates(h)
 
@@ -163,27 +212,48 @@ def _broadcast_pair(xs, rays):
     return shape[:-1], xs, rays
 
 
+class _ConeRays:
+    """Generator inputs of a cone detector's ray directions (sphrt_rays_cone, bit-identical to
+    ``geom.rays``), staged for the device; of() gives None for other geometries (their rays are
+    copied from the host)."""
+
+    @classmethod
+    def of(cls, geom):
+        spec = geom._ray_spec() if hasattr(geom, '_ray_spec') else None
+        if spec is None:
+            return None
+        circ, frame, row, col = (spec[0],) + tuple(t.to(tr.float64).contiguous() for t in spec[1:])
+        shape = tuple(geom.shape)
+        n_views = frame.shape[0] if frame.dim() == 2 else 1
+        h, w = shape[-2], shape[-1]
+        if n_views * h * w != math.prod(shape) or row.shape[-1] != h:
+            return None
+        self = cls()
+        self.circ, self.shape, self.n_views, self.h, self.w = circ, shape, n_views, h, w
+        # (frame, row, col) as one blob
+        self.host = tr.concat([frame.reshape(-1), row.reshape(-1), col.reshape(-1)])
+        self.sizes = [frame.numel(), row.numel(), col.numel()]
+        return self
+
+    def stage(self, staging):
+        self.slot = staging.add(self.host)
+
+    def launch(self, dev, staging=None):
+        """The rays (*shape, 3) on `dev`, from the staged copy or a copy of their own."""
+        packed = staging.get(self.slot, self.host) if staging is not None else self.host.to(dev)
+        frame_d, row_d, col_d = packed.split(self.sizes)
+        rays = tr.empty(self.shape + (3,), dtype=tr.float64, device=dev)
+        _lib.check(_lib.load().sphrt_rays_cone(
+            self.n_views, self.h, self.w, int(self.circ), _lib.ptr(frame_d), _lib.ptr(row_d),
+            _lib.ptr(col_d), _lib.ptr(rays), _lib.stream_of(dev)), 'sphrt_rays_cone')
+        return rays
+
+
 def _device_rays(geom, dev):
     """Cone-detector ray directions generated on the device (sphrt_rays_cone), bit-identical to
     ``geom.rays``; None for other geometries (their rays are copied from the host)."""
-    spec = geom._ray_spec() if hasattr(geom, '_ray_spec') else None
-    if spec is None:
-        return None
-    circ, frame, row, col = (spec[0],) + tuple(t.to(tr.float64).contiguous() for t in spec[1:])
-    shape = tuple(geom.shape)
-    n_views = frame.shape[0] if frame.dim() == 2 else 1
-    h, w = shape[-2], shape[-1]
-    if n_views * h * w != math.prod(shape) or row.shape[-1] != h:
-        return None
-    lib = _lib.load()
-    # one host-to-device copy for the three inputs
-    packed = tr.concat([frame.reshape(-1), row.reshape(-1), col.reshape(-1)]).to(dev)
-    frame_d, row_d, col_d = packed.split([frame.numel(), row.numel(), col.numel()])
-    rays = tr.empty(shape + (3,), dtype=tr.float64, device=dev)
-    _lib.check(lib.sphrt_rays_cone(n_views, h, w, int(circ), _lib.ptr(frame_d), _lib.ptr(row_d),
-                                   _lib.ptr(col_d), _lib.ptr(rays), _lib.stream_of(dev)),
-               'sphrt_rays_cone')
-    return rays
+    cone = _ConeRays.of(geom)
+    return cone.launch(dev) if cone is not None else None
 
 
 def _geom_rays(geom, dev):
@@ -240,23 +310,33 @@ def _permute_rays(rays, perm):
 class _RayBatch:
     """Device copies of the unique starts / directions + the broadcast descriptor."""
 
-    def __init__(self, grid, xs, rays, device):
-        """grid=None: no start voxels (per-family solves only)."""
+    @staticmethod
+    def host_starts(grid, xs):
+        """(starts, start voxels) on the host: float64 (..., 3) and int32 (..., 4)."""
+        xs_u = tr.asarray(xs, dtype=tr.float64).detach().to('cpu').contiguous()
+        st = tr.zeros(xs_u.shape[:-1] + (4,), dtype=tr.int32)
+        if grid is not None:
+            starts = _find_starts_host(grid, xs_u)             # (3, ...) on the host
+            st[..., :3] = starts.moveaxis(0, -1).to(tr.int32)
+        return xs_u, st
+
+    def __init__(self, grid, xs, rays, device, staged=None):
+        """grid=None: no start voxels (per-family solves only).  staged: the device copies of
+        host_starts(grid, xs) (a _Staging's), else they are made here."""
         rshape, xs, rays = _broadcast_pair(xs, rays)
         if len(rshape) > _lib.MAX_DIMS:
             raise ValueError(f'ray batch rank {len(rshape)} > {_lib.MAX_DIMS}')
         self.shape = rshape
         self.n = math.prod(rshape)
-        xs_u = xs.detach().to('cpu').contiguous()
-        st = tr.zeros(xs_u.shape[:-1] + (4,), dtype=tr.int32)
-        if grid is not None:
-            starts = _find_starts_host(grid, xs_u)             # (3, ...) on the host
-            st[..., :3] = starts.moveaxis(0, -1).to(tr.int32)
-        # starts and start voxels in one host-to-device copy
-        xb, sb = xs_u.reshape(-1).view(tr.uint8), st.reshape(-1).view(tr.uint8)
-        packed = tr.concat([xb, sb]).to(device)
-        self.xs = packed[:xb.numel()].view(tr.float64).view(xs_u.shape)
-        self.start = packed[xb.numel():].view(tr.int32).view(st.shape)
+        if staged is not None:
+            self.xs, self.start = staged
+        else:
+            xs_u, st = self.host_starts(grid, xs)
+            # starts and start voxels in one host-to-device copy
+            xb, sb = xs_u.reshape(-1).view(tr.uint8), st.reshape(-1).view(tr.uint8)
+            packed = tr.concat([xb, sb]).to(device)
+            self.xs = packed[:xb.numel()].view(tr.float64).view(xs_u.shape)
+            self.start = packed[xb.numel():].view(tr.int32).view(st.shape)
         self.rays = rays.detach().contiguous().to(device)
         full = rshape + (3,)
         xs_str = self.xs.expand(full).stride()
@@ -640,13 +720,23 @@ class Operator:
 
     def _trace_on(self, dev):
         lib = _lib.load()
-        self._plan = _Plan(self.grid, dev)
-        rays = _geom_rays(self.geom, dev)
+        # plan tables, cone-ray spec and start bins: one host-to-device copy
+        stg = _Staging()
+        self._plan = _Plan(self.grid, dev, staging=stg)
+        cone = _ConeRays.of(self.geom)
+        if cone is not None:
+            cone.stage(stg)
+        xs_h, st_h = _RayBatch.host_starts(self.grid, self.geom.ray_starts)
+        s_xs, s_st = stg.add(xs_h), stg.add(st_h)
+        stg.upload(dev)
+        self._plan.attach(stg)
+        rays = cone.launch(dev, stg) if cone is not None else self.geom.rays
         perm = _trace_order(self.geom, rays)
         ray_id = None
         if perm is not None:           # trace in wedges; rows report their geometry ray
             rays, ray_id = _permute_rays(rays, perm.to(dev, non_blocking=True))
-        batch = _RayBatch(self.grid, self.geom.ray_starts, rays, dev)
+        batch = _RayBatch(self.grid, xs_h, rays, dev,
+                          staged=(stg.get(s_xs, xs_h), stg.get(s_st, st_h)))
         self._ray_shape = batch.shape
         n = batch.n
         stream = _lib.stream_of(dev)
