@@ -113,6 +113,21 @@ def test_trace_order():
     assert _trace_order(rect + ConeCircGeom((7, 12), pos=(3, 0, 1)), circ.rays) is None
 
 
+def test_staging_round_trip():
+    """_Staging (one host-to-device copy for the plan tables, ray spec and start bins): every
+    blob comes back with its dtype, shape and values, at 16-byte aligned offsets."""
+    from sph_raytracer_amd.raytracer import _Staging
+    parts = [tr.arange(7, dtype=tr.uint8), tr.rand(5, 3, dtype=tr.float64),
+             tr.arange(12, dtype=tr.int32).reshape(3, 4), tr.rand(3, dtype=tr.float32)]
+    stg = _Staging()
+    slots = [stg.add(t) for t in parts]
+    stg.upload('cpu')
+    for slot, t in zip(slots, parts):
+        got = stg.get(slot, t)
+        assert got.dtype == t.dtype and got.shape == t.shape and tr.equal(got, t)
+        assert got.data_ptr() % 16 == stg._dev.data_ptr() % 16
+
+
 def test_conerectgeom():
     from sph_raytracer_amd import ConeRectGeom
     g = ConeRectGeom((11, 11), (4, 0, 1), fov=(23, 45))
