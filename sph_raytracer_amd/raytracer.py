@@ -261,7 +261,11 @@ def _geom_rays(geom, dev):
     return geom.rays if rays is None else rays
 
 
-_WEDGE = 5    # azimuth columns per wedge of the ConeCirc trace order
+# azimuth columns per wedge of the ConeCirc trace order; measured (C5 forward f64 / transposed
+# adjoint f64 / retrieval iteration, C4 forward): 2: 46.5 / 42.5 / 0.157 ms, 21.9; 3: 45.8 /
+# 43.5 / 0.157 ms, 21.3; 4: 45.6 / 46.7 / 0.161 ms, 21.1; 5: 45.8 / 47.7 / 0.164 ms, 21.2; 8: 48.0
+# / 48.3 / 0.167 ms, 21.5 us.  SPHRT_WEDGE overrides it (A/B studies).
+_WEDGE = int(os.environ.get('SPHRT_WEDGE', '3'))
 
 
 def _trace_order(geom, rays):
@@ -269,10 +273,9 @@ def _trace_order(geom, rays):
 
     ConeCirc pixels are (radius, azimuth) with the azimuth fastest: ~36 consecutive rays (one
     workgroup block at C5) sweep most of a ring, whose rays part around the view axis.  Wedges of
-    _WEDGE azimuth columns, radius-major inside, keep a block's rays together: granules per
-    block 1105 -> 770 at C5 (oracle study), forward f32 33.5 -> 28.4 us, f64 53.7 -> 44.2 us,
-    transposed adjoint f64 56.1 -> 47.6 us (tools/exp studies; ConeRect rows are already
-    compact: strips beat every tiling measured).  Only the order of the CSR's rows changes: every
+    _WEDGE azimuth columns, radius-major inside, keep a block's rays together: C5 table stride
+    1536 -> 1024, forward f32 33.2 -> 29.5 us, f64 52.7 -> 45.8 us, transposed adjoint f64 53.4
+    -> 43.5 us (ConeRect rows are already compact: strips beat every tiling measured).  Only the order of the CSR's rows changes: every
     row reports its geometry ray (sphrt_csr_index ray_ids), outputs stay in geometry order.
     SPHRT_RAY_ORDER=natural keeps the geometry order."""
     if os.environ.get('SPHRT_RAY_ORDER', 'auto') == 'natural':

@@ -97,15 +97,17 @@ def test_find_starts_host():
 
 
 def test_trace_order():
-    """ConeCirc detectors are traced in wedges of 5 azimuth columns, radius-major inside (a
+    """ConeCirc detectors are traced in wedges of _WEDGE azimuth columns, radius-major inside (a
     permutation of each view's pixels); ConeRect and mixed geometries keep the geometry order."""
     from sph_raytracer_amd import ConeCircGeom, ConeRectGeom
-    from sph_raytracer_amd.raytracer import _trace_order, _wedge_order
+    from sph_raytracer_amd.raytracer import _WEDGE, _trace_order, _wedge_order
     p = _wedge_order(7, 12)
     assert sorted(p.tolist()) == list(range(84))
-    assert p[:7].tolist() == [0, 1, 2, 3, 4, 12, 13]        # wedge 0: columns 0-4, radius 0, 1
-    assert p[35:38].tolist() == [5, 6, 7]                     # wedge 1 starts after 7 x 5 pixels
-    assert p[-2:].tolist() == [82, 83]                        # the last, 2-column wedge
+    w = _WEDGE
+    assert p[:w + 2].tolist() == list(range(w)) + [12, 13]   # wedge 0: radius 0, then 1
+    assert p[7 * w:7 * w + 2].tolist() == [w, w + 1]         # wedge 1 after 7 x w pixels
+    last = 12 - (12 // w) * w or w                            # the last wedge's width
+    assert p[-last:].tolist() == list(range(84 - last, 84))
     circ = sum(ConeCircGeom((7, 12), pos=(3, 0, 1)) for _ in range(2))
     assert tr.equal(_trace_order(circ, circ.rays), p)
     rect = ConeRectGeom((7, 12), pos=(3, 0, 1))
