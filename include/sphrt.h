@@ -306,6 +306,16 @@ int sphrt_sq_residual_f64(const double *yhat, const void *y, int y_is_f64, int64
                           double *r_scaled, double *partial_sums, void *stream);
 int sphrt_neg_reg_f64(const double *d, int64_t n, double c_neg, double *g, double *partial_sums,
                       void *stream);
+/* One Adam step on float64 coefficients (torch.optim.Adam(fused=True), amsgrad and maximize off:
+ * torch._fused_adam_'s per-element arithmetic, bitwise), step = the step count after this step's
+ * increment (1, 2, ...).  With partial_sums set, the NegRegularizer is folded in first, as
+ * sphrt_neg_reg_f64 on d = param before the step (grad itself is not modified); NULL: no
+ * regulariser.  Replaces, per retrieval iteration, the reference's optim.step() after
+ * tot_loss.backward() (retrieval.py:115-116; loss.py:140-162 for the regulariser term). */
+int sphrt_adam_neg_f64(double *param, const double *grad, double *exp_avg, double *exp_avg_sq,
+                       int64_t n, double lr, double beta1, double beta2, double eps,
+                       double weight_decay, double step, double c_neg, double *partial_sums,
+                       void *stream);
 
 /* ---- fused no-store mode: trace + integrate in one pass (nothing persisted) --------------- */
 int sphrt_trace_integrate_f32(const sphrt_plan *plan, const sphrt_rays *rays,

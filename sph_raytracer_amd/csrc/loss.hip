@@ -69,6 +69,44 @@ __global__ __launch_bounds__(kLossThreads) void neg_reg_kernel(
     block_partial(acc, part);
 }
 
+// Adam (torch.optim.Adam with fused=True: torch._fused_adam_'s per-element arithmetic, amsgrad
+// and maximize off) on float64 coefficients, with the NegRegularizer's gradient term and loss
+// partials folded in: one launch where the loop made three (neg_reg, the step-count add, the
+// fused step on 36 pieces).  The multiply-adds are the fused ones torch's ROCm build emits for
+// `beta1 * m + (1 - beta1) * g` and `beta2 * v + (1 - beta2) * g * g` (fma of the left product,
+// and of p * weight_decay + g), written out here since this library builds with
+// -ffp-contract=off: measured bitwise equal to torch._fused_adam_ over 20 steps with and without
+// weight decay, where the unfused and the right-product forms differ from step 1
+// (`test_adam_matches_torch_fused`).  Bias corrections from the device's pow and sqrt, as torch's
+// kernel computes them from its float32 step count.
+__global__ __launch_bounds__(kLossThreads) void adam_neg_kernel(
+    double* __restrict__ param, const double* __restrict__ grad, double* __restrict__ exp_avg,
+    double* __restrict__ exp_avg_sq, int64_t n, double lr, double beta1, double beta2, double eps,
+    double weight_decay, double step, double c_neg, double* __restrict__ part) {
+    const double bc1 = 1 - pow(beta1, step);
+    const double bc2s = sqrt(1 - pow(beta2, step));
+    const double step_size = lr / bc1;
+    const double ob1 = 1 - beta1, ob2 = 1 - beta2;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kLossThreads + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kLossThreads) {
+        double p = param[i], g = grad[i];
+        if (part) {                                        // as neg_reg_kernel
+            const double c = p > 0.0 ? 0.0 : p;
+            acc += __builtin_fabs(c);
+            if (p < 0.0) g = g - c_neg;
+        }
+        if (weight_decay != 0) g = fma(p, weight_decay, g);
+        const double m = fma(beta1, exp_avg[i], ob1 * g);
+        const double v = fma(beta2, exp_avg_sq[i], ob2 * g * g);
+        const double denom = sqrt(v) / bc2s + eps;
+        param[i] = p - step_size * m / denom;
+        exp_avg[i] = m;
+        exp_avg_sq[i] = v;
+    }
+    if (part) block_partial(acc, part);
+}
+
 static unsigned loss_grid(int64_t n) {
     const int64_t b = (n + kLossThreads - 1) / kLossThreads;
     return (unsigned)(b < kLossMaxBlocks ? (b > 0 ? b : 1) : kLossMaxBlocks);
@@ -104,4 +142,18 @@ extern "C" int sphrt_neg_reg_f64(const double* d, int64_t n, double c_neg, doubl
     hipLaunchKernelGGL(neg_reg_kernel, dim3(loss_grid(n)), dim3(kLossThreads), 0,
                        (hipStream_t)stream, d, n, c_neg, g, partial_sums);
     return check_launch("neg_reg");
+}
+
+extern "C" int sphrt_adam_neg_f64(double* param, const double* grad, double* exp_avg,
+                                  double* exp_avg_sq, int64_t n, double lr, double beta1,
+                                  double beta2, double eps, double weight_decay, double step,
+                                  double c_neg, double* partial_sums, void* stream) {
+    if (n <= 0) return fail("sphrt_adam_neg_f64: empty volume");
+    if (!param || !grad || !exp_avg || !exp_avg_sq) return fail("null buffer");
+    if (!(step >= 1)) return fail("sphrt_adam_neg_f64: step counts from 1");
+    StreamGuard guard(stream);
+    hipLaunchKernelGGL(adam_neg_kernel, dim3(loss_grid(n)), dim3(kLossThreads), 0,
+                       (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2,
+                       eps, weight_decay, step, c_neg, partial_sums);
+    return check_launch("adam_neg");
 }

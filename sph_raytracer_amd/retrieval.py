@@ -159,8 +159,9 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     """`gd` for `_direct_plan` loops: the same arithmetic as autograd's, op by op, so the
     iterates are the same (the Operator forward, the adjoint of the SquareLoss residual, the
     NegRegularizer's -lam/N on negative voxels, the optimiser step), without building and walking
-    a graph every iteration: one forward, one adjoint, the two fused loss tails of
-    csrc/loss.hip and the optimiser step.  The loss values are the fused kernels' partial sums,
+    a graph every iteration: one forward, one adjoint, the residual kernel of csrc/loss.hip
+    and the optimiser step (for Adam, one csrc/loss.hip launch that also applies the
+    regulariser; otherwise its own kernel, then opt.step()).  The loss values are the fused kernels' partial sums,
     summed for all iterations after the loop: deterministic, within rounding of the autograd
     loop's torch.mean.
 
@@ -215,7 +216,10 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                     2 * c_sq, _lib.ptr(r_scaled), _lib.ptr(part_sq[it]), stream),
                     'sphrt_sq_residual_f64')
                 g = f._apply_adjoint(r_scaled, tuple(d.shape), d.dtype, d.device)
-                if neg is not None:
+                if step is not None:
+                    # the regulariser's gradient term and loss partials inside the Adam launch
+                    step(g, c_neg, part_neg[it] if neg is not None else None, stream)
+                elif neg is not None:
                     # g -= lam/N where d < 0, and the partial sums of |clamp(d, max=0)|
                     _lib.check(lib.sphrt_neg_reg_f64(_lib.ptr(d), n_vox, c_neg, _lib.ptr(g),
                                                      _lib.ptr(part_neg[it]), stream),
@@ -224,9 +228,7 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                     fv = float(scaled(part_sq[it], n_meas, sq.lam))
                     rv = float(scaled(part_neg[it], n_vox, neg.lam)) if neg is not None else 0
                     bar.describe(f'F:{fv:.1e} R:{rv:.1e} O:0')
-                if step is not None:
-                    step(g)
-                else:
+                if step is None:
                     coeffs.grad = g
                     opt.step()
                 done = it + 1
@@ -242,13 +244,15 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
 
 
 def _split_fused_adam(opt, coeffs):
-    """torch.optim.Adam(fused=True)'s step on `coeffs` as a function of the gradient, or None.
+    """torch.optim.Adam(fused=True)'s step on `coeffs` as one sphrt_adam_neg_f64 launch, or None.
 
     The fused step (torch._fused_adam_) runs one workgroup per 65536-element chunk of each
-    tensor: a 64^3 volume is 4 workgroups on a 256-CU GPU (78 us of a 0.32 ms C5 iteration).
-    The same step over up to 36 contiguous pieces of the volume (the most one launch takes) runs
-    the same per-element arithmetic (bitwise the same iterates) on up to 36 workgroups; the
-    optimiser's own state is left untouched (the loop owns the moments)."""
+    tensor: a 64^3 volume is 4 workgroups on a 256-CU GPU (78 us of a 0.32 ms C5 iteration; on
+    36 contiguous pieces, the most one launch takes, 15 us plus 5 us for the step counts).
+    csrc/loss.hip runs the same per-element arithmetic (bitwise: test_adam_matches_torch_fused)
+    over the whole volume with the NegRegularizer's gradient term folded in, ~4 us.  The
+    optimiser's own state is left untouched (the loop owns the moments and the step count)."""
+    from . import _lib
     if type(opt) is not t.optim.Adam or len(opt.param_groups) != 1:
         return None
     grp = opt.param_groups[0]
@@ -257,22 +261,18 @@ def _split_fused_adam(opt, coeffs):
             and not grp.get('decoupled_weight_decay') and isinstance(grp['lr'], float)
             and len(grp['params']) == 1 and grp['params'][0] is coeffs):
         return None
-    n = coeffs.numel()
-    pieces = max(1, min(36, -(-n // 4096)))
-    size = -(-(-(-n // pieces)) // 64) * 64          # a multiple of 64 elements per piece
-    sizes = [min(size, n - i) for i in range(0, n, size)]
+    lib = _lib.load()
     flat = coeffs.detach().view(-1)
     m, v = t.zeros_like(flat), t.zeros_like(flat)
-    params, ms, vs = flat.split(sizes), m.split(sizes), v.split(sizes)
-    steps = [t.zeros((), dtype=t.float32, device=coeffs.device) for _ in sizes]
-    b1, b2 = grp['betas']
+    b1, b2 = (float(b) for b in grp['betas'])
+    lr, eps, wd = float(grp['lr']), float(grp['eps']), float(grp['weight_decay'])
+    count = [0]
 
-    def step(g):
-        t._foreach_add_(steps, 1)
-        t._fused_adam_(list(params), list(g.view(-1).split(sizes)), list(ms), list(vs), [], steps,
-                       amsgrad=False, lr=grp['lr'], beta1=b1, beta2=b2,
-                       weight_decay=grp['weight_decay'], eps=grp['eps'], maximize=False,
-                       grad_scale=None, found_inf=None)
+    def step(g, c_neg, part, stream):
+        count[0] += 1
+        _lib.check(lib.sphrt_adam_neg_f64(_lib.ptr(flat), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v),
+                                          flat.numel(), lr, b1, b2, eps, wd, float(count[0]),
+                                          c_neg, _lib.ptr(part), stream), 'sphrt_adam_neg_f64')
     return step
 
 

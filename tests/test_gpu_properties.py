@@ -788,6 +788,44 @@ def test_run_records(c2, gpu, monkeypatch):
     assert np.allclose(yf, ref, rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.parametrize('wd', [0.0, 0.01])
+@pytest.mark.parametrize('c_neg', [None, 0.3])
+def test_adam_matches_torch_fused(wd, c_neg, gpu):
+    """sphrt_adam_neg_f64 (the retrieval loop's one-launch regulariser + Adam step) gives
+    torch._fused_adam_'s parameters and moments bitwise over 20 steps of gradients spanning four
+    decades, with and without weight decay; with the regulariser folded in, the same as
+    sphrt_neg_reg_f64 on the gradient first (gradient and loss partials)."""
+    from sph_raytracer_amd import _lib
+    lib = _lib.load()
+    n = 70001                                   # ragged: not a multiple of the workgroup
+    gen = tr.Generator(device='cpu').manual_seed(3)
+    p0 = tr.randn(n, generator=gen, dtype=tr.float64).to(gpu)
+    pa, pb = p0.clone(), p0.clone()
+    ma, va, mb, vb = (tr.zeros(n, dtype=tr.float64, device=gpu) for _ in range(4))
+    steps = [tr.zeros((), dtype=tr.float32, device=gpu)]
+    np_ = lib.sphrt_loss_partials(n)
+    stream = _lib.stream_of(gpu)
+    for it in range(20):
+        g = tr.randn(n, generator=gen, dtype=tr.float64).to(gpu) * 10.0 ** (it % 4 - 2)
+        ga = g.clone()
+        part_a = tr.empty(np_, dtype=tr.float64, device=gpu)
+        part_b = tr.full((np_,), float('nan'), dtype=tr.float64, device=gpu)
+        if c_neg is not None:
+            _lib.check(lib.sphrt_neg_reg_f64(_lib.ptr(pa), n, c_neg, _lib.ptr(ga),
+                                             _lib.ptr(part_a), stream), 'neg_reg')
+        tr._foreach_add_(steps, 1)
+        tr._fused_adam_([pa], [ga], [ma], [va], [], steps, amsgrad=False, lr=0.01, beta1=0.9,
+                        beta2=0.999, weight_decay=wd, eps=1e-8, maximize=False, grad_scale=None,
+                        found_inf=None)
+        _lib.check(lib.sphrt_adam_neg_f64(
+            _lib.ptr(pb), _lib.ptr(g), _lib.ptr(mb), _lib.ptr(vb), n, 0.01, 0.9, 0.999, 1e-8, wd,
+            float(it + 1), c_neg or 0.0, _lib.ptr(part_b if c_neg is not None else None),
+            stream), 'adam_neg')
+        assert tr.equal(pa, pb) and tr.equal(ma, mb) and tr.equal(va, vb), it
+        if c_neg is not None:
+            assert tr.equal(part_a, part_b), it
+
+
 @pytest.mark.parametrize('lams, meas_dtype', [((1, 1), tr.float64), ((0.5, 2), tr.float64),
                                               ((1, None), tr.float32)])
 def test_gd_direct_matches_autograd(lams, meas_dtype, gpu, monkeypatch):
