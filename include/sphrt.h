@@ -296,14 +296,16 @@ int sphrt_f64_to_f32(const double *src, float *dst, int64_t n, void *stream);
 
 /* ---- retrieval loss tails (csrc/loss.hip; retrieval._gd_direct) ------------------------------
  * SquareLoss: r = yhat - y (y float32 or float64, promoted), r_scaled = r * scale, and the
- * partial sums of r * r.  NegRegularizer: g -= c_neg where d < 0, and the partial sums of
+ * partial sums of r * r; with `order` (NULL: identity), r_scaled[j] is ray order[j]'s (a
+ * trace's sphrt_csr_index ray_ids: the transposed adjoint's input in trace order).  NegRegularizer: g -= c_neg where d < 0, and the partial sums of
  * |clamp(d, max=0)|.  The elementwise values are single IEEE operations, the values torch's
  * elementwise ops give (reference loss.py:87-162).  Each call writes sphrt_loss_partials(n)
  * partial sums (fixed partition and order); the loss is their sum / n, within rounding of
  * torch.mean. */
 int64_t sphrt_loss_partials(int64_t n);
 int sphrt_sq_residual_f64(const double *yhat, const void *y, int y_is_f64, int64_t n, double scale,
-                          double *r_scaled, double *partial_sums, void *stream);
+                          const int32_t *order, double *r_scaled, double *partial_sums,
+                          void *stream);
 int sphrt_neg_reg_f64(const double *d, int64_t n, double c_neg, double *g, double *partial_sums,
                       void *stream);
 /* One Adam step on float64 coefficients (torch.optim.Adam(fused=True), amsgrad and maximize off:

@@ -96,7 +96,7 @@ _SIGNATURES = [
                                     ctypes.c_size_t, c_vp]),
     ('sphrt_f64_to_f32', c_int, [c_vp, c_vp, c_i64, c_vp]),
     ('sphrt_loss_partials', c_i64, [c_i64]),
-    ('sphrt_sq_residual_f64', c_int, [c_vp, c_vp, c_int, c_i64, c_dbl, c_vp, c_vp, c_vp]),
+    ('sphrt_sq_residual_f64', c_int, [c_vp, c_vp, c_int, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp]),
     ('sphrt_neg_reg_f64', c_int, [c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp]),
     ('sphrt_adam_neg_f64', c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl,
                                    c_dbl, c_dbl, c_vp, c_vp]),

@@ -18,7 +18,7 @@
 namespace sphrt {
 
 constexpr int kLossThreads = 256;
-constexpr int kLossMaxBlocks = 256;
+constexpr int kLossMaxBlocks = 1024;   // (a 64^3 volume: one element per thread)
 
 // Workgroup sum in a fixed order (wave shuffles, then the four wave totals in order); thread 0
 // stores it.  No cross-workgroup step: the partials of every iteration are summed after the loop
@@ -38,16 +38,18 @@ __device__ __forceinline__ void block_partial(double v, double* out) {
 }
 
 // r = yhat - y (y float32 or float64, promoted exactly); r_scaled = r * scale; partial sums of
-// r * r.
+// r * r.  With `order` (a trace's row -> geometry ray map), r_scaled[j] is the residual of ray
+// order[j]: the transposed adjoint's input in trace order, without a separate permutation.
 template <typename TY>
 __global__ __launch_bounds__(kLossThreads) void sq_residual_kernel(
     const double* __restrict__ yhat, const TY* __restrict__ y, int64_t n, double scale,
-    double* __restrict__ r_scaled, double* __restrict__ part) {
+    const int32_t* __restrict__ order, double* __restrict__ r_scaled, double* __restrict__ part) {
     double acc = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kLossThreads + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * kLossThreads) {
+    for (int64_t j = (int64_t)blockIdx.x * kLossThreads + threadIdx.x; j < n;
+         j += (int64_t)gridDim.x * kLossThreads) {
+        const int64_t i = order ? (int64_t)order[j] : j;
         const double r = yhat[i] - (double)y[i];
-        r_scaled[i] = r * scale;
+        r_scaled[j] = r * scale;
         acc += r * r;
     }
     block_partial(acc, part);
@@ -109,7 +111,11 @@ __global__ __launch_bounds__(kLossThreads) void adam_neg_kernel(
 
 static unsigned loss_grid(int64_t n) {
     const int64_t b = (n + kLossThreads - 1) / kLossThreads;
-    return (unsigned)(b < kLossMaxBlocks ? (b > 0 ? b : 1) : kLossMaxBlocks);
+    static const int64_t cap = [] {   // SPHRT_LOSS_BLOCKS: A/B studies
+        const char* e = getenv("SPHRT_LOSS_BLOCKS");
+        return (int64_t)(e ? atoi(e) : kLossMaxBlocks);
+    }();
+    return (unsigned)(b < cap ? (b > 0 ? b : 1) : cap);
 }
 
 }  // namespace sphrt
@@ -119,18 +125,18 @@ using namespace sphrt;
 extern "C" int64_t sphrt_loss_partials(int64_t n) { return n > 0 ? (int64_t)loss_grid(n) : 0; }
 
 extern "C" int sphrt_sq_residual_f64(const double* yhat, const void* y, int y_is_f64, int64_t n,
-                                     double scale, double* r_scaled, double* partial_sums,
-                                     void* stream) {
+                                     double scale, const int32_t* order, double* r_scaled,
+                                     double* partial_sums, void* stream) {
     if (n <= 0) return fail("sphrt_sq_residual_f64: empty measurement");
     if (!yhat || !y || !r_scaled || !partial_sums) return fail("null buffer");
     StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     if (y_is_f64)
         hipLaunchKernelGGL(sq_residual_kernel<double>, dim3(loss_grid(n)), dim3(kLossThreads), 0,
-                           st, yhat, (const double*)y, n, scale, r_scaled, partial_sums);
+                           st, yhat, (const double*)y, n, scale, order, r_scaled, partial_sums);
     else
         hipLaunchKernelGGL(sq_residual_kernel<float>, dim3(loss_grid(n)), dim3(kLossThreads), 0,
-                           st, yhat, (const float*)y, n, scale, r_scaled, partial_sums);
+                           st, yhat, (const float*)y, n, scale, order, r_scaled, partial_sums);
     return check_launch("sq_residual");
 }
 

@@ -988,11 +988,20 @@ class Operator:
         csr[key] = dict(desc=c, keep=(vox_p, blocks_p, loc, tab, runs), n_t=T)
         return csr[key]
 
-    def _apply_adjoint(self, y, dshape, ddtype, ddevice):
+    def _apply_adjoint(self, y, dshape, ddtype, ddevice, trace_order=False):
         with tr.cuda.device(self._cdev):
-            return self._apply_adjoint_on(y, dshape, ddtype, ddevice)
+            return self._apply_adjoint_on(y, dshape, ddtype, ddevice, trace_order)
 
-    def _apply_adjoint_on(self, y, dshape, ddtype, ddevice):
+    def _adjoint_trace_order(self):
+        """The row -> geometry ray map (int32, device) when the adjoint takes its input in
+        trace order (static, transposed adjoint, a reordered trace), else None."""
+        csr = self._csr
+        if self.grid.dynamic or self.adjoint_mode != 'transpose' or csr is None:
+            return None
+        return csr['ray_id']
+
+    def _apply_adjoint_on(self, y, dshape, ddtype, ddevice, trace_order=False):
+        """trace_order: y is already in trace order (_adjoint_trace_order's map applied)."""
         dev = self._cdev
         n_chan, div, out_shape = self._layout(dshape)
         csr = self._csr
@@ -1006,7 +1015,7 @@ class Operator:
         if self.adjoint_mode == 'transpose' and (div == 0 or paired is not None):
             cdt = ddtype if ddtype in (tr.float32, tr.float64) else tr.float32
             yv = yv.to(cdt)
-            if csr['ray_id'] is not None:   # the transpose's columns are trace rows
+            if csr['ray_id'] is not None and not trace_order:   # its columns are trace rows
                 yv = yv.view(-1, n).index_select(1, self._ray_id_long()).reshape(-1)
             if paired is not None:      # columns of the flattened (T, vol) density
                 if 'transposed' not in paired:

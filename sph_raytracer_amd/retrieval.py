@@ -186,6 +186,9 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     bar = _Bar(range(num_iterations), progress_bar)
     lib = _lib.load()
     n_meas, n_vox = yd.numel(), coeffs.numel()
+    order = f._adjoint_trace_order()
+    if order is not None and order.numel() != n_meas:
+        order = None
     # every iteration's loss as the workgroup partial sums of its fused kernel, one row per
     # iteration, summed once after the loop (no reduction launch, no host sync per iteration)
     ps, pn = lib.sphrt_loss_partials(n_meas), lib.sphrt_loss_partials(n_vox)
@@ -210,12 +213,14 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                                      f'output {tuple(yhat.shape)}')
                 # r = f(d) - y, r * (2 lam / N) (the adjoint's input) and the partial sums of
                 # r * r (the loss) in one launch (csrc/loss.hip)
+                # (in the trace's ray order when the adjoint takes that: no permutation launch)
                 r_scaled = t.empty_like(yhat)
                 _lib.check(lib.sphrt_sq_residual_f64(
                     _lib.ptr(yhat), _lib.ptr(yd), int(yd.dtype == t.float64), n_meas,
-                    2 * c_sq, _lib.ptr(r_scaled), _lib.ptr(part_sq[it]), stream),
+                    2 * c_sq, _lib.ptr(order), _lib.ptr(r_scaled), _lib.ptr(part_sq[it]), stream),
                     'sphrt_sq_residual_f64')
-                g = f._apply_adjoint(r_scaled, tuple(d.shape), d.dtype, d.device)
+                g = f._apply_adjoint(r_scaled, tuple(d.shape), d.dtype, d.device,
+                                     trace_order=order is not None)
                 if step is not None:
                     # the regulariser's gradient term and loss partials inside the Adam launch
                     step(g, c_neg, part_neg[it] if neg is not None else None, stream)
