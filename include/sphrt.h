@@ -210,6 +210,12 @@ typedef struct sphrt_csr {
     /* (optional, sphrt_csr_runs) per block SPHRT_RUN_FIELDS int32: its rows' rays and its share
      * of the empty rays as ranges; NULL: the forward reads row_ray / empty_ray instead. */
     const int32_t *runs;
+    /* Block order of the forward (a performance hint: results are identical).  0: the default
+     * order; 1: reversed.  A caller streaming two CSRs in turn that together outgrow the
+     * memory-side cache (the retrieval loop's forward and transposed adjoint, C5: 2 x ~165 MB)
+     * flips it every iteration, so each launch starts on the lines the previous one left cached
+     * instead of the ones it evicted first (C5 retrieval 0.138 -> 0.133 ms/iteration). */
+    int64_t order;
 } sphrt_csr;
 
 int64_t sphrt_csr_blocks(int64_t n_segments);

@@ -41,7 +41,7 @@ class CSR(ctypes.Structure):
                 ('n_fallback', c_i64), ('empty_ray', c_vp), ('tab_stride', c_i64),
                 ('tab_bytes', c_i64), ('stage_shape', ctypes.c_int32 * 3),
                 ('stage_brick', ctypes.c_int32 * 3), ('stage_cols', c_i64), ('stage', c_vp),
-                ('stage_bytes', c_i64), ('runs', c_vp)]
+                ('stage_bytes', c_i64), ('runs', c_vp), ('order', c_i64)]
 
 
 ROW_HEAD = 0x80000000

@@ -953,7 +953,12 @@ __device__ __forceinline__ uint32_t window_chunk(const RawChunk<L, LOCAL, P>& r,
 // XCD), so blocks that gather the same lines share an L2; 0 keeps dispatch order.  Bijective for
 // any grid size.  Chosen per launch by fwd_chunk().
 __device__ __forceinline__ int64_t block_of(int chunk) {
-    const uint32_t n = gridDim.x, b = blockIdx.x;
+    const uint32_t n = gridDim.x;
+    uint32_t b = blockIdx.x;
+    if (chunk < 0) {                 // ~chunk, blocks in reverse order
+        chunk = ~chunk;
+        b = n - 1 - b;
+    }
     if (chunk <= 0) return (int64_t)b;
     const uint32_t q = n / 8, r = n % 8, x = b % 8, i = b / 8, k = (uint32_t)chunk;
     if (k > q) return (int64_t)((x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i);
@@ -1661,10 +1666,10 @@ static int fwd_chunk(const sphrt_csr* c, size_t elem) {
         const char* e = getenv("SPHRT_XCD_CHUNK");
         return e ? atoi(e) : -1;
     }();
-    if (forced >= 0) return forced;
-    if (c->n_cols * (int64_t)elem > (int64_t)(4 << 20)) return 64;
-    if (c->n_blocks <= 256 * 6) return INT32_MAX;
-    return 0;
+    int k = forced >= 0 ? forced
+            : c->n_cols * (int64_t)elem > (int64_t)(4 << 20) ? 64
+            : c->n_blocks <= 256 * 6 ? INT32_MAX : 0;
+    return (c->order & 1) ? ~k : k;   // (block_of: reversed)
 }
 
 template <typename T, typename L>

@@ -788,6 +788,33 @@ def test_run_records(c2, gpu, monkeypatch):
     assert np.allclose(yf, ref, rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.parametrize('kind, grid_shape', [('rect', (20, 20, 20)), ('circ', (96, 96, 96))])
+def test_block_order_hint(kind, grid_shape, gpu):
+    """sphrt_csr.order = 1 (blocks in reverse order) changes nothing but the order: forward
+    (float32, float64) and transposed adjoint bitwise equal to order 0, for a one-wave launch
+    (one contiguous range per XCD) and a multi-wave one (dispatch order for float32, runs of 64
+    blocks per XCD for float64, brick staging)."""
+    from sph_raytracer_amd import Operator
+    small = kind == 'rect'
+    grid, geom = _orbit(8 if small else 64, (16, 24) if small else (32, 64), kind=kind,
+                        grid_shape=grid_shape)
+    op = Operator(grid, geom, device=gpu)
+    assert (op._csr['desc'].n_blocks > 256 * 6) == (not small)
+    g = tr.Generator(device='cpu').manual_seed(5)
+    x = tr.rand(grid.shape, dtype=tr.float64, generator=g).to(gpu)
+    y = tr.rand(tuple(geom.shape), dtype=tr.float64, generator=g).to(gpu)
+    descs = [op._csr['desc'], op._transposed()['desc']]
+    outs = []
+    for order in (0, 1):
+        for dsc in descs:
+            dsc.order = order
+        outs.append((op(x.float()), op(x), op.T(y)))
+    for dsc in descs:
+        dsc.order = 0
+    for a, b in zip(*outs):
+        assert tr.equal(a, b)
+
+
 @pytest.mark.parametrize('wd', [0.0, 0.01])
 @pytest.mark.parametrize('c_neg', [None, 0.3])
 def test_adam_matches_torch_fused(wd, c_neg, gpu):
