@@ -211,10 +211,11 @@ typedef struct sphrt_csr {
      * of the empty rays as ranges; NULL: the forward reads row_ray / empty_ray instead. */
     const int32_t *runs;
     /* Block order of the forward (a performance hint: results are identical).  0: the default
-     * order; 1: reversed.  A caller streaming two CSRs in turn that together outgrow the
-     * memory-side cache (the retrieval loop's forward and transposed adjoint, C5: 2 x ~165 MB)
-     * flips it every iteration, so each launch starts on the lines the previous one left cached
-     * instead of the ones it evicted first (C5 retrieval 0.138 -> 0.133 ms/iteration). */
+     * order; 1: reversed.  The Python layer flips it after every launch of a CSR of more than one
+     * resident wave of blocks, so a CSR (or a forward / adjoint pair) that outgrows the
+     * memory-side cache starts each launch on the lines the previous launch left cached instead
+     * of the ones it evicted first (C3 forward f32 233 -> 213 us; C5 retrieval 0.138 -> 0.133
+     * ms/iteration). */
     int64_t order;
 } sphrt_csr;
 

@@ -111,6 +111,8 @@ PyObject* py_add(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     Py_RETURN_NONE;
 }
 
+constexpr int64_t kAlternateMinBlocks = 256 * 6;   // raytracer._ALTERNATE_MIN_BLOCKS
+
 // forward(capsule, density) -> Tensor, or None when no binding applies
 PyObject* py_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     if (nargs != 2) {
@@ -146,6 +148,11 @@ PyObject* py_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
         }
         const int rc = x.fn(csr, d.const_data_ptr(), x.n_chan, x.n_vox, x.div,
                             out.mutable_data_ptr(), x.n, stream);
+        // multi-wave CSRs alternate their block order from call to call (raytracer._alternate)
+        if (rc == 0) {
+            auto* c = static_cast<sphrt_csr*>(const_cast<void*>(x.csr));
+            if (c->n_blocks > kAlternateMinBlocks) c->order ^= 1;
+        }
         if (rc != 0) {
             const std::string msg = std::string("sphrt_forward: ") +
                                     (b->last_error ? b->last_error() : "failed");

@@ -541,6 +541,21 @@ def _stage_bytes(desc, n_chan, elem):
     return n_chan * desc.stage_cols * elem if desc.stage_shape[0] > 0 else 0
 
 
+# Launches of more blocks than one resident wave (6 workgroups per CU) alternate their block order
+# (sphrt_csr.order) from call to call: a CSR that outgrows the memory-side cache then starts each
+# launch on the lines the previous launch touched last, which are the ones still cached, instead
+# of the ones it evicted first.  Same results.  Measured on repeated forwards (tools/prof, MI355X):
+# C3 f32 233 -> 213 us, f64 364 -> 350 us, C5 f32 29.3 -> 28.3 us; one-wave launches (C2) gain
+# nothing and keep their order.  The C++ fast path (csrc/fastpath.cpp) applies the same rule.
+_ALTERNATE_MIN_BLOCKS = 256 * 6
+
+
+def _alternate(desc):
+    """Flip a multi-wave CSR's block order for its next launch."""
+    if desc.n_blocks > _ALTERNATE_MIN_BLOCKS:
+        desc.order ^= 1
+
+
 def _call_forward(fn, desc, d, n_chan, cs, div, out, ocs, dev):
     """sphrt_forward_f32/_f64 on the current stream of `dev`.  A brick-staged CSR gets this
     call's stage buffer from torch's caching allocator on that stream (released to the same
@@ -797,6 +812,7 @@ class Operator:
                 st = _raw_stream(density.device.index)
                 if fn(desc, density.data_ptr(), n_chan, n_vox, div, out.data_ptr(), n, st):
                     _lib.check(-1, 'sphrt_forward')
+                _alternate(desc._obj)
                 return out.view(shape)
         density = tr.as_tensor(density)
         if density.requires_grad and tr.is_grad_enabled():
@@ -839,6 +855,7 @@ class Operator:
         desc, n_chan, cs, div = self._launch_args(d, n_chan, div)
         fn = lib.sphrt_forward_f32 if d.dtype == tr.float32 else lib.sphrt_forward_f64
         _call_forward(fn, desc, d, n_chan, cs, div, out, self._csr['n'], self._cdev)
+        _alternate(desc)
 
     def _forward_kernel_name(self, d):
         """The forward kernel instantiation a launch on `d` runs (sphrt_forward_*'s choice, for
@@ -1027,6 +1044,7 @@ class Operator:
             lib = _lib.load()
             fn = lib.sphrt_forward_f32 if cdt == tr.float32 else lib.sphrt_forward_f64
             _call_forward(fn, tdesc, yv, n_chan, n, 0, res, vol, dev)
+            _alternate(tdesc)
             return res.reshape(dshape).to(device=ddevice, dtype=ddtype)
         acc = tr.zeros(math.prod(dshape), dtype=tr.float64, device=dev)
         _lib.check(_lib.load().sphrt_adjoint_accumulate(

@@ -186,7 +186,6 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     bar = _Bar(range(num_iterations), progress_bar)
     lib = _lib.load()
     n_meas, n_vox = yd.numel(), coeffs.numel()
-    descs = [f._csr['desc']] + ([f._transposed()['desc']] if f.adjoint_mode == 'transpose' else [])
     order = f._adjoint_trace_order()
     if order is not None and order.numel() != n_meas:
         order = None
@@ -205,11 +204,6 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     try:
         with t.no_grad():
             for it in bar:
-                # forward and adjoint blocks in reverse order every other iteration: the two
-                # CSRs together outgrow the memory-side cache (C5), and each launch then starts
-                # on the lines the previous iteration's left in it (sphrt_csr.order; same results)
-                for desc in descs:
-                    desc.order = it % 2
                 opt.zero_grad()
                 d = coeffs.detach()
                 stream = _lib.stream_of(d.device)
@@ -245,9 +239,6 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                 done = it + 1
     except KeyboardInterrupt:
         pass
-    finally:
-        for desc in descs:
-            desc.order = 0
     losses[sq] = scaled(part_sq[:done], n_meas, sq.lam).cpu().tolist()
     if neg is not None:
         losses[neg] = scaled(part_neg[:done], n_vox, neg.lam).cpu().tolist()

@@ -793,7 +793,9 @@ def test_block_order_hint(kind, grid_shape, gpu):
     """sphrt_csr.order = 1 (blocks in reverse order) changes nothing but the order: forward
     (float32, float64) and transposed adjoint bitwise equal to order 0, for a one-wave launch
     (one contiguous range per XCD) and a multi-wave one (dispatch order for float32, runs of 64
-    blocks per XCD for float64, brick staging)."""
+    blocks per XCD for float64, brick staging).  Multi-wave CSRs alternate their order from call
+    to call on every path (general, ctypes fast path, C++ fast path, adjoint); one-wave CSRs
+    keep order 0."""
     from sph_raytracer_amd import Operator
     small = kind == 'rect'
     grid, geom = _orbit(8 if small else 64, (16, 24) if small else (32, 64), kind=kind,
@@ -803,16 +805,20 @@ def test_block_order_hint(kind, grid_shape, gpu):
     g = tr.Generator(device='cpu').manual_seed(5)
     x = tr.rand(grid.shape, dtype=tr.float64, generator=g).to(gpu)
     y = tr.rand(tuple(geom.shape), dtype=tr.float64, generator=g).to(gpu)
-    descs = [op._csr['desc'], op._transposed()['desc']]
-    outs = []
-    for order in (0, 1):
-        for dsc in descs:
+    fwd, adj = op._csr['desc'], op._transposed()['desc']
+    calls = {'f32': (op, x.float(), fwd), 'f64': (op, x, fwd), 'adj': (op.T, y, adj)}
+    outs = {}
+    for _ in range(4):                       # general path first, then the fast paths
+        for name, (fn, arg, dsc) in calls.items():
+            before = dsc.order
+            outs.setdefault((name, before), []).append(fn(arg))
+            assert dsc.order == (before if small else 1 - before)
+    for name, (fn, arg, dsc) in calls.items():
+        for order in (0, 1):
             dsc.order = order
-        outs.append((op(x.float()), op(x), op.T(y)))
-    for dsc in descs:
-        dsc.order = 0
-    for a, b in zip(*outs):
-        assert tr.equal(a, b)
+            outs.setdefault((name, order), []).append(fn(arg))
+        ref = outs[(name, 0)][0]
+        assert all(tr.equal(ref, o) for k, v in outs.items() if k[0] == name for o in v)
 
 
 @pytest.mark.parametrize('wd', [0.0, 0.01])
