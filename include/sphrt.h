@@ -217,6 +217,10 @@ typedef struct sphrt_csr {
      * of the ones it evicted first (C3 forward f32 233 -> 213 us; C5 retrieval 0.138 -> 0.133
      * ms/iteration). */
     int64_t order;
+    /* 1: `stage` already holds this call's density in the brick layout (pad columns zero), e.g.
+     * written by sphrt_adam_neg_f64 after an earlier forward packed the same buffer; the forward
+     * skips its pack.  0: the forward packs (the default). */
+    int64_t stage_packed;
 } sphrt_csr;
 
 int64_t sphrt_csr_blocks(int64_t n_segments);
@@ -319,12 +323,15 @@ int sphrt_neg_reg_f64(const double *d, int64_t n, double c_neg, double *g, doubl
  * torch._fused_adam_'s per-element arithmetic, bitwise), step = the step count after this step's
  * increment (1, 2, ...).  With partial_sums set, the NegRegularizer is folded in first, as
  * sphrt_neg_reg_f64 on d = param before the step (grad itself is not modified); NULL: no
- * regulariser.  Replaces, per retrieval iteration, the reference's optim.step() after
+ * regulariser.  With stage_of (a brick-staged CSR over these n voxels, its `stage` buffer set),
+ * the updated coefficients are also written to their staged columns, so the next forward can
+ * run with stage_packed = 1 (pad columns are left as they are: zero after a forward's pack);
+ * NULL: no stage.  Replaces, per retrieval iteration, the reference's optim.step() after
  * tot_loss.backward() (retrieval.py:115-116; loss.py:140-162 for the regulariser term). */
 int sphrt_adam_neg_f64(double *param, const double *grad, double *exp_avg, double *exp_avg_sq,
                        int64_t n, double lr, double beta1, double beta2, double eps,
                        double weight_decay, double step, double c_neg, double *partial_sums,
-                       void *stream);
+                       const sphrt_csr *stage_of, void *stream);
 
 /* ---- fused no-store mode: trace + integrate in one pass (nothing persisted) --------------- */
 int sphrt_trace_integrate_f32(const sphrt_plan *plan, const sphrt_rays *rays,

@@ -41,7 +41,8 @@ class CSR(ctypes.Structure):
                 ('n_fallback', c_i64), ('empty_ray', c_vp), ('tab_stride', c_i64),
                 ('tab_bytes', c_i64), ('stage_shape', ctypes.c_int32 * 3),
                 ('stage_brick', ctypes.c_int32 * 3), ('stage_cols', c_i64), ('stage', c_vp),
-                ('stage_bytes', c_i64), ('runs', c_vp), ('order', c_i64)]
+                ('stage_bytes', c_i64), ('runs', c_vp), ('order', c_i64),
+                ('stage_packed', c_i64)]
 
 
 ROW_HEAD = 0x80000000
@@ -99,7 +100,7 @@ _SIGNATURES = [
     ('sphrt_sq_residual_f64', c_int, [c_vp, c_vp, c_int, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp]),
     ('sphrt_neg_reg_f64', c_int, [c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp]),
     ('sphrt_adam_neg_f64', c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl,
-                                   c_dbl, c_dbl, c_vp, c_vp]),
+                                   c_dbl, c_dbl, c_vp, ctypes.POINTER(CSR), c_vp]),
     ('sphrt_trace_integrate_f32', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_i64, c_i64,
                                           c_i64, c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
     ('sphrt_trace_integrate_f64', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_i64, c_i64,

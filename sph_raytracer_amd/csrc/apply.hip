@@ -19,6 +19,7 @@
 #include <stdlib.h>
 
 #include "common.hpp"
+#include "stage.hpp"
 
 namespace sphrt {
 
@@ -405,49 +406,6 @@ __device__ __forceinline__ void load8(const int32_t* __restrict__ vox, const L* 
 // for masked slots, so table granule r sits at 16*(r+1)), and the row-head flag in bit 15.
 __device__ __forceinline__ uint16_t loc_code(int rank, uint32_t v, bool head) {
     return (uint16_t)((16 * (rank + 1) + 4 * (int)(v & 3u)) | (head ? 0x8000 : 0));
-}
-
-// ---- brick staging (sphrt_csr.stage_*) ----------------------------------------------------
-// A ray's consecutive voxels step in r, e or a; in the natural (r, e, a) order only steps in a stay
-// inside one 128-byte line, so a workgroup's granules spread over as many lines as granules.
-// Staged, the columns are bricks of br x be x ba voxels (32 = one float line): the same granules
-// fall into 1.7x (C3) to 2.8x (C5) fewer lines, and the granule DMA's L2 requests drop with them
-// (C3 f32 forward 267 -> 241 us, C5 41.9 -> 35.2 us with the pack; tools/brick_study.py).  Natural voxel v -> column:
-struct StageMap {
-    uint32_t on, ne, na, br, be, ba, nbe, nba;
-};
-
-__device__ __forceinline__ uint32_t stage_col(uint32_t v, const StageMap& s) {
-    if (!s.on) return v;
-    const uint32_t a = v % s.na, q = v / s.na, e = q % s.ne, r = q / s.ne;
-    const uint32_t blk = ((r / s.br) * s.nbe + e / s.be) * s.nba + a / s.ba;
-    return blk * (s.br * s.be * s.ba) + ((r % s.br) * s.be + e % s.be) * s.ba + a % s.ba;
-}
-
-static bool staged(const sphrt_csr* c) { return c->stage_shape[0] > 0; }
-
-// Validated map of a CSR (on = 0 when staging is off); false on inconsistent fields.
-static bool stage_map(const sphrt_csr* c, StageMap& m) {
-    m = StageMap{0, 1, 1, 1, 1, 1, 1, 1};
-    if (!staged(c)) return true;
-    int64_t cols = 1, vol = 1;
-    for (int d = 0; d < 3; ++d) {
-        const int64_t n = c->stage_shape[d], b = c->stage_brick[d];
-        if (n < 1 || b < 1) return false;
-        cols *= (n + b - 1) / b * b;
-        vol *= n;
-    }
-    const int64_t bv = (int64_t)c->stage_brick[0] * c->stage_brick[1] * c->stage_brick[2];
-    if (bv % 4 != 0 || cols != c->stage_cols || vol != c->n_cols || cols >= INT32_MAX) return false;
-    m.on = 1;
-    m.ne = (uint32_t)c->stage_shape[1];
-    m.na = (uint32_t)c->stage_shape[2];
-    m.br = (uint32_t)c->stage_brick[0];
-    m.be = (uint32_t)c->stage_brick[1];
-    m.ba = (uint32_t)c->stage_brick[2];
-    m.nbe = (m.ne + m.be - 1) / m.be;
-    m.nba = (m.na + m.ba - 1) / m.ba;
-    return true;
 }
 
 // Columns the granule tables and the table-mode forward address.
@@ -1691,9 +1649,9 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic, int32_t, false, P>), grid, block, 0, st,
                            SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, nullptr);
     } else if (use_tables(c, td, n_chan, tcs, div)) {
-        if (sm.on) {   // natural -> brick layout, every channel
-            if (!c->stage || (int64_t)sizeof(T) * n_chan * c->stage_cols > c->stage_bytes)
-                return fail("brick stage buffer missing or too small for this call");
+        if (sm.on && (!c->stage || (int64_t)sizeof(T) * n_chan * c->stage_cols > c->stage_bytes))
+            return fail("brick stage buffer missing or too small for this call");
+        if (sm.on && !c->stage_packed) {   // natural -> brick layout, every channel
             const int64_t brick_rows = c->stage_cols / c->stage_brick[2];
             const dim3 pg((unsigned)((brick_rows + 255) / 256), (unsigned)imin64(n_chan, 65535));
             hipLaunchKernelGGL(stage_pack_kernel<T>, pg, dim3(256), 0, st, density, chan_stride,

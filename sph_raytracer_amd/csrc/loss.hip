@@ -14,6 +14,7 @@
 // reduction tree, the partials summed in a fixed order) but their order differs from
 // torch.mean's: loss values agree with it to rounding (~1e-16).
 #include "common.hpp"
+#include "stage.hpp"
 
 namespace sphrt {
 
@@ -84,25 +85,46 @@ __global__ __launch_bounds__(kLossThreads) void neg_reg_kernel(
 __global__ __launch_bounds__(kLossThreads) void adam_neg_kernel(
     double* __restrict__ param, const double* __restrict__ grad, double* __restrict__ exp_avg,
     double* __restrict__ exp_avg_sq, int64_t n, double lr, double beta1, double beta2, double eps,
-    double weight_decay, double step, double c_neg, double* __restrict__ part) {
-    const double bc1 = 1 - pow(beta1, step);
-    const double bc2s = sqrt(1 - pow(beta2, step));
+    double weight_decay, double step, double c_neg, double* __restrict__ part, StageMap sm,
+    double* __restrict__ stage) {
+    // the bias corrections once per workgroup (wave 0), under the first element's loads
+    __shared__ double bc[2];
+    const int64_t i0 = (int64_t)blockIdx.x * kLossThreads + threadIdx.x;
+    const bool in0 = i0 < n;
+    double p0 = 0.0, g0 = 0.0, m0 = 0.0, v0 = 0.0;
+    if (in0) {
+        p0 = param[i0];
+        g0 = grad[i0];
+        m0 = exp_avg[i0];
+        v0 = exp_avg_sq[i0];
+    }
+    if (threadIdx.x < 64) {
+        const double b1 = 1 - pow(beta1, step), b2s = sqrt(1 - pow(beta2, step));
+        if (threadIdx.x == 0) {
+            bc[0] = b1;
+            bc[1] = b2s;
+        }
+    }
+    __syncthreads();
+    const double bc1 = bc[0], bc2s = bc[1];
     const double step_size = lr / bc1;
     const double ob1 = 1 - beta1, ob2 = 1 - beta2;
     double acc = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kLossThreads + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * kLossThreads) {
-        double p = param[i], g = grad[i];
+    for (int64_t i = i0; i < n; i += (int64_t)gridDim.x * kLossThreads) {
+        const bool first = i == i0;
+        double p = first ? p0 : param[i], g = first ? g0 : grad[i];
         if (part) {                                        // as neg_reg_kernel
             const double c = p > 0.0 ? 0.0 : p;
             acc += __builtin_fabs(c);
             if (p < 0.0) g = g - c_neg;
         }
         if (weight_decay != 0) g = fma(p, weight_decay, g);
-        const double m = fma(beta1, exp_avg[i], ob1 * g);
-        const double v = fma(beta2, exp_avg_sq[i], ob2 * g * g);
+        const double m = fma(beta1, first ? m0 : exp_avg[i], ob1 * g);
+        const double v = fma(beta2, first ? v0 : exp_avg_sq[i], ob2 * g * g);
         const double denom = sqrt(v) / bc2s + eps;
-        param[i] = p - step_size * m / denom;
+        const double pn = p - step_size * m / denom;
+        param[i] = pn;
+        if (stage) stage[stage_col((uint32_t)i, sm)] = pn;   // the next forward's brick copy
         exp_avg[i] = m;
         exp_avg_sq[i] = v;
     }
@@ -153,13 +175,25 @@ extern "C" int sphrt_neg_reg_f64(const double* d, int64_t n, double c_neg, doubl
 extern "C" int sphrt_adam_neg_f64(double* param, const double* grad, double* exp_avg,
                                   double* exp_avg_sq, int64_t n, double lr, double beta1,
                                   double beta2, double eps, double weight_decay, double step,
-                                  double c_neg, double* partial_sums, void* stream) {
+                                  double c_neg, double* partial_sums, const sphrt_csr* stage_of,
+                                  void* stream) {
     if (n <= 0) return fail("sphrt_adam_neg_f64: empty volume");
     if (!param || !grad || !exp_avg || !exp_avg_sq) return fail("null buffer");
     if (!(step >= 1)) return fail("sphrt_adam_neg_f64: step counts from 1");
+    StageMap sm{};
+    double* stage = nullptr;
+    if (stage_of && staged(stage_of)) {
+        if (!stage_map(stage_of, sm)) return fail("inconsistent brick staging fields");
+        if (stage_of->n_cols != n)
+            return fail("sphrt_adam_neg_f64: %lld voxels, the CSR has %lld columns", (long long)n,
+                        (long long)stage_of->n_cols);
+        if (!stage_of->stage || (int64_t)sizeof(double) * stage_of->stage_cols > stage_of->stage_bytes)
+            return fail("brick stage buffer missing or too small");
+        stage = (double*)stage_of->stage;
+    }
     StreamGuard guard(stream);
     hipLaunchKernelGGL(adam_neg_kernel, dim3(loss_grid(n)), dim3(kLossThreads), 0,
                        (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2,
-                       eps, weight_decay, step, c_neg, partial_sums);
+                       eps, weight_decay, step, c_neg, partial_sums, sm, stage);
     return check_launch("adam_neg");
 }

@@ -819,6 +819,32 @@ class Operator:
             return _LineIntegral.apply(density, self)
         return self._apply_forward(density)
 
+    def _stage_for_loop(self, dtype):
+        """(descriptor copy, its stage buffer) for a loop that keeps the brick-staged density
+        current itself (retrieval._gd_direct: the Adam launch writes it), or None when the
+        forward CSR is not brick-staged or the grid is dynamic.  The copy's stage_packed starts
+        at 0: the first _forward_staged packs."""
+        desc = self._csr['desc'] if self._csr is not None else None
+        if desc is None or self.grid.dynamic or not _stage_bytes(desc, 1, 1):
+            return None
+        self._lengths(dtype)
+        need = _stage_bytes(desc, 1, tr.finfo(dtype).bits // 8)
+        buf = tr.empty(need, dtype=tr.uint8, device=self._cdev)
+        sd = _lib.CSR.from_buffer_copy(desc)
+        sd.stage, sd.stage_bytes, sd.stage_packed = buf.data_ptr(), need, 0
+        return sd, buf
+
+    def _forward_staged(self, d, out, sd):
+        """Static single-channel forward of d (contiguous, on the compute device) into the flat
+        out on the current stream, through a _stage_for_loop descriptor (its stage_packed says
+        whether the stage already holds d)."""
+        with tr.cuda.device(self._cdev):
+            lib = _lib.load()
+            fn = lib.sphrt_forward_f32 if d.dtype == tr.float32 else lib.sphrt_forward_f64
+            _lib.check(fn(sd, _lib.ptr(d), 1, math.prod(self.grid.shape[-3:]), 0, _lib.ptr(out),
+                          self._csr['n'], _lib.stream_of(self._cdev)), 'sphrt_forward')
+            _alternate(sd)
+
     def _lengths(self, dtype):
         """Segment lengths as streamed by the forward kernel: the float64 trace, or (float32
         path) a float32 copy made once — half the bytes, <=6e-8 relative rounding."""

@@ -5,6 +5,7 @@ and adjoint HIP kernels on the cached trace; the optimiser step is plain PyTorch
 examples/static_retrieval.py loop (FullyDenseModel, SquareLoss + NegRegularizer) runs the same
 arithmetic without autograd (_gd_direct): the same iterates, a quarter of the launches.
 """
+import ctypes
 import math
 
 import torch as t
@@ -186,6 +187,11 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     bar = _Bar(range(num_iterations), progress_bar)
     lib = _lib.load()
     n_meas, n_vox = yd.numel(), coeffs.numel()
+    # Adam keeps the forward's brick-staged density current (no pack launch per iteration)
+    staged = f._stage_for_loop(coeffs.dtype) if step is not None else None
+    if staged is not None and f._csr['n'] != n_meas:
+        staged = None
+    yhat_buf = t.empty(n_meas, dtype=coeffs.dtype, device=coeffs.device) if staged else None
     order = f._adjoint_trace_order()
     if order is not None and order.numel() != n_meas:
         order = None
@@ -207,7 +213,14 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                 opt.zero_grad()
                 d = coeffs.detach()
                 stream = _lib.stream_of(d.device)
-                yhat = f(d)
+                if staged is not None:
+                    # the forward reads the brick copy the previous Adam launch wrote (the first
+                    # one packs it)
+                    f._forward_staged(d, yhat_buf, staged[0])
+                    staged[0].stage_packed = 1
+                    yhat = yhat_buf.view(yd.shape)
+                else:
+                    yhat = f(d)
                 if yhat.shape != yd.shape:
                     raise ValueError(f'measurements {tuple(yd.shape)} do not match the operator '
                                      f'output {tuple(yhat.shape)}')
@@ -223,7 +236,8 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                                      trace_order=order is not None)
                 if step is not None:
                     # the regulariser's gradient term and loss partials inside the Adam launch
-                    step(g, c_neg, part_neg[it] if neg is not None else None, stream)
+                    step(g, c_neg, part_neg[it] if neg is not None else None, stream,
+                         staged[0] if staged is not None else None)
                 elif neg is not None:
                     # g -= lam/N where d < 0, and the partial sums of |clamp(d, max=0)|
                     _lib.check(lib.sphrt_neg_reg_f64(_lib.ptr(d), n_vox, c_neg, _lib.ptr(g),
@@ -273,11 +287,13 @@ def _split_fused_adam(opt, coeffs):
     lr, eps, wd = float(grp['lr']), float(grp['eps']), float(grp['weight_decay'])
     count = [0]
 
-    def step(g, c_neg, part, stream):
+    def step(g, c_neg, part, stream, stage_of=None):
         count[0] += 1
         _lib.check(lib.sphrt_adam_neg_f64(_lib.ptr(flat), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v),
                                           flat.numel(), lr, b1, b2, eps, wd, float(count[0]),
-                                          c_neg, _lib.ptr(part), stream), 'sphrt_adam_neg_f64')
+                                          c_neg, _lib.ptr(part),
+                                          ctypes.byref(stage_of) if stage_of is not None else None,
+                                          stream), 'sphrt_adam_neg_f64')
     return step
 
 

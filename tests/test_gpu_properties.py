@@ -852,11 +852,55 @@ def test_adam_matches_torch_fused(wd, c_neg, gpu):
                         found_inf=None)
         _lib.check(lib.sphrt_adam_neg_f64(
             _lib.ptr(pb), _lib.ptr(g), _lib.ptr(mb), _lib.ptr(vb), n, 0.01, 0.9, 0.999, 1e-8, wd,
-            float(it + 1), c_neg or 0.0, _lib.ptr(part_b if c_neg is not None else None),
+            float(it + 1), c_neg or 0.0, _lib.ptr(part_b if c_neg is not None else None), None,
             stream), 'adam_neg')
         assert tr.equal(pa, pb) and tr.equal(ma, mb) and tr.equal(va, vb), it
         if c_neg is not None:
             assert tr.equal(part_a, part_b), it
+
+
+def test_gd_direct_brick_staged(gpu, monkeypatch):
+    """The direct loop on a brick-staged (multi-wave) operator, where the Adam launch writes the
+    next forward's staged density instead of the forward packing it: iterates and losses as the
+    autograd loop's (bitwise / 1e-13), and the stage the loop leaves equals a fresh pack of the
+    final coefficients."""
+    from sph_raytracer_amd import Operator, retrieval
+    from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
+    from sph_raytracer_amd.model import FullyDenseModel
+    grid, geom = _orbit(64, (50, 100), kind='circ', grid_shape=(64, 64, 64))
+    op = Operator(grid, geom, device=gpu)
+    assert op._csr['desc'].stage_shape[0] > 0          # brick-staged
+    x = tr.zeros(grid.shape, dtype=tr.float64, device=gpu)
+    x[:, 32:, :32] = 1
+    meas = op(x)
+    made = []
+    orig = Operator._stage_for_loop
+
+    def spy(self, dtype):
+        r = orig(self, dtype)
+        made.append(r)
+        return r
+
+    monkeypatch.setattr(Operator, '_stage_for_loop', spy)
+    runs = []
+    for use_direct in (True, False):
+        if not use_direct:
+            monkeypatch.setattr(retrieval, '_direct_plan', lambda *a: None)
+        fns = [SquareLoss(), NegRegularizer()]
+        c, yh, hist = retrieval.gd(op, meas.clone(), FullyDenseModel(grid), lr=1e-1,
+                                   num_iterations=6, loss_fns=fns, progress_bar=False)
+        runs.append((c.detach().clone(), yh.detach().clone(), list(hist.values())))
+    (ca, ya, ha), (cb, yb, hb) = runs
+    assert len(made) == 1 and made[0] is not None
+    for la, lb in zip(ha, hb):
+        assert np.allclose(la, lb, rtol=1e-13, atol=0), (la, lb)
+    assert tr.equal(ca, cb) and tr.equal(ya, yb)
+    # the stage the direct loop left holds the coefficients it ended with (its last Adam launch)
+    sd, buf = made[0]
+    cols = tr.tensor([_stage_col(v, tuple(grid.shape), tuple(sd.stage_brick))
+                      for v in range(0, x.numel(), 997)], device=gpu)
+    staged = buf.view(tr.float64)[:sd.stage_cols]
+    assert tr.equal(staged[cols], ca.reshape(-1)[::997])
 
 
 @pytest.mark.parametrize('lams, meas_dtype', [((1, 1), tr.float64), ((0.5, 2), tr.float64),
