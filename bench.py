@@ -267,12 +267,39 @@ def main():
     t_host = (time.perf_counter() - t0) / reps_h
 
     k_reps = 50
+    adj_steps = min(args.steps, 50)      # the adjoint leg below
     k_ms, k_method = kernel_time_ms(op, x, reps=k_reps)
     # launch order of the forward kernel in this process, for tools/rocprof_legs.py (splits a
     # rocprofv3 kernel trace of this command into these legs)
     log('legs ' + json.dumps([['first', 1], ['warmup', args.warmup], ['steps', args.steps]] +
                              ([['final_gather_fwd', 1]] if dist is not None else []) +
-                             [['cold', 3], ['pcie', 3 + reps_h], ['graph', 1 + 4 * k_reps]]))
+                             [['cold', 3], ['pcie', 3 + reps_h], ['graph', 1 + 4 * k_reps]] +
+                             ([['adjoint', 3 + adj_steps]] if not grid.dynamic else [])))
+    # the adjoint (op.T, static grids; BASELINE configs[2] is a forward + adjoint run): the
+    # transposed CSR is built by the first call (untimed), then `adj_steps` calls are timed
+    adjoint = None
+    if not grid.dynamic:
+        y_adj = torch.rand(tuple(op.geom.shape), dtype=dtype, device=dev)
+        for _ in range(3):
+            op.T(y_adj)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(adj_steps):
+            op.T(y_adj)
+        torch.cuda.synchronize(dev)
+        barrier()
+        t_adj = (time.perf_counter() - t0) / adj_steps
+        if dist is not None:
+            tt = torch.tensor([t_adj], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t_adj = tt.item()
+        n_vox = math.prod(shape[-3:])
+        adj_bytes = n_vox * (x.element_size() + 4) + total_seg * (4 + 2 * x.element_size())
+        adjoint = {'ms_per_step': t_adj * 1e3, 'rays_per_s': n_rays * world / t_adj,
+                   'alg_GBps_per_gpu': adj_bytes / t_adj / 1e9, 'steps': adj_steps,
+                   'what': 'op.T(y), y = torch.rand(geom.shape): the transposed CSR (built by the '
+                           'first of 3 untimed calls) through the same table kernel; per-step '
+                           'wall time incl. launch; bytes as SURVEY 8(d) with voxels as rows'}
     kname = op._forward_kernel_name(x)
     traffic, traffic_src = None, None
     # HBM bytes per launch from the newest committed rocprofv3 --pmc passes of this kernel
@@ -307,6 +334,7 @@ def main():
                    'parallelism': f'obs-sharded x{world}' + (' (final stack: one RCCL all-gather)' if world > 1 else '')},
         'peak_gb_resident': peak_gb,
         'final_gather': gather,
+        'adjoint': adjoint,
         'pcie_inclusive': {'rays_per_s': n_rays / t_host, 'ms_per_call': t_host * 1e3,
                            'what': 'op(x) with x and the result in host memory (per rank)'},
         'cold': {'rays_per_s': n_rays * world / t_warm_cold, 'seconds': t_warm_cold,

@@ -719,6 +719,7 @@ class Operator:
         self._csr = None
         self._fast = {}     # (shape, dtype, device) -> bound forward launch (steady-state calls)
         self._fastc = None  # the same bindings inside the CPython entry (csrc/fastpath.cpp)
+        self._fastc_T = None  # the adjoint's steady-state bindings (T), same entry
         # 'transpose': deterministic voxel-major adjoint (default); 'atomic': float64 atomics
         # (used anyway when views are paired with time slices)
         self.adjoint_mode = 'transpose'
@@ -1091,8 +1092,43 @@ class Operator:
         (raytracer.py:715-748).  Static grids only, like the reference."""
         if self.grid.dynamic:
             raise NotImplementedError
+        fc = self._fastc_T
+        if fc is not None:
+            # steady state in one C call: the transposed CSR's forward (csrc/fastpath.cpp)
+            out = self._fastfn(fc, line_integrations)
+            if out is not None:
+                return out
         y = tr.as_tensor(line_integrations)
-        return self._apply_adjoint(y, tuple(self.grid.shape), y.dtype, tr.device(self.device))
+        res = self._apply_adjoint(y, tuple(self.grid.shape), y.dtype, tr.device(self.device))
+        self._bind_adjoint(y, res)
+        return res
+
+    def _bind_adjoint(self, y, res):
+        """Register T's steady-state binding for y's shape/dtype when the general path did no
+        more than one transposed-CSR forward: y contiguous on the compute device, float32/64, the
+        result left there in y's dtype, no ray permutation (a trace in geometry order), no
+        staged transpose."""
+        csr, dev = self._csr, self._cdev
+        if not (type(y) is tr.Tensor and y.device == dev and res.device == dev
+                and y.dtype in (tr.float32, tr.float64) and res.dtype == y.dtype
+                and y.is_contiguous() and self.adjoint_mode == 'transpose'
+                and csr is not None and csr['ray_id'] is None and y.numel() == csr['n']):
+            return
+        tdesc = self._transposed()['desc']
+        if _stage_bytes(tdesc, 1, y.element_size()):
+            return
+        fast = _lib.load_fast()
+        if fast is None:
+            return
+        lib = _lib.load()
+        fn = lib.sphrt_forward_f32 if y.dtype == tr.float32 else lib.sphrt_forward_f64
+        if self._fastc_T is None:
+            self._fastfn = fast.forward
+            self._fastc_T = fast.new(_lib.address(lib.sphrt_last_error))
+        vol = math.prod(self.grid.shape[-3:])
+        fast.add(self._fastc_T, tuple(y.shape), y.dtype == tr.float64, dev.index,
+                 _lib.address(fn), ctypes.addressof(tdesc), 1, csr['n'], 0, vol,
+                 tuple(res.shape), 0)
 
     # -- compatibility views -----------------------------------------------------------------------
     def _padded(self):

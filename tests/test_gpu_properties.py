@@ -473,6 +473,27 @@ def test_fast_path_matches_general_path(c2, gpu):
         assert y3.shape == (2,) + tuple(geom.shape) and tr.equal(y3[0], y0)
 
 
+def test_adjoint_fast_path_matches_general_path(c2, gpu):
+    """op.T on a bound shape/dtype goes through the CPython entry as one transposed-CSR forward:
+    bitwise the general path's result, fresh outputs; a ConeCirc (wedge-ordered) operator, whose
+    adjoint permutes its input first, keeps the general path."""
+    from sph_raytracer_amd import Operator
+    grid, geom, op = c2
+    for dt in (tr.float32, tr.float64):
+        y = tr.rand(tuple(geom.shape), dtype=dt, device=gpu)
+        a0 = op.T(y)                     # general path, binds
+        a1 = op.T(y)                     # fast path
+        a2 = op.T(y)
+        assert op._fastc_T is not None
+        assert a1.shape == a0.shape == tuple(grid.shape) and a1.dtype == dt
+        assert tr.equal(a0, a1) and tr.equal(a1, a2) and a1.data_ptr() != a2.data_ptr()
+        assert tr.equal(op.T(y.cpu()).to(gpu), a0)            # host input: general path
+    cgrid, cgeom = _orbit(6, (12, 16), kind='circ', grid_shape=(12, 12, 12))
+    cop = Operator(cgrid, cgeom, device=gpu)
+    yc = tr.rand(tuple(cgeom.shape), dtype=tr.float64, device=gpu)
+    assert tr.equal(cop.T(yc), cop.T(yc)) and cop._fastc_T is None
+
+
 def test_dynamic_pairing_forward_and_adjoint(gpu):
     """View i <-> time slice i (dynamic grid, a collection of T views): the forward runs on the
     time-paired CSR (granule tables over the flattened (T, vol) density) and the adjoint on its
