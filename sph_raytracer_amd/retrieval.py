@@ -162,9 +162,10 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     NegRegularizer's -lam/N on negative voxels, the optimiser step), without building and walking
     a graph every iteration: one forward, one adjoint, the residual kernel of csrc/loss.hip
     and the optimiser step (for Adam, one csrc/loss.hip launch that also applies the
-    regulariser; otherwise its own kernel, then opt.step()).  The loss values are the fused kernels' partial sums,
-    summed for all iterations after the loop: deterministic, within rounding of the autograd
-    loop's torch.mean.
+    regulariser and keeps the forward's brick-staged density current; otherwise the
+    regulariser's own kernel, then opt.step()).  The loss values are the fused kernels' partial
+    sums, summed for all iterations after the loop: deterministic, within rounding of the
+    autograd loop's torch.mean.
 
     Gradient of lam * mean((y - f(d))^2): autograd's chain gives (lam / N) * (2 * (y - f(d)))
     negated, i.e. (f(d) - y) * (2 * (lam / N)) exactly (scaling by 2 and negation are exact).
@@ -269,8 +270,10 @@ def _split_fused_adam(opt, coeffs):
     tensor: a 64^3 volume is 4 workgroups on a 256-CU GPU (78 us of a 0.32 ms C5 iteration; on
     36 contiguous pieces, the most one launch takes, 15 us plus 5 us for the step counts).
     csrc/loss.hip runs the same per-element arithmetic (bitwise: test_adam_matches_torch_fused)
-    over the whole volume with the NegRegularizer's gradient term folded in, ~4 us.  The
-    optimiser's own state is left untouched (the loop owns the moments and the step count)."""
+    over the whole volume with the NegRegularizer's gradient term folded in, and, given a
+    brick-staged forward descriptor (stage_of), writes the updated coefficients to its stage
+    too.  The optimiser's own state is left untouched (the loop owns the moments and the step
+    count)."""
     from . import _lib
     if type(opt) is not t.optim.Adam or len(opt.param_groups) != 1:
         return None
