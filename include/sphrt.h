@@ -277,8 +277,9 @@ int sphrt_csr_time_columns(const sphrt_csr *csr, int64_t div, int64_t vol, int32
  * derived); otherwise every ray is integrated for all n_chan channels (static multichannel).
  * float64: products and sums in float64.  float32 (streams `len32`): products and each thread's
  * run of up to 8 consecutive segments of a row in float32 (the reference's own f32 product
- * rounding, raytracer.py:710), the runs of a row stitched across threads in float64, each row
- * rounded once; measured within 1.9e-7 relative of float64 accumulation. */
+ * rounding, raytracer.py:710), the runs of a row stitched across threads in float32 as well
+ * (the reference sums in float32 too); measured within 2.5e-7 relative of float64
+ * accumulation (C2-C5). */
 int sphrt_forward_f32(const sphrt_csr *csr, const float *density, int64_t n_chan,
                       int64_t chan_stride, int64_t ray_chan_div, float *out,
                       int64_t out_chan_stride, void *stream);

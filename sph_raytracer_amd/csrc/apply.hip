@@ -314,14 +314,33 @@ __device__ __forceinline__ int block_excl_count1(int v, int& total, int (&cnt)[4
     return base + inc - v;
 }
 
-template <int W = 4>
-__device__ __forceinline__ double block_excl_segsum1(bool has, double tail, bool& tot_has,
-                                                     double& tot_sum, int (&hs)[4],
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp0(float x) {
+    return __int_as_float(dpp0<CTRL, ROWS>(__float_as_int(x)));
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ void seg_step(int& h, float& s) {
+    const int hu = dpp0<CTRL, ROWS>(h);
+    const float su = dpp0<CTRL, ROWS>(s);
+    s = h ? s : su + s;
+    h |= hu;
+}
+
+// float32 forwards stitch a row's runs across threads in float too (the segmented scan's DPP
+// steps and wave totals at half the width): C2 forward 6.68 -> 6.37 us, C5 28.3 -> 27.5 us, C3
+// unchanged; largest relative difference from float64 accumulation 1.8e-7 -> 2.5e-7 (C2-C5,
+// forward and adjoint).  SPHRT_FWD_STITCH32=0 at build time stitches in double (A/B studies).
+#ifndef SPHRT_FWD_STITCH32
+#define SPHRT_FWD_STITCH32 1
+#endif
+template <int W = 4, typename S = double>
+__device__ __forceinline__ S block_excl_segsum1(bool has, S tail, bool& tot_has,
+                                                     S& tot_sum, int (&hs)[4],
                                                      double (&sm)[4]) {
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int h = has ? 1 : 0;
-    double s = tail;
+    S s = tail;
     seg_step<kShr1>(h, s);
     seg_step<kShr2>(h, s);
     seg_step<kShr4>(h, s);
@@ -329,22 +348,22 @@ __device__ __forceinline__ double block_excl_segsum1(bool has, double tail, bool
     seg_step<kBcast15, 0xa>(h, s);
     seg_step<kBcast31, 0xc>(h, s);
     const int eh = dpp0<kWaveShr1>(h);
-    const double es = dpp0<kWaveShr1>(s);
+    const S es = dpp0<kWaveShr1>(s);
     if (lane == 63) {
         hs[wid] = h;
-        sm[wid] = s;
+        sm[wid] = (double)s;
     }
     lds_barrier();
     const int4 hv = *reinterpret_cast<const int4*>(hs);   // vector LDS reads, no per-wave loop
     const double2 s01 = *reinterpret_cast<const double2*>(sm);
     const double2 s23 = *reinterpret_cast<const double2*>(sm + 2);
     const int hw[4] = {hv.x, hv.y, W > 2 ? hv.z : 0, W > 2 ? hv.w : 0};   // (W = 2: 2, 3 unused)
-    const double sw[4] = {s01.x, s01.y, W > 2 ? s23.x : 0.0, W > 2 ? s23.y : 0.0};
-    double t[4];                                   // segmented prefix through wave w
+    const S sw[4] = {(S)s01.x, (S)s01.y, W > 2 ? (S)s23.x : (S)0, W > 2 ? (S)s23.y : (S)0};
+    S t[4];                                        // segmented prefix through wave w
     t[0] = sw[0];
 #pragma unroll
     for (int w = 1; w < 4; ++w) t[w] = hw[w] ? sw[w] : t[w - 1] + sw[w];
-    const double cs = wid == 0 ? 0.0 : wid == 1 ? t[0] : wid == 2 ? t[1] : t[2];
+    const S cs = wid == 0 ? (S)0 : wid == 1 ? t[0] : wid == 2 ? t[1] : t[2];
     tot_sum = t[3];
     tot_has = (hw[0] | hw[1] | hw[2] | hw[3]) != 0;
     return eh ? es : cs + es;
@@ -1109,7 +1128,9 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             stage_partial_tail<T, TabT, THR>(rho, tab_b, (int)n_tab, n_cols, dens);
         }
         FWD_STAMP(2);
-        double carry = 0.0;                 // open run entering the pass
+        using Stitch = typename std::conditional<SPHRT_FWD_STITCH32 && sizeof(T) == 4, float,
+                                                  double>::type;
+        Stitch carry = 0;                   // open run entering the pass
         rbase = 0;
 #pragma clang loop unroll(disable)
         for (int64_t base = base0; base < s1; base += kPass) {
@@ -1231,7 +1252,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             }
             // Products and thread-local runs in A (float for a float density: the reference's own
             // precision, 4-cycle VALU ops instead of 8-cycle f64 ones); runs that cross threads are
-            // stitched in double.
+            // stitched in Stitch (A as well, SPHRT_FWD_STITCH32).
             A p[P];
 #pragma unroll
             for (int k = 0; k < P; ++k) p[k] = (A)rv[k] * (A)l[k];
@@ -1257,27 +1278,27 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
                 if (k < P) tail = ((hmask >> k) & 1 ? (A)0 : tail) + p[k];
             }
             bool tot_has;
-            double tot_sum;
+            Stitch tot_sum;
 #ifdef SPHRT_FWD_ABL_SEGSCAN   // diagnostic builds only: no segmented scan (wrong results)
             const double ex = 0.0;
             tot_has = true;
-            tot_sum = (double)tail;
+            tot_sum = (Stitch)tail;
 #else
-            const double ex = block_excl_segsum1<W>(hmask != 0, (double)tail, tot_has, tot_sum,
+            const Stitch ex = block_excl_segsum1<W, Stitch>(hmask != 0, (Stitch)tail, tot_has, tot_sum,
                                                  sh.has[par], sh.sum[par]);
 #endif
             par ^= 1;
             FWD_STAMP(4);
             // the run open at this thread's start: the segmented prefix of the earlier threads,
             // plus the carry of earlier passes when no earlier thread of this pass saw a head
-            const double run0 = hb > 0 ? ex : carry + ex;
+            const Stitch run0 = hb > 0 ? ex : carry + ex;
             uint32_t cmask = hmask;
             {
                 const int first = lo - o, end = hi - o;
                 if (base == base0 && first >= 0 && first < P) cmask &= ~(1u << first);
                 if (base + kPass >= s1 && end > 0 && end <= P) cmask |= 1u << P;
             }
-            if ((cmask >> h1) & 1) oc[r_prev] = (T)(run0 + (double)qa);
+            if ((cmask >> h1) & 1) oc[r_prev] = (T)(run0 + (Stitch)qa);
             if (h2 != h1 && ((cmask >> h2) & 1)) oc[r_first] = (T)v1;
             if (h3 != h2 && ((cmask >> h3) & 1)) oc[r_second] = (T)v2;
             if (hcount > 2) {                         // rare: closes of the fourth and later runs

@@ -12,8 +12,8 @@ Differences from the reference, by design:
   ``op.regs`` / ``op.lens`` rebuild a padded compatibility view on demand;
 - crossings at exactly equal distances are ordered as the reference's libstdc++ introsort orders
   them whenever that order can change a voxel (rare rays, replayed by an exact kernel);
-- float64 forwards accumulate in float64; float32 forwards multiply and sum runs of up to 8
-  segments in float32 and stitch the runs of a row in float64, rounding each row once;
+- float64 forwards accumulate in float64; float32 forwards multiply and sum in float32 (runs of
+  up to 8 segments per thread, stitched across threads), within 2.5e-7 of float64 accumulation;
 - the caller's ``geom.rays`` tensor is never normalised in place.
 """
 import ctypes
