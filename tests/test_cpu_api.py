@@ -322,6 +322,38 @@ def test_library_builds_and_exports_header():
     assert lib.sphrt_scan_workspace_bytes(10_000) > 0
 
 
+def test_loss_abi_argument_checks():
+    """The retrieval entry points reject bad arguments before touching the device: an empty
+    problem, null buffers, a step count below 1, a staged CSR whose columns are not the
+    coefficients; each with a message in sphrt_last_error.  (No compute call: no GPU here.)"""
+    from sph_raytracer_amd import _lib
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)      # never dereferenced: every call below fails its checks first
+    none = None
+
+    def adam(param, n, step, stage_of=None):
+        return lib.sphrt_adam_neg_f64(param, p, p, p, n, 0.1, 0.9, 0.999, 1e-8, 0.0, step, 0.0,
+                                      none, stage_of, none)
+
+    cases = [
+        (lambda: adam(p, 0, 1.0), b'empty'),
+        (lambda: adam(none, 8, 1.0), b'null'),
+        (lambda: adam(p, 8, 0.0), b'step'),
+        (lambda: lib.sphrt_sq_residual_f64(p, p, 1, 0, 1.0, none, p, p, none), b'empty'),
+        (lambda: lib.sphrt_sq_residual_f64(p, none, 1, 8, 1.0, none, p, p, none), b'null'),
+        (lambda: lib.sphrt_neg_reg_f64(p, 0, 0.1, p, p, none), b'empty'),
+    ]
+    csr = _lib.CSR()          # a brick-staged CSR over 4^3 voxels, without a stage buffer
+    csr.stage_shape[:] = [4, 4, 4]
+    csr.stage_brick[:] = [2, 4, 4]
+    csr.stage_cols, csr.n_cols = 64, 64
+    cases += [(lambda: adam(p, 32, 1.0, ctypes.byref(csr)), b'columns'),
+              (lambda: adam(p, 64, 1.0, ctypes.byref(csr)), b'stage buffer')]
+    for call, word in cases:
+        assert call() != 0
+        assert word in lib.sphrt_last_error().lower(), lib.sphrt_last_error()
+
+
 def test_fastpath_entry_builds_and_declines_foreign_inputs():
     """csrc/fastpath.cpp (the CPython entry for steady-state Operator calls) builds against the
     installed torch, loads, and returns None for anything it has no binding for (CPU tensors,
