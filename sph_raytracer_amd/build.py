@@ -66,13 +66,14 @@ def build_fast(force=False, verbose=False):
             os.path.getmtime(FAST_OUT) >= max(os.path.getmtime(src), os.path.getmtime(__file__),
                                               os.path.getmtime(os.path.join(ROOT, 'include', 'sphrt.h'))):
         return FAST_OUT
-    cmd = fast_command(FAST_OUT + '.tmp')
+    tmp = f'{FAST_OUT}.tmp{os.getpid()}'   # per process: ranks that start together never share it
+    cmd = fast_command(tmp)
     if verbose:
         print(' '.join(cmd))
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f'g++ (fastpath.cpp) failed ({res.returncode}):\n{res.stderr[-4000:]}')
-    os.replace(FAST_OUT + '.tmp', FAST_OUT)
+    os.replace(tmp, FAST_OUT)
     return FAST_OUT
 
 
@@ -84,7 +85,7 @@ def build(force=False, verbose=False):
     cmd = command()
     if verbose:
         print(' '.join(cmd))
-    tmp = OUT + '.tmp'
+    tmp = f'{OUT}.tmp{os.getpid()}'
     cmd[cmd.index(OUT)] = tmp
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
