@@ -494,7 +494,9 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
     return loc, tab, runs
 
 
-_BRICK = (2, 4, 4)   # (r, e, a) voxels per staging brick: 32 = one 128-byte float line
+_BRICK = (4, 2, 4)   # (r, e, a) voxels per staging brick: 32 = one 128-byte float line
+# (4, 2, 4) over round 1's (2, 4, 4): C3 forward f32 214.5 -> 204.1 us, f64 350.4 -> 333.5 us, C5
+# unchanged (27.7 / 45.3 us); 11 shapes swept in profiles/r02_brick_sweep.jsonl.
 _SINGLE_WAVE_BLOCKS = 256 * 6   # forward workgroups resident at once (256 CUs x 6)
 
 
