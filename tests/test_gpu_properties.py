@@ -141,9 +141,10 @@ def _stage_col(v, shape, brick):
 def test_brick_staged_tables(gpu, monkeypatch):
     """Brick staging forced on a grid no brick divides (padded staging, 3 channels growing the
     stage): tables and loc address the staged columns, and the staged table forward equals the
-    per-segment gather forward bitwise (_check_granule_tables), for two bricks."""
+    per-segment gather forward bitwise (_check_granule_tables), for three bricks (4,2,4: the
+    default, r padded 30 -> 32)."""
     from sph_raytracer_amd import Operator
-    for brick in ('2,4,4', '4,4,2'):
+    for brick in ('4,2,4', '2,4,4', '4,4,2'):
         monkeypatch.setenv('SPHRT_BRICK', brick)
         monkeypatch.setenv('SPHRT_BRICK_T', '1,2,8')     # transposed: rays, 30 columns padded
         grid, geom = _orbit(4, (24, 30), grid_shape=(30, 21, 26))
@@ -703,7 +704,7 @@ def test_onepass_trace_full_size(kind, n_views, det, grid_shape, gpu, monkeypatc
 
 
 @pytest.mark.parametrize('grid_shape, staged', [((50, 50, 50), 'auto'), ((96, 80, 90), 'auto'),
-                                                ((30, 21, 26), '2,4,4')])
+                                                ((30, 21, 26), '2,4,4'), ((30, 21, 26), '4,2,4')])
 def test_onepass_tables_equal_twopass(grid_shape, staged, gpu, monkeypatch):
     """Granule tables built in one pass (wide tables + pack) equal the count + fill ones: block
     records, loc, tables (bitmap build at 50^3, radix build above 2^19 voxels, brick-staged)."""
