@@ -86,9 +86,11 @@ def main():
     a32 = torch.empty(nvox, dtype=torch.float32, device=dev)
     y32 = y.float()
 
-    def adjoint_t(yy, out):
+    from sph_raytracer_amd.raytracer import _call_forward
+
+    def adjoint_t(yy, out):     # through _call_forward: a staged T (SPHRT_BRICK_T) gets its stage
         fn = lib.sphrt_forward_f32 if yy.dtype == torch.float32 else lib.sphrt_forward_f64
-        _lib.check(fn(T, _lib.ptr(yy), 1, n, 0, _lib.ptr(out), nvox, _lib.stream_of(dev)), 'adjT')
+        _call_forward(fn, T, yy, 1, n, 0, out, nvox, dev)
 
     variants = {
         'forward_f32': (lambda: op._launch_forward(x32, o32, 1, 0), n * 8 + total * 12),
