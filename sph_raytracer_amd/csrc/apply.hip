@@ -1639,15 +1639,19 @@ static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int
 // 596 -> 366 us; adjoint f64 377 -> 331 us); when the whole grid is resident at once (one wave of
 // <= 6 blocks per CU), one contiguous range per XCD cuts the first-touch misses (C2 forward f32
 // 7.0 -> 6.7 us); otherwise (the array fits every L2, several waves) dispatch order is as fast or
-// faster (C5 f64 64 vs 68 us with runs of 64).
+// faster (C5 f64 64 vs 68 us with runs of 64).  Round 2 (4,2,4 bricks, profiles/r02_xcd_chunk_sweep):
+// runs of 64 also win for multi-wave grids whose array is 1-4 MB (C5 f64 forward 45.5 -> 44.0 us;
+// C3 keeps 64: f32 204.8 us against 208.3 / 210.1 at 32 / 128); C5 f32 (1 MB) stays in dispatch order.
 static int fwd_chunk(const sphrt_csr* c, size_t elem) {
     static const int forced = [] {     // SPHRT_XCD_CHUNK=k: runs of k blocks (A/B studies)
         const char* e = getenv("SPHRT_XCD_CHUNK");
         return e ? atoi(e) : -1;
     }();
+    const int64_t bytes = c->n_cols * (int64_t)elem;
     int k = forced >= 0 ? forced
-            : c->n_cols * (int64_t)elem > (int64_t)(4 << 20) ? 64
-            : c->n_blocks <= 256 * 6 ? INT32_MAX : 0;
+            : bytes > (int64_t)(4 << 20) ? 64
+            : c->n_blocks <= 256 * 6 ? INT32_MAX
+            : bytes > (int64_t)(1 << 20) ? 64 : 0;
     return (c->order & 1) ? ~k : k;   // (block_of: reversed)
 }
 
