@@ -1642,6 +1642,9 @@ static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int
 // faster (C5 f64 64 vs 68 us with runs of 64).  Round 2 (4,2,4 bricks, profiles/r02_xcd_chunk_sweep):
 // runs of 64 also win for multi-wave grids whose array is 1-4 MB (C5 f64 forward 45.5 -> 44.0 us;
 // C3 keeps 64: f32 204.8 us against 208.3 / 210.1 at 32 / 128); C5 f32 (1 MB) stays in dispatch order.
+// A time-paired CSR (sphrt_csr.order bit 1: each view reads its own time slice of T * vol
+// columns) takes one contiguous range per XCD, so that an XCD's rays stay on few slices (C4: f32
+// 20.3 -> 18.9 us, f64 28.4 -> 26.5 us against runs of 64).
 static int fwd_chunk(const sphrt_csr* c, size_t elem) {
     static const int forced = [] {     // SPHRT_XCD_CHUNK=k: runs of k blocks (A/B studies)
         const char* e = getenv("SPHRT_XCD_CHUNK");
@@ -1649,6 +1652,7 @@ static int fwd_chunk(const sphrt_csr* c, size_t elem) {
     }();
     const int64_t bytes = c->n_cols * (int64_t)elem;
     int k = forced >= 0 ? forced
+            : (c->order & 2) ? INT32_MAX
             : bytes > (int64_t)(4 << 20) ? 64
             : c->n_blocks <= 256 * 6 ? INT32_MAX
             : bytes > (int64_t)(1 << 20) ? 64 : 0;

@@ -1029,6 +1029,7 @@ class Operator:
         c = _lib.CSR.from_buffer_copy(csr['desc'])
         _clear_stage(c)                             # time-paired columns are not bricked
         c.vox, c.blocks, c.n_cols = vox_p.data_ptr(), blocks_p.data_ptr(), T * vol
+        c.order |= 2        # disjoint slices per view: one contiguous block range per XCD (sphrt.h)
         c.loc, c.tab, c.tab_stride, c.n_fallback = None, None, 0, 0
         loc, tab, runs = _local_tables(lib, c, blocks_p, nblocks, total, dev, stream)
         csr[key] = dict(desc=c, keep=(vox_p, blocks_p, loc, tab, runs), n_t=T)
