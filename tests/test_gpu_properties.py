@@ -547,6 +547,13 @@ def test_dynamic_pairing_forward_and_adjoint(gpu):
     xg2 = x.clone().requires_grad_(True)
     (op(xg2) * y).sum().backward()
     assert tr.equal(xg2.grad, atx)                       # deterministic
+    # the paired CSR's contiguous-XCD-range hint (order bit 1) changes the block order only
+    pd = op._paired(T, div)['desc']
+    assert pd.order & 2
+    for bits in (pd.order & 1, (pd.order & 1) ^ 1):       # dispatch-order / runs and reversed
+        pd.order = bits
+        assert tr.equal(op(x), fx)
+    pd.order = 2
     f32 = op(x.float())
     assert tr.allclose(f32.double(), fx, rtol=1e-5, atol=1e-6)
     assert op._fastc is not None and tr.equal(op(x), fx)     # bound: the CPython fast path
