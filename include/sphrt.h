@@ -229,7 +229,7 @@ int64_t sphrt_csr_blocks(int64_t n_segments);
 size_t sphrt_csr_index_workspace_bytes(int64_t n_rays);
 /* ray_ids: NULL (row r is ray r), or the ray each row reports in row_ray / empty_ray — the
  * output index of a trace made in another ray order than the geometry's (the Operator traces
- * ConeCirc views in wedges of 5 azimuth columns, raytracer._trace_order). */
+ * ConeCirc views in wedges of raytracer._WEDGE (3) azimuth columns, raytracer._trace_order). */
 int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_t *row_ray,
                     int32_t *empty_ray, int64_t *blocks, int64_t n_blocks, const int32_t *ray_ids,
                     void *workspace, void *stream);
@@ -335,6 +335,16 @@ int sphrt_adam_neg_f64(double *param, const double *grad, double *exp_avg, doubl
                        int64_t n, double lr, double beta1, double beta2, double eps,
                        double weight_decay, double step, double c_neg, double *partial_sums,
                        const sphrt_csr *stage_of, void *stream);
+/* The same step with the arithmetic of the default Adam on GPU tensors (torch.optim.Adam without
+ * fused=: the multi-tensor "foreach" implementation, which the reference's optim(optim_vars,
+ * **kwargs), retrieval.py:84, runs on a ROCm device), bitwise.  Its bias corrections come from
+ * the host as torch computes them in Python: step_size = -lr / (1 - beta1**t), bc2_sqrt =
+ * (1 - beta2**t) ** 0.5.  Regulariser and stage as sphrt_adam_neg_f64. */
+int sphrt_adam_foreach_neg_f64(double *param, const double *grad, double *exp_avg,
+                               double *exp_avg_sq, int64_t n, double step_size, double beta1,
+                               double beta2, double eps, double weight_decay, double bc2_sqrt,
+                               double c_neg, double *partial_sums, const sphrt_csr *stage_of,
+                               void *stream);
 
 /* ---- fused no-store mode: trace + integrate in one pass (nothing persisted) --------------- */
 int sphrt_trace_integrate_f32(const sphrt_plan *plan, const sphrt_rays *rays,

@@ -101,6 +101,9 @@ _SIGNATURES = [
     ('sphrt_neg_reg_f64', c_int, [c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp]),
     ('sphrt_adam_neg_f64', c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_dbl, c_dbl, c_dbl, c_dbl,
                                    c_dbl, c_dbl, c_vp, ctypes.POINTER(CSR), c_vp]),
+    ('sphrt_adam_foreach_neg_f64', c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_dbl, c_dbl,
+                                           c_dbl, c_dbl, c_dbl, c_dbl, c_vp, ctypes.POINTER(CSR),
+                                           c_vp]),
     ('sphrt_trace_integrate_f32', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_i64, c_i64,
                                           c_i64, c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
     ('sphrt_trace_integrate_f64', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_i64, c_i64,
@@ -126,8 +129,28 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    _check_hash(lib.sphrt_version().decode(), LIB_PATH)
     _lib = lib
     return lib
+
+
+def _check_hash(version, path):
+    """Refuse a library built from other sources than this tree's (build.source_hash, embedded
+    as the version's 'src <hash>'): a stale binary shipped next to edited sources would
+    otherwise run silently.  Trees without the sources (an installed copy) skip the check."""
+    from . import build
+    if not build.have_sources():
+        return
+    want = build.source_hash()
+    got = version.rsplit(' src ', 1)[-1] if ' src ' in version else None
+    if got != want:
+        raise RuntimeError(f'sph_raytracer_amd: {path} was built from sources {got}, this tree is '
+                           f'{want}; rebuild with `python -m sph_raytracer_amd.build`')
+
+
+def source_hash():
+    """The hash of the sources the loaded library was built from (sphrt_version)."""
+    return load().sphrt_version().decode().rsplit(' src ', 1)[-1]
 
 
 _fast = None
@@ -145,6 +168,7 @@ def load_fast():
             spec = importlib.util.spec_from_file_location('_sphrt_fast', FAST_PATH)
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)
+            _check_hash(getattr(mod, 'version', ''), FAST_PATH)
             _fast = mod
     return _fast or None
 

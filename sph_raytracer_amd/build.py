@@ -6,7 +6,9 @@ The library goes to sph_raytracer_amd/lib/libsphrt.so, which travels with the re
 the GPU box (it is git-ignored, not gpurun-ignored).  Device code is compiled with
 -ffp-contract=off: the solver's fused multiply-adds are explicit (csrc/solve.hpp).
 """
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -28,20 +30,50 @@ def hipcc():
     raise RuntimeError('hipcc not found (ROCm 7.x expected under /opt/rocm)')
 
 
+_FLAGS = ['-O3', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off', '-munsafe-fp-atomics']
+FAST_SOURCE = 'fastpath.cpp'
+# sphrt_version() ends in "src <hash>"; the same text is in the library file (host rodata), so a
+# build's hash can be read without loading it
+_HASH_RE = re.compile(rb'sph_raytracer_amd [^\x00]*? src ([0-9a-f]{16})')
+
+
+def source_hash():
+    """Hash of everything the libraries are built from: the HIP/C++ sources and headers, the C
+    ABI header, the target and the compile flags (16 hex digits).  Embedded into both libraries
+    at build time (-DSPHRT_SOURCE_HASH); _lib.load() refuses a library whose hash differs from
+    the tree's, and build() rebuilds on a mismatch (not on file times)."""
+    h = hashlib.sha256()
+    files = sorted(SOURCES + HEADERS + [FAST_SOURCE])
+    for name, path in [(f, os.path.join(CSRC, f)) for f in files] + \
+            [('sphrt.h', os.path.join(ROOT, 'include', 'sphrt.h'))]:
+        with open(path, 'rb') as fh:
+            data = fh.read()
+        h.update(name.encode() + b'\0' + str(len(data)).encode() + b'\0' + data)
+    h.update(' '.join([ARCH] + _FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def have_sources():
+    return all(os.path.exists(os.path.join(CSRC, f)) for f in SOURCES + HEADERS + [FAST_SOURCE])
+
+
+def embedded_hash(path):
+    """The source hash a built library carries (None: not built, or built without one)."""
+    if not os.path.exists(path):
+        return None
+    with open(path, 'rb') as fh:
+        m = _HASH_RE.search(fh.read())
+    return m.group(1).decode() if m else None
+
+
 def command(out=OUT, extra=()):
-    return [hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared',
-            '-ffp-contract=off', '-munsafe-fp-atomics',
+    return [hipcc(), f'--offload-arch={ARCH}', *_FLAGS, f'-DSPHRT_SOURCE_HASH="{source_hash()}"',
             '-I', os.path.join(ROOT, 'include'), '-I', CSRC,
             *extra, '-o', out] + [os.path.join(CSRC, s) for s in SOURCES]
 
 
 def _stale(out):
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, 'include', 'sphrt.h'),
-                                                                   os.path.abspath(__file__)]
-    return any(os.path.getmtime(d) > t for d in deps)
+    return embedded_hash(out) != source_hash()
 
 
 def fast_command(out=FAST_OUT):
@@ -51,7 +83,8 @@ def fast_command(out=FAST_OUT):
     import torch
     tdir = os.path.dirname(torch.__file__)
     return ['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-D__HIP_PLATFORM_AMD__=1',
-            '-DUSE_ROCM=1', '-I', os.path.join(tdir, 'include'),
+            '-DUSE_ROCM=1', f'-DSPHRT_SOURCE_HASH="{source_hash()}"',
+            '-I', os.path.join(tdir, 'include'),
             '-I', os.path.join(tdir, 'include', 'torch', 'csrc', 'api', 'include'),
             '-I', '/opt/rocm/include', '-I', os.path.join(ROOT, 'include'),
             '-I', sysconfig.get_paths()['include'],
@@ -61,10 +94,7 @@ def fast_command(out=FAST_OUT):
 
 
 def build_fast(force=False, verbose=False):
-    src = os.path.join(CSRC, 'fastpath.cpp')
-    if not force and os.path.exists(FAST_OUT) and \
-            os.path.getmtime(FAST_OUT) >= max(os.path.getmtime(src), os.path.getmtime(__file__),
-                                              os.path.getmtime(os.path.join(ROOT, 'include', 'sphrt.h'))):
+    if not force and not _stale(FAST_OUT):
         return FAST_OUT
     tmp = f'{FAST_OUT}.tmp{os.getpid()}'   # per process: ranks that start together never share it
     cmd = fast_command(tmp)
@@ -77,21 +107,45 @@ def build_fast(force=False, verbose=False):
     return FAST_OUT
 
 
+def _run(cmd, what, verbose):
+    if verbose:
+        print(' '.join(cmd))
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f'{what} failed ({res.returncode}):\n{res.stderr[-4000:]}')
+
+
+def build_lib(out=OUT, extra=(), verbose=False):
+    """hipcc every source to an object in parallel (the translation units share no device code),
+    then link them: the same command() flags, a fraction of the wall time of one serial hipcc."""
+    from concurrent.futures import ThreadPoolExecutor
+    cmd = command(out, extra)
+    i = cmd.index('-o')
+    flags, srcs = [c for c in cmd[1:i] if c != '-shared'], cmd[i + 2:]
+    tag = f'{os.getpid()}_{abs(hash(tuple(extra))) % 10**8}'
+    objs = [f'{out}.{os.path.splitext(os.path.basename(src))[0]}.{tag}.o' for src in srcs]
+    try:
+        with ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as pool:
+            for f in [pool.submit(_run, [cmd[0], *flags, '-c', src, '-o', obj], f'hipcc {src}',
+                                  verbose) for src, obj in zip(srcs, objs)]:
+                f.result()
+        tmp = f'{out}.tmp{os.getpid()}'   # per process: ranks that start together never share it
+        _run([cmd[0], f'--offload-arch={ARCH}', '-shared', '-fPIC', *objs, '-o', tmp], 'hipcc link',
+             verbose)
+        os.replace(tmp, out)
+    finally:
+        for obj in objs:
+            if os.path.exists(obj):
+                os.remove(obj)
+    return out
+
+
 def build(force=False, verbose=False):
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     build_fast(force, verbose)
     if not force and not _stale(OUT):
         return OUT
-    cmd = command()
-    if verbose:
-        print(' '.join(cmd))
-    tmp = f'{OUT}.tmp{os.getpid()}'
-    cmd[cmd.index(OUT)] = tmp
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError(f'hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}')
-    os.replace(tmp, OUT)
-    return OUT
+    return build_lib(OUT, verbose=verbose)
 
 
 if __name__ == '__main__':

@@ -4,7 +4,10 @@
 
 #include "common.hpp"
 
-#define SPHRT_VERSION "sph_raytracer_amd 0.1 (gfx950)"
+#ifndef SPHRT_SOURCE_HASH   // set by build.py: a hash of the sources and flags (build.source_hash)
+#define SPHRT_SOURCE_HASH "unhashed"
+#endif
+#define SPHRT_VERSION "sph_raytracer_amd 0.3 (gfx950) src " SPHRT_SOURCE_HASH
 
 namespace sphrt {
 

@@ -1692,7 +1692,9 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
         // tables, 5 per CU (C5 forward f64 62.1 -> 53.0 us, transposed adjoint 58.8 -> 53.7 us).
         // Not below: C3's 34.8 KB tables (4 per CU) measured 364 -> 383 us with halves (more
         // resident workgroups, more L2 misses; few of its tables even need the second phase).
-        const bool half = sizeof(T) == 8 && edma && (size_t)(c->tab_stride + 1) * 32 > 40 * 1024 &&
+        // (the half-table kernel exists for the default segments per thread only: P == kPer)
+        const bool half = sizeof(T) == 8 && P == kPer && edma &&
+                          (size_t)(c->tab_stride + 1) * 32 > 40 * 1024 &&
                           c->tab_stride <= 2 * kHalfTab && half_tables_on();
         size_t lds = (size_t)((half ? kHalfTab
                                : edma ? imax64(c->tab_stride, kGranEarly * kThreads)

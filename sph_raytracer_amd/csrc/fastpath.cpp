@@ -176,4 +176,17 @@ PyModuleDef module = {PyModuleDef_HEAD_INIT, "_sphrt_fast", nullptr, -1, methods
 
 }  // namespace
 
-PyMODINIT_FUNC PyInit__sphrt_fast() { return PyModule_Create(&module); }
+#ifndef SPHRT_SOURCE_HASH
+#define SPHRT_SOURCE_HASH "unhashed"
+#endif
+
+// the tree this entry was built from (build.source_hash(); checked by _lib.load_fast)
+PyMODINIT_FUNC PyInit__sphrt_fast() {
+    PyObject* m = PyModule_Create(&module);
+    if (m && PyModule_AddStringConstant(m, "version",
+                                        "sph_raytracer_amd fastpath src " SPHRT_SOURCE_HASH) < 0) {
+        Py_DECREF(m);
+        return nullptr;
+    }
+    return m;
+}

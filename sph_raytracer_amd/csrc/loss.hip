@@ -72,16 +72,25 @@ __global__ __launch_bounds__(kLossThreads) void neg_reg_kernel(
     block_partial(acc, part);
 }
 
-// Adam (torch.optim.Adam with fused=True: torch._fused_adam_'s per-element arithmetic, amsgrad
-// and maximize off) on float64 coefficients, with the NegRegularizer's gradient term and loss
-// partials folded in: one launch where the loop made three (neg_reg, the step-count add, the
-// fused step on 36 pieces).  The multiply-adds are the fused ones torch's ROCm build emits for
-// `beta1 * m + (1 - beta1) * g` and `beta2 * v + (1 - beta2) * g * g` (fma of the left product,
-// and of p * weight_decay + g), written out here since this library builds with
-// -ffp-contract=off: measured bitwise equal to torch._fused_adam_ over 20 steps with and without
-// weight decay, where the unfused and the right-product forms differ from step 1
-// (`test_adam_matches_torch_fused`).  Bias corrections from the device's pow and sqrt, as torch's
-// kernel computes them from its float32 step count.
+// Adam on float64 coefficients, with the NegRegularizer's gradient term and loss partials folded
+// in: one launch where the loop made three or more (neg_reg, the step-count add, the optimiser's
+// own launches).  Two arithmetics, each the per-element operation sequence of one of torch's
+// implementations (amsgrad and maximize off):
+//  - FOREACH = false: torch.optim.Adam(fused=True), torch._fused_adam_.  The multiply-adds are
+//    the fused ones torch's ROCm build emits for `beta1 * m + (1 - beta1) * g` and
+//    `beta2 * v + (1 - beta2) * g * g` (fma of the left product, and of p * weight_decay + g),
+//    written out here since this library builds with -ffp-contract=off: measured bitwise equal
+//    to torch._fused_adam_ over 20 steps with and without weight decay, where the unfused and the
+//    right-product forms differ from step 1 (`test_adam_matches_torch_fused`).  Bias corrections
+//    from the device's pow and sqrt, as torch's kernel computes them from its float32 step count.
+//  - FOREACH = true: the default Adam on GPU tensors (torch.optim.adam._multi_tensor_adam, what
+//    the reference's `optim(optim_vars, **kwargs)`, retrieval.py:84, runs on a CUDA/ROCm device):
+//    _foreach_add(g, p, alpha=wd), _foreach_lerp_(m, g, 1 - beta1), _foreach_mul_(v, beta2),
+//    _foreach_addcmul_(v, g, g, 1 - beta2), sqrt, / sqrt(1 - beta2^t), + eps,
+//    _foreach_addcdiv_(p, m, denom, -lr / (1 - beta1^t)); each functor's `a + s * x` is one
+//    fma in torch's ROCm build.  The bias corrections come from the host (Python floats, as
+//    torch computes them): `step_size` is the negative step, `bc2s` sqrt(1 - beta2^t).
+template <bool FOREACH>
 __global__ __launch_bounds__(kLossThreads) void adam_neg_kernel(
     double* __restrict__ param, const double* __restrict__ grad, double* __restrict__ exp_avg,
     double* __restrict__ exp_avg_sq, int64_t n, double lr, double beta1, double beta2, double eps,
@@ -98,31 +107,50 @@ __global__ __launch_bounds__(kLossThreads) void adam_neg_kernel(
         m0 = exp_avg[i0];
         v0 = exp_avg_sq[i0];
     }
-    if (threadIdx.x < 64) {
-        const double b1 = 1 - pow(beta1, step), b2s = sqrt(1 - pow(beta2, step));
-        if (threadIdx.x == 0) {
-            bc[0] = b1;
-            bc[1] = b2s;
+    double step_size, bc2s;
+    if constexpr (FOREACH) {
+        step_size = lr;            // (host: -lr / (1 - beta1^t))
+        bc2s = step;               // (host: sqrt(1 - beta2^t))
+    } else {
+        if (threadIdx.x < 64) {
+            const double b1 = 1 - pow(beta1, step), b2s = sqrt(1 - pow(beta2, step));
+            if (threadIdx.x == 0) {
+                bc[0] = b1;
+                bc[1] = b2s;
+            }
         }
+        __syncthreads();
+        step_size = lr / bc[0];
+        bc2s = bc[1];
     }
-    __syncthreads();
-    const double bc1 = bc[0], bc2s = bc[1];
-    const double step_size = lr / bc1;
     const double ob1 = 1 - beta1, ob2 = 1 - beta2;
     double acc = 0.0;
     for (int64_t i = i0; i < n; i += (int64_t)gridDim.x * kLossThreads) {
         const bool first = i == i0;
         double p = first ? p0 : param[i], g = first ? g0 : grad[i];
+        const double mo = first ? m0 : exp_avg[i], vo = first ? v0 : exp_avg_sq[i];
         if (part) {                                        // as neg_reg_kernel
             const double c = p > 0.0 ? 0.0 : p;
             acc += __builtin_fabs(c);
             if (p < 0.0) g = g - c_neg;
         }
-        if (weight_decay != 0) g = fma(p, weight_decay, g);
-        const double m = fma(beta1, first ? m0 : exp_avg[i], ob1 * g);
-        const double v = fma(beta2, first ? v0 : exp_avg_sq[i], ob2 * g * g);
-        const double denom = sqrt(v) / bc2s + eps;
-        const double pn = p - step_size * m / denom;
+        double m, v, pn;
+        if constexpr (FOREACH) {
+            if (weight_decay != 0) g = fma(weight_decay, p, g);
+            // lerp(m, g, w) with w = 1 - beta1 (ATen Lerp.h: the small-weight form below 0.5)
+            m = __builtin_fabs(ob1) < 0.5 ? fma(ob1, g - mo, mo) : fma(-(g - mo), 1.0 - ob1, g);
+            v = fma(ob2, g * g, vo * beta2);
+            double den = sqrt(v);
+            den = den / bc2s;
+            den = den + eps;
+            pn = fma(step_size, m / den, p);
+        } else {
+            if (weight_decay != 0) g = fma(p, weight_decay, g);
+            m = fma(beta1, mo, ob1 * g);
+            v = fma(beta2, vo, ob2 * g * g);
+            const double denom = sqrt(v) / bc2s + eps;
+            pn = p - step_size * m / denom;
+        }
         param[i] = pn;
         if (stage) stage[stage_col((uint32_t)i, sm)] = pn;   // the next forward's brick copy
         exp_avg[i] = m;
@@ -172,28 +200,55 @@ extern "C" int sphrt_neg_reg_f64(const double* d, int64_t n, double c_neg, doubl
     return check_launch("neg_reg");
 }
 
-extern "C" int sphrt_adam_neg_f64(double* param, const double* grad, double* exp_avg,
-                                  double* exp_avg_sq, int64_t n, double lr, double beta1,
-                                  double beta2, double eps, double weight_decay, double step,
-                                  double c_neg, double* partial_sums, const sphrt_csr* stage_of,
-                                  void* stream) {
-    if (n <= 0) return fail("sphrt_adam_neg_f64: empty volume");
+static int adam_launch(bool foreach, double* param, const double* grad, double* exp_avg,
+                       double* exp_avg_sq, int64_t n, double a, double beta1, double beta2,
+                       double eps, double weight_decay, double b, double c_neg,
+                       double* partial_sums, const sphrt_csr* stage_of, void* stream,
+                       const char* what) {
+    if (n <= 0) return fail("%s: empty volume", what);
     if (!param || !grad || !exp_avg || !exp_avg_sq) return fail("null buffer");
-    if (!(step >= 1)) return fail("sphrt_adam_neg_f64: step counts from 1");
     StageMap sm{};
     double* stage = nullptr;
     if (stage_of && staged(stage_of)) {
         if (!stage_map(stage_of, sm)) return fail("inconsistent brick staging fields");
         if (stage_of->n_cols != n)
-            return fail("sphrt_adam_neg_f64: %lld voxels, the CSR has %lld columns", (long long)n,
+            return fail("%s: %lld voxels, the CSR has %lld columns", what, (long long)n,
                         (long long)stage_of->n_cols);
         if (!stage_of->stage || (int64_t)sizeof(double) * stage_of->stage_cols > stage_of->stage_bytes)
             return fail("brick stage buffer missing or too small");
         stage = (double*)stage_of->stage;
     }
     StreamGuard guard(stream);
-    hipLaunchKernelGGL(adam_neg_kernel, dim3(loss_grid(n)), dim3(kLossThreads), 0,
-                       (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2,
-                       eps, weight_decay, step, c_neg, partial_sums, sm, stage);
-    return check_launch("adam_neg");
+    if (foreach)
+        hipLaunchKernelGGL(adam_neg_kernel<true>, dim3(loss_grid(n)), dim3(kLossThreads), 0,
+                           (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq, n, a, beta1,
+                           beta2, eps, weight_decay, b, c_neg, partial_sums, sm, stage);
+    else
+        hipLaunchKernelGGL(adam_neg_kernel<false>, dim3(loss_grid(n)), dim3(kLossThreads), 0,
+                           (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq, n, a, beta1,
+                           beta2, eps, weight_decay, b, c_neg, partial_sums, sm, stage);
+    return check_launch(what);
+}
+
+extern "C" int sphrt_adam_neg_f64(double* param, const double* grad, double* exp_avg,
+                                  double* exp_avg_sq, int64_t n, double lr, double beta1,
+                                  double beta2, double eps, double weight_decay, double step,
+                                  double c_neg, double* partial_sums, const sphrt_csr* stage_of,
+                                  void* stream) {
+    if (!(step >= 1)) return fail("sphrt_adam_neg_f64: step counts from 1");
+    return adam_launch(false, param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps,
+                       weight_decay, step, c_neg, partial_sums, stage_of, stream,
+                       "sphrt_adam_neg_f64");
+}
+
+extern "C" int sphrt_adam_foreach_neg_f64(double* param, const double* grad, double* exp_avg,
+                                          double* exp_avg_sq, int64_t n, double step_size,
+                                          double beta1, double beta2, double eps,
+                                          double weight_decay, double bc2_sqrt, double c_neg,
+                                          double* partial_sums, const sphrt_csr* stage_of,
+                                          void* stream) {
+    if (!(bc2_sqrt > 0)) return fail("sphrt_adam_foreach_neg_f64: bias correction must be > 0");
+    return adam_launch(true, param, grad, exp_avg, exp_avg_sq, n, step_size, beta1, beta2, eps,
+                       weight_decay, bc2_sqrt, c_neg, partial_sums, stage_of, stream,
+                       "sphrt_adam_foreach_neg_f64");
 }

@@ -58,13 +58,8 @@ def gd(f, y, model, coeffs=None, num_iterations=100, loss_fns=[SquareLoss()], op
     for v in optim_vars:
         v.requires_grad_()
     best_loss, best_coeffs = float('inf'), None
-    # A torch optimiser with a fused GPU step (Adam, AdamW, SGD, ...) takes it unless the caller
-    # chose an implementation: one kernel per step instead of ~10 multi-tensor launches, with
-    # the same update within rounding (C5: 0.42-0.52 -> 0.36 ms per iteration).
-    if ('foreach' not in kwargs and 'fused' not in kwargs and 'fused' in _init_args(optim)
-            and all(isinstance(v, t.Tensor) and v.is_cuda and v.is_floating_point()
-                    for v in optim_vars)):
-        kwargs['fused'] = True
+    # the optimiser exactly as the reference builds it (retrieval.py:84): torch's own default
+    # implementation choice (foreach on GPU tensors) unless the caller passes foreach=/fused=
     opt = optim(optim_vars, **kwargs)
     plan = _direct_plan(f, y, model, coeffs, loss_fns, optim_vars)
     if plan is not None:
@@ -137,8 +132,11 @@ def _direct_plan(f, y, model, coeffs, loss_fns, optim_vars):
         return None
     if len(optim_vars) != 1 or optim_vars[0] is not coeffs or coeffs.dtype != t.float64:
         return None     # (float64, the reference's coefficients: every scalar below is exact)
-    if not (isinstance(y, t.Tensor) and y.device == coeffs.device
-            and y.dtype in (t.float32, t.float64) and coeffs.is_cuda and coeffs.is_contiguous() and tuple(coeffs.shape) == tuple(f.grid.shape)):
+    if not (isinstance(y, t.Tensor) and coeffs.is_cuda and coeffs.device == f._cdev
+            and y.device == coeffs.device and y.dtype in (t.float32, t.float64)
+            and coeffs.is_contiguous() and tuple(coeffs.shape) == tuple(f.grid.shape)
+            and tuple(y.shape) == tuple(f._ray_shape)):
+        # (other devices, or a y the reference's SquareLoss would broadcast: the autograd loop)
         return None
     sq = neg = None
     for fn in loss_fns:
@@ -184,7 +182,7 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     yd = yd.contiguous()
     c_sq = sq.lam / yd.numel()
     c_neg = neg.lam / coeffs.numel() if neg is not None else 0.0
-    step = _split_fused_adam(opt, coeffs)
+    step = _split_adam(opt, coeffs)
     bar = _Bar(range(num_iterations), progress_bar)
     lib = _lib.load()
     n_meas, n_vox = yd.numel(), coeffs.numel()
@@ -209,7 +207,10 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
         return val if _unit(lam) else lam * val
 
     try:
-        with t.no_grad():
+        # every launch below on the coefficients' GPU, whatever device is current (the C entry
+        # points launch on the stream's device; torch's default stream handle is the current
+        # device's)
+        with t.no_grad(), t.cuda.device(coeffs.device):
             for it in bar:
                 opt.zero_grad()
                 d = coeffs.detach()
@@ -263,46 +264,58 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     return best, f(best), losses
 
 
-def _split_fused_adam(opt, coeffs):
-    """torch.optim.Adam(fused=True)'s step on `coeffs` as one sphrt_adam_neg_f64 launch, or None.
+def _split_adam(opt, coeffs):
+    """torch.optim.Adam's step on `coeffs` as one csrc/loss.hip launch, or None.
 
-    The fused step (torch._fused_adam_) runs one workgroup per 65536-element chunk of each
-    tensor: a 64^3 volume is 4 workgroups on a 256-CU GPU (78 us of a 0.32 ms C5 iteration; on
-    36 contiguous pieces, the most one launch takes, 15 us plus 5 us for the step counts).
-    csrc/loss.hip runs the same per-element arithmetic (bitwise: test_adam_matches_torch_fused)
-    over the whole volume with the NegRegularizer's gradient term folded in, and, given a
-    brick-staged forward descriptor (stage_of), writes the updated coefficients to its stage
-    too.  The optimiser's own state is left untouched (the loop owns the moments and the step
-    count)."""
+    The launch runs the per-element arithmetic of the implementation torch itself would pick for
+    this optimiser, bitwise: torch._fused_adam_ for Adam(fused=True) (sphrt_adam_neg_f64;
+    `test_adam_matches_torch_fused`), the multi-tensor foreach step for the default Adam on a GPU
+    tensor (sphrt_adam_foreach_neg_f64; `test_adam_matches_torch_foreach`) — the reference's own
+    `optim(optim_vars, **kwargs)` (retrieval.py:84).  Either way it is one launch over the whole
+    volume with the NegRegularizer's gradient term folded in, where torch runs ~10 foreach
+    launches (or a fused step of one workgroup per 65536 elements: a 64^3 volume is 4 workgroups
+    on a 256-CU GPU), and given a brick-staged forward descriptor (stage_of) it writes the
+    updated coefficients to its stage too.  The optimiser's own state is left untouched (the loop
+    owns the moments and the step count).  Anything else (amsgrad, maximize, capturable,
+    differentiable, tensor hyper-parameters, the single-tensor path): None, and opt.step() runs."""
     from . import _lib
     if type(opt) is not t.optim.Adam or len(opt.param_groups) != 1:
         return None
     grp = opt.param_groups[0]
-    if not (grp.get('fused') and not grp.get('amsgrad') and not grp.get('maximize')
-            and not grp.get('capturable') and not grp.get('differentiable')
-            and not grp.get('decoupled_weight_decay') and isinstance(grp['lr'], float)
+    if not (not grp.get('amsgrad') and not grp.get('maximize') and not grp.get('capturable')
+            and not grp.get('differentiable') and not grp.get('decoupled_weight_decay')
+            and all(isinstance(grp[k], float) for k in ('lr', 'eps', 'weight_decay'))
+            and all(isinstance(b, float) for b in grp['betas'])
             and len(grp['params']) == 1 and grp['params'][0] is coeffs):
+        return None
+    fused, foreach = grp.get('fused'), grp.get('foreach')
+    if not fused and foreach is None:       # torch's own resolution (Optimizer defaults)
+        from torch.optim.optimizer import _default_to_fused_or_foreach
+        _, foreach = _default_to_fused_or_foreach([coeffs], False, use_fused=False)
+    if not fused and not foreach:
         return None
     lib = _lib.load()
     flat = coeffs.detach().view(-1)
     m, v = t.zeros_like(flat), t.zeros_like(flat)
-    b1, b2 = (float(b) for b in grp['betas'])
-    lr, eps, wd = float(grp['lr']), float(grp['eps']), float(grp['weight_decay'])
+    b1, b2 = grp['betas']
+    lr, eps, wd = grp['lr'], grp['eps'], grp['weight_decay']
     count = [0]
 
     def step(g, c_neg, part, stream, stage_of=None):
         count[0] += 1
-        _lib.check(lib.sphrt_adam_neg_f64(_lib.ptr(flat), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v),
-                                          flat.numel(), lr, b1, b2, eps, wd, float(count[0]),
-                                          c_neg, _lib.ptr(part),
-                                          ctypes.byref(stage_of) if stage_of is not None else None,
-                                          stream), 'sphrt_adam_neg_f64')
+        stage = ctypes.byref(stage_of) if stage_of is not None else None
+        if fused:
+            _lib.check(lib.sphrt_adam_neg_f64(
+                _lib.ptr(flat), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), flat.numel(), lr, b1, b2,
+                eps, wd, float(count[0]), c_neg, _lib.ptr(part), stage, stream),
+                'sphrt_adam_neg_f64')
+            return
+        # the foreach step's bias corrections, as torch computes them (Python floats of the
+        # float32 step count)
+        st = float(count[0])
+        step_size = (lr / (1 - b1 ** st)) * -1
+        bc2_sqrt = (1 - b2 ** st) ** 0.5
+        _lib.check(lib.sphrt_adam_foreach_neg_f64(
+            _lib.ptr(flat), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), flat.numel(), step_size, b1, b2,
+            eps, wd, bc2_sqrt, c_neg, _lib.ptr(part), stage, stream), 'sphrt_adam_foreach_neg_f64')
     return step
-
-
-def _init_args(optim):
-    import inspect
-    try:
-        return inspect.signature(optim.__init__).parameters
-    except (TypeError, ValueError):
-        return {}

@@ -1,6 +1,7 @@
 """Generate golden vectors from the real reference (this container only; needs /root/reference).
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py          # trace / forward / adjoint fixtures
+    python tests/golden/make_golden.py pins     # dynamic gradients, multichannel, gd() run
 
 Every case stores its INPUTS (grid boundaries, ray starts, ray directions as the reference
 geometry produced them, densities, adjoint inputs) and the reference's OUTPUTS (non-zero trace
@@ -99,6 +100,106 @@ def solver_case():
     print(f'solvers: {n} rays -> {os.path.getsize(path) / 1e3:.0f} kB')
 
 
+def save_grad_case(name, grid, geom, pairs, note=''):
+    """Reference forward and autograd gradient of (op(x) * y).sum() for each (x, y) in `pairs`,
+    float64 and float32 (the backward gd() runs: raytracer.py:705-712 through autograd), with the
+    inputs (rays as the reference geometry produced them)."""
+    xs, rays = geom.ray_starts.clone(), geom.rays.clone()
+    op = RT.Operator(grid, geom)
+    out = dict(grid_arrays(grid), xs=xs.numpy(), rays=rays.numpy(),
+               ray_shape=np.array(op.lens.shape[:-1]), note=np.array(note))
+    for i, (d, y) in enumerate(pairs):
+        out[f'density{i}'] = d.to(tr.float64).numpy()
+        out[f'gy{i}'] = y.to(tr.float64).numpy()
+        for dt, tag in ((tr.float64, '64'), (tr.float32, '32')):
+            x = d.to(dt).clone().requires_grad_()
+            res = op(x)
+            (res * y.to(dt)).sum().backward()
+            out[f'fwd{tag}_{i}'] = res.detach().numpy()
+            out[f'grad{tag}_{i}'] = x.grad.numpy()
+    path = os.path.join(HERE, f'{name}.npz')
+    np.savez_compressed(path, **out)
+    print(f'{name}: rays={int(np.prod(op.lens.shape[:-1]))} pairs={len(pairs)} '
+          f'-> {os.path.getsize(path) / 1e3:.0f} kB')
+
+
+def gd_case(name='gd_circ16', n_iter=25):
+    """A reference gd() run: examples/static_retrieval.py's loop (FullyDenseModel, [SquareLoss(),
+    NegRegularizer()], lr 0.1, the reference's default Adam: retrieval.py:84-116, loss.py:92-95,
+    153-155) on a 16^3 grid seen by 12 ConeCirc views; stores the inputs, the measurement, every
+    iteration's loss values and the final coefficients.  Also prints how far the same run moves
+    when the measurement is perturbed by one ulp per value (the run's own rounding sensitivity,
+    which bounds any two correct implementations' agreement)."""
+    L, M, RET = R.loss, R.model, R.retrieval
+    grid = G.SphericalGrid(shape=(16, 16, 16))
+    geom = orbit(12, lambda p: G.ConeCircGeom(shape=(20, 16), pos=p, fov=(0, 45)))
+    xs, rays = geom.ray_starts.clone(), geom.rays.clone()
+    op = RT.Operator(grid, geom)
+    truth = tr.zeros(grid.shape, dtype=tr.float64)
+    truth[:, 8:, :8] = 1
+    truth[:, :8, 8:] = 1
+    meas = op(truth).detach()
+
+    def run(y):
+        fns = [L.SquareLoss(), L.NegRegularizer()]
+        c, yres, losses = RET.gd(op, y.clone(), M.FullyDenseModel(grid), lr=1e-1,
+                                 num_iterations=n_iter, loss_fns=fns, progress_bar=False)
+        return c.detach(), yres.detach(), [np.array(losses[f]) for f in fns]
+
+    coeffs, yres, (l_sq, l_neg) = run(meas)
+    g = np.random.default_rng(1)
+    m = meas.numpy()
+    pert = np.where(g.random(m.shape) < 0.5, np.nextafter(m, np.inf), np.nextafter(m, -np.inf))
+    c2, _, (s2, n2) = run(tr.from_numpy(pert))
+    print(f'{name}: 1-ulp measurement perturbation moves coeffs by '
+          f'{float((c2 - coeffs).abs().max()):.3g}, SquareLoss by '
+          f'{float(np.max(np.abs(s2 - l_sq) / np.abs(l_sq))):.3g} rel, NegRegularizer by '
+          f'{float(np.max(np.abs(n2 - l_neg))):.3g} abs')
+    out = dict(grid_arrays(grid), xs=xs.numpy(), rays=rays.numpy(),
+               ray_shape=np.array(op.lens.shape[:-1]), truth=truth.numpy(), meas=meas.numpy(),
+               loss_sq=l_sq, loss_neg=l_neg, coeffs=coeffs.numpy(), y_result=yres.numpy(),
+               lr=np.array(0.1), iterations=np.array(n_iter),
+               note=np.array('reference gd(): 16^3, 12 ConeCirc (20,16), SquareLoss + '
+                             'NegRegularizer, Adam lr 0.1 (default implementation), 25 iterations'))
+    path = os.path.join(HERE, f'{name}.npz')
+    np.savez_compressed(path, **out)
+    print(f'{name}: final SquareLoss {l_sq[-1]:.4g} (from {l_sq[0]:.4g}) -> '
+          f'{os.path.getsize(path) / 1e3:.0f} kB')
+
+
+def pins():
+    """Fixtures pinning the rows the trace fixtures do not: the dynamic adjoint (autograd through
+    the time-indexed gather), multichannel forwards, and a whole gd() retrieval."""
+    g = tr.Generator().manual_seed(21)
+    # dynamic: 6 views paired with 6 time slices (the dynamic_obs geometry) ...
+    grid = G.SphericalGrid(shape=(6, 12, 10, 14))
+    geom = orbit(6, lambda p: G.ConeCircGeom(shape=(16, 12), pos=p, fov=(0, 45)))
+    save_grad_case('dynamic_grad', grid, geom,
+                   [(tr.rand(grid.shape, generator=g, dtype=tr.float64),
+                     tr.rand(geom.shape, generator=g, dtype=tr.float64))],
+                   note='dynamic (6,12,10,14), 6 ConeCirc (16,12) views, view i <-> time i')
+    # ... and one detector seen at every time step (t = arange(T)[:, None, None, None])
+    grid = G.SphericalGrid(shape=(4, 12, 10, 14))
+    geom = G.ConeRectGeom((18, 22), pos=(4, 2, 1.5), fov=(40, 40))
+    save_grad_case('dynamic_single_grad', grid, geom,
+                   [(tr.rand(grid.shape, generator=g, dtype=tr.float64),
+                     tr.rand((4, 18, 22), generator=g, dtype=tr.float64))],
+                   note='dynamic (4,12,10,14), one ConeRect (18,22): every time step, every ray')
+    # multichannel static forwards: 3 channels, (2, 2) channels, and the preview3d shape
+    # (plotting.py:280-297: one channel per azimuth rotation, (Na, Nr, Ne, Na))
+    grid = G.SphericalGrid(shape=(12, 10, 14))
+    geom = G.ConeRectGeom((24, 20), pos=(5, 0.3, 1), fov=(45, 45))
+    pairs = [(tr.rand((C,) + tuple(grid.shape), generator=g, dtype=tr.float64),
+              tr.rand(tuple(C) + tuple(geom.shape) if isinstance(C, tuple) else
+                      (C,) + tuple(geom.shape), generator=g, dtype=tr.float64))
+             for C in (3, 14)]
+    pairs.append((tr.rand((2, 2) + tuple(grid.shape), generator=g, dtype=tr.float64),
+                  tr.rand((2, 2) + tuple(geom.shape), generator=g, dtype=tr.float64)))
+    save_grad_case('multichannel', grid, geom, pairs,
+                   note='static (12,10,14), ConeRect (24,20); channels 3, 14 (preview3d), (2,2)')
+    gd_case()
+
+
 def main():
     tr.manual_seed(0)
     # C1: examples/single_vantage.py geometry at the BASELINE (50, 100) detector
@@ -179,4 +280,6 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    # `make_golden.py`: the trace fixtures; `make_golden.py pins`: dynamic_grad,
+    # dynamic_single_grad, multichannel, gd_circ16
+    pins() if sys.argv[1:] == ['pins'] else main()

@@ -322,6 +322,34 @@ def test_library_builds_and_exports_header():
     assert lib.sphrt_scan_workspace_bytes(10_000) > 0
 
 
+def test_library_carries_the_tree_hash(tmp_path, monkeypatch):
+    """Both libraries embed the hash of the sources + flags they were built from; it equals this
+    tree's, build() decides staleness by it (not by file times), and a library built from other
+    sources is refused at load."""
+    from sph_raytracer_amd import _lib, build
+    build.build()
+    want = build.source_hash()
+    assert len(want) == 16
+    assert build.embedded_hash(build.OUT) == want == _lib.source_hash()
+    assert build.embedded_hash(build.FAST_OUT) == want
+    assert _lib.load_fast().version.endswith(want)
+    assert not build._stale(build.OUT)
+    fake = tmp_path / 'lib.so'
+    fake.write_bytes(b'\0sph_raytracer_amd 0.3 (gfx950) src 0123456789abcdef\0')
+    assert build.embedded_hash(str(fake)) == '0123456789abcdef' and build._stale(str(fake))
+    with pytest.raises(RuntimeError, match='rebuild'):
+        _lib._check_hash('sph_raytracer_amd 0.3 (gfx950) src 0123456789abcdef', 'x.so')
+    _lib._check_hash(f'sph_raytracer_amd 0.3 (gfx950) src {want}', 'x.so')
+    # a touched (not edited) source does not make the build stale
+    src = os.path.join(build.CSRC, 'api.hip')
+    st = os.stat(src)
+    try:
+        os.utime(src, (st.st_atime, st.st_mtime + 100))
+        assert not build._stale(build.OUT)
+    finally:
+        os.utime(src, (st.st_atime, st.st_mtime))
+
+
 def test_loss_abi_argument_checks():
     """The retrieval entry points reject bad arguments before touching the device: an empty
     problem, null buffers, a step count below 1, a staged CSR whose columns are not the

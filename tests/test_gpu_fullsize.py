@@ -1,0 +1,190 @@
+"""Parity at the full BASELINE sizes of C3 and C4, every ray against the C oracle.
+
+C3: (128,128,128) grid, 128-view orbit x ConeRect (128,256) = 4.19 M rays, ~115 M segments —
+the production path of the HBM roofline run: the multi-wave forward with (4,2,4) brick staging,
+run records and the alternating block order, its 32-bit-free (uint16) granule tables, and the
+transposed adjoint.  C4: dynamic (50,50,50,50) grid, 50-view orbit x ConeCirc (100,50), view i
+<-> time slice i: the time-paired CSR over 6.25 M columns (int32 granule tables, one contiguous
+block range per XCD) and its transposed adjoint (the gradient).
+
+The oracle traces every ray on the host (16 threads over view chunks; ~3 s at C3), so these are
+whole-config comparisons, not samples: per ray the canonical voxel sequence exactly and lengths
+within 1e-12 (golden_cases.compare_segments), line integrals within 1e-10 relative (float64) and
+1e-5 (float32), the adjoint / gradient volume within 1e-10 (float64) and 1e-5 (float32) of its
+largest magnitude.
+"""
+import math
+import os
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+import torch as tr
+
+import golden_cases as gc
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+THREADS = 16      # the GPU box's CPU share
+
+
+def _orbit(n_views, det, kind, grid_shape):
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom, SphericalGrid
+    grid = SphericalGrid(shape=grid_shape)
+    geoms = []
+    for th in tr.linspace(0, 2 * tr.pi, n_views):
+        pos = (5 * tr.cos(th), 5 * tr.sin(th), 1)
+        geoms.append(ConeRectGeom(det, pos=pos, fov=(45, 45)) if kind == 'rect'
+                     else ConeCircGeom(shape=det, pos=pos, fov=(0, 45)))
+    return grid, sum(geoms)
+
+
+def _oracle_trace(grid, geom):
+    """Every ray of `geom` through the C oracle (IEEE sqrt), one view per task -> per view
+    (ptr, vox, seg)."""
+    from oracle import oracle
+    from sph_raytracer_amd.raytracer import find_starts
+    oracle.use_mkl_sqrt(False)
+    shp = tuple(grid.shape)[-3:]
+    g = oracle.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy())
+    rays = geom.rays.numpy()
+    xs = np.broadcast_to(geom.ray_starts.numpy(), rays.shape)
+    n_views = rays.shape[0]
+
+    def one(v):
+        x = np.ascontiguousarray(xs[v].reshape(-1, 3))
+        d = np.ascontiguousarray(rays[v].reshape(-1, 3))
+        st = find_starts(grid, tr.from_numpy(x)).numpy()
+        return oracle.trace_segments(g, x, d, st)
+
+    oracle.load()
+    with ThreadPoolExecutor(THREADS) as pool:
+        views = list(pool.map(one, range(n_views)))
+    assert all(len(p) - 1 == math.prod(rays.shape[1:-1]) for p, _, _ in views)
+    return views, math.prod(shp)
+
+
+def _gpu_views(op, n_views):
+    """The GPU trace split per view (geometry order) on the host."""
+    ptr, vox, seg = (t.cpu().numpy() for t in op.segments())
+    per = (len(ptr) - 1) // n_views
+    out = []
+    for v in range(n_views):
+        p = ptr[v * per:(v + 1) * per + 1]
+        a, b = p[0], p[-1]
+        out.append((p - a, vox[a:b], seg[a:b]))
+    return out
+
+
+def _compare_all(ref_views, got_views, scale, what):
+    for v, (r, g) in enumerate(zip(ref_views, got_views)):
+        msg = gc.compare_segments(r, g, scale, f'{what} view {v}')
+        assert msg is None, msg
+
+
+def _flat(views):
+    ptrs, voxs, segs, base = [], [], [], 0
+    for p, v, s in views:
+        ptrs.append(p[:-1] + base)
+        voxs.append(v)
+        segs.append(s)
+        base += p[-1]
+    ptr = np.concatenate(ptrs + [np.array([base])])
+    return ptr, np.concatenate(voxs), np.concatenate(segs)
+
+
+@pytest.fixture(scope='module')
+def c3(gpu):
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(128, (128, 256), 'rect', (128, 128, 128))
+    op = Operator(grid, geom, device=gpu)
+    ref, n_vox = _oracle_trace(grid, geom)
+    return grid, geom, op, ref, n_vox
+
+
+def test_c3_full_trace_vs_oracle(c3):
+    """All 4.19 M C3 rays: voxel sequences exact, lengths 1e-12 (the production trace path)."""
+    grid, geom, op, ref, _ = c3
+    assert op._csr['n'] == 128 * 128 * 256 and op._csr['total'] > 100_000_000
+    _compare_all(ref, _gpu_views(op, 128), 5.1, 'C3')
+
+
+def test_c3_full_forward_and_adjoint_vs_oracle(c3, gpu):
+    """C3 forward (float64, float32) and transposed adjoint (float64, float32) over every ray /
+    voxel against the oracle's segments, through the product configuration: (4,2,4) brick
+    staging, run records, alternating block order (each call below flips it)."""
+    grid, geom, op, ref, n_vox = c3
+    desc = op._csr['desc']
+    assert tuple(desc.stage_brick) == (4, 2, 4) and desc.runs and desc.n_blocks > 256 * 6
+    ptr, vox, seg = _flat(ref)
+    ray = np.repeat(np.arange(len(ptr) - 1), np.diff(ptr))
+    g = tr.Generator().manual_seed(11)
+    x = tr.rand(grid.shape, dtype=tr.float64, generator=g)
+    y = tr.rand(tuple(geom.shape), dtype=tr.float64, generator=g)
+    want = np.bincount(ray, x.numpy().reshape(-1)[vox] * seg, minlength=len(ptr) - 1)
+    for dt, tol in ((tr.float64, gc.F64_RTOL), (tr.float32, gc.F32_RTOL)):
+        for _ in range(2):                         # both block orders
+            got = op(x.to(gpu, dt)).cpu().numpy().reshape(-1)
+            err = gc.rel_close(got, want, tol)
+            assert err <= tol, f'C3 forward {dt} rel err {err:.3g}'
+    want_t = np.bincount(vox, y.numpy().reshape(-1)[ray] * seg, minlength=n_vox)
+    scale = np.abs(want_t).max()
+    for dt, tol in ((tr.float64, 1e-10), (tr.float32, 1e-5)):
+        for _ in range(2):
+            got = op.T(y.to(gpu, dt)).cpu().numpy().reshape(-1)
+            err = float(np.abs(got - want_t).max() / scale)
+            assert err <= tol, f'C3 adjoint {dt} rel err {err:.3g}'
+
+
+@pytest.fixture(scope='module')
+def c4(gpu):
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(50, (100, 50), 'circ', (50, 50, 50, 50))
+    op = Operator(grid, geom, device=gpu, dynamic=True)
+    ref, n_vox = _oracle_trace(grid, geom)
+    return grid, geom, op, ref, n_vox
+
+
+def test_c4_full_trace_vs_oracle(c4):
+    """All 250 k C4 rays (ConeCirc wedge trace order, reordered to geometry order)."""
+    grid, geom, op, ref, _ = c4
+    assert op._csr['ray_id'] is not None
+    _compare_all(ref, _gpu_views(op, 50), 5.1, 'C4')
+
+
+def test_c4_full_forward_and_gradient_vs_oracle(c4, gpu):
+    """C4 dynamic forward (view i reads time slice i) and its gradient (autograd: the transposed
+    time-paired CSR), float64 and float32, against the oracle; the time-paired CSR spans 6.25 M
+    columns, so its granule tables are int32."""
+    grid, geom, op, ref, n_vox = c4
+    ptr, vox, seg = _flat(ref)
+    n = len(ptr) - 1
+    per_view = n // 50
+    ray = np.repeat(np.arange(n), np.diff(ptr))
+    t_of = ray // per_view
+    g = tr.Generator().manual_seed(12)
+    x = tr.rand(grid.shape, dtype=tr.float64, generator=g)
+    # the C4 density pattern plus noise, so every slice differs
+    x[:, :, 25:, :25] += 1
+    for t in range(50):
+        x[t, :, (2 * t) % 50, :] += 1
+    y = tr.rand(tuple(geom.shape), dtype=tr.float64, generator=g)
+    col = t_of * n_vox + vox
+    want = np.bincount(ray, x.numpy().reshape(-1)[col] * seg, minlength=n)
+    want_g = np.bincount(col, y.numpy().reshape(-1)[ray] * seg, minlength=50 * n_vox)
+    scale = np.abs(want_g).max()
+    for dt, tol, gtol in ((tr.float64, gc.F64_RTOL, 1e-10), (tr.float32, gc.F32_RTOL, 1e-5)):
+        for _ in range(2):
+            xd = x.to(gpu, dt).requires_grad_()
+            out = op(xd)
+            assert tuple(out.shape) == (50, 100, 50)
+            err = gc.rel_close(out.detach().cpu().numpy().reshape(-1), want, tol)
+            assert err <= tol, f'C4 forward {dt} rel err {err:.3g}'
+            (out * y.to(gpu, dt)).sum().backward()
+            err = float(np.abs(xd.grad.cpu().numpy().reshape(-1) - want_g).max() / scale)
+            assert err <= gtol, f'C4 gradient {dt} rel err {err:.3g}'
+    rec = op._paired(50, per_view)
+    assert rec is not None and rec['desc'].n_cols == 50 * n_vox and rec['desc'].tab_bytes == 4
+    assert rec['desc'].order & 2          # one contiguous block range per XCD

@@ -599,10 +599,12 @@ def test_workgroup_orders_cover_every_block(grid_shape, n_views, det, order, gpu
     assert float((gott - reft).abs().max()) <= 1e-12 * float(reft.abs().max())
 
 
-def test_gd_fused_optimiser_matches_foreach(gpu):
-    """gd() gives a torch optimiser its fused GPU step unless the caller picks one: the same loss
-    history, coefficients and reconstruction as the multi-tensor (foreach) Adam within rounding
-    (relative 1e-9 after 30 steps); the masks/weights of 1 that the losses skip change nothing."""
+def test_gd_optimiser_as_the_reference_builds_it(gpu):
+    """gd() builds the optimiser exactly as the reference does (retrieval.py:84: no implementation
+    chosen for the caller, so torch's default multi-tensor step on GPU tensors); an explicit
+    Adam(fused=True) gives the same loss history, coefficients and reconstruction within
+    rounding (relative 1e-9 after 30 steps); the masks/weights of 1 that the losses skip change
+    nothing."""
     from sph_raytracer_amd import Operator, retrieval
     from sph_raytracer_amd.loss import CheaterLoss, NegRegularizer, SquareLoss
     from sph_raytracer_amd.model import FullyDenseModel
@@ -612,14 +614,25 @@ def test_gd_fused_optimiser_matches_foreach(gpu):
     x[:, :8, 8:] = 1
     op = Operator(grid, geom, device=gpu)
     meas = op(x)
+    made = []
+    orig = tr.optim.Adam.__init__
+
+    def spy(self, params, **kw):
+        made.append(dict(kw))
+        orig(self, params, **kw)
+
     runs = []
-    for kw, fns in (({}, [0.5 * SquareLoss(), NegRegularizer(), CheaterLoss(x)]),
-                    ({'foreach': True}, [SquareLoss(lam=0.5, projection_mask=tr.ones_like(meas)),
-                                         NegRegularizer(volume_mask=tr.ones_like(x)),
-                                         CheaterLoss(x)])):
-        c, yh, hist = retrieval.gd(op, meas, FullyDenseModel(grid), lr=1e-1, num_iterations=30,
-                                   loss_fns=fns, progress_bar=False, **kw)
+    for kw, fns in (({'fused': True}, [0.5 * SquareLoss(), NegRegularizer(), CheaterLoss(x)]),
+                    ({}, [SquareLoss(lam=0.5, projection_mask=tr.ones_like(meas)),
+                          NegRegularizer(volume_mask=tr.ones_like(x)), CheaterLoss(x)])):
+        tr.optim.Adam.__init__ = spy
+        try:
+            c, yh, hist = retrieval.gd(op, meas, FullyDenseModel(grid), lr=1e-1, num_iterations=30,
+                                       loss_fns=fns, progress_bar=False, **kw)
+        finally:
+            tr.optim.Adam.__init__ = orig
         runs.append((c.detach().clone(), yh.detach().clone(), list(hist.values())))
+    assert made == [{'fused': True, 'lr': 1e-1}, {'lr': 1e-1}]     # nothing added to the caller's
     (ca, ya, ha), (cb, yb, hb) = runs
     for a, b in zip(ha, hb):
         assert len(a) == len(b) == 30
@@ -946,9 +959,56 @@ def test_gd_direct_brick_staged(gpu, monkeypatch):
     assert tr.equal(staged[cols], ca.reshape(-1)[::997])
 
 
+@pytest.mark.parametrize('wd', [0.0, 0.01])
+@pytest.mark.parametrize('c_neg', [None, 0.3])
+@pytest.mark.parametrize('beta1', [0.9, 0.3])
+def test_adam_matches_torch_foreach(wd, c_neg, beta1, gpu):
+    """sphrt_adam_foreach_neg_f64 gives torch.optim.Adam's default GPU step (foreach=True, the
+    multi-tensor path the reference's `optim(optim_vars)` takes on a ROCm tensor) bitwise over 20
+    steps of gradients spanning four decades: parameters and both moments, with and without
+    weight decay, both lerp forms (1 - beta1 below / above 0.5), the regulariser folded in as
+    sphrt_neg_reg_f64 on the gradient first."""
+    from sph_raytracer_amd import _lib
+    lib = _lib.load()
+    n = 70001
+    gen = tr.Generator(device='cpu').manual_seed(4)
+    p0 = tr.randn(n, generator=gen, dtype=tr.float64).to(gpu)
+    pa, pb = p0.clone(), p0.clone()
+    mb, vb = (tr.zeros(n, dtype=tr.float64, device=gpu) for _ in range(2))
+    opt = tr.optim.Adam([pa], lr=0.01, betas=(beta1, 0.999), eps=1e-8, weight_decay=wd,
+                        foreach=True)
+    np_ = lib.sphrt_loss_partials(n)
+    stream = _lib.stream_of(gpu)
+    for it in range(20):
+        g = tr.randn(n, generator=gen, dtype=tr.float64).to(gpu) * 10.0 ** (it % 4 - 2)
+        ga = g.clone()
+        part_a = tr.empty(np_, dtype=tr.float64, device=gpu)
+        part_b = tr.full((np_,), float('nan'), dtype=tr.float64, device=gpu)
+        if c_neg is not None:
+            _lib.check(lib.sphrt_neg_reg_f64(_lib.ptr(pa), n, c_neg, _lib.ptr(ga),
+                                             _lib.ptr(part_a), stream), 'neg_reg')
+        pa.grad = ga
+        opt.step()
+        st = float(it + 1)
+        _lib.check(lib.sphrt_adam_foreach_neg_f64(
+            _lib.ptr(pb), _lib.ptr(g), _lib.ptr(mb), _lib.ptr(vb), n, (0.01 / (1 - beta1 ** st)) * -1,
+            beta1, 0.999, 1e-8, wd, (1 - 0.999 ** st) ** 0.5, c_neg or 0.0,
+            _lib.ptr(part_b if c_neg is not None else None), None, stream), 'adam_foreach')
+        state = opt.state[pa]
+        for name, a, b in (('param', pa, pb), ('exp_avg', state['exp_avg'], mb),
+                           ('exp_avg_sq', state['exp_avg_sq'], vb)):
+            if not tr.equal(a, b):
+                k = int((a != b).nonzero()[0])
+                pytest.fail(f'step {it}: {name} differs at {int((a != b).sum())} of {n} '
+                            f'elements, first {k}: {a[k].item()!r} vs {b[k].item()!r}')
+        if c_neg is not None:
+            assert tr.equal(part_a, part_b), it
+
+
+@pytest.mark.parametrize('optim_kw', [{}, {'fused': True}])
 @pytest.mark.parametrize('lams, meas_dtype', [((1, 1), tr.float64), ((0.5, 2), tr.float64),
                                               ((1, None), tr.float32)])
-def test_gd_direct_matches_autograd(lams, meas_dtype, gpu, monkeypatch):
+def test_gd_direct_matches_autograd(lams, meas_dtype, optim_kw, gpu, monkeypatch):
     """The static_retrieval.py loop without autograd (retrieval._gd_direct: forward, residual,
     adjoint, -lam/N on negative voxels, Adam) gives the autograd loop's iterates bitwise: the
     same coefficients and reconstruction, for unit and non-unit weights, with and without the
@@ -977,7 +1037,7 @@ def test_gd_direct_matches_autograd(lams, meas_dtype, gpu, monkeypatch):
             monkeypatch.setattr(retrieval, '_direct_plan', lambda *a: None)
         fns = [lams[0] * SquareLoss()] + ([lams[1] * NegRegularizer()] if lams[1] else [])
         c, yh, hist = retrieval.gd(op, meas.clone(), FullyDenseModel(grid), lr=1e-1,
-                                   num_iterations=25, loss_fns=fns, progress_bar=False)
+                                   num_iterations=25, loss_fns=fns, progress_bar=False, **optim_kw)
         runs.append((c.detach().clone(), yh.detach().clone(), list(hist.values())))
     assert len(calls) == 1
     (ca, ya, ha), (cb, yb, hb) = runs
@@ -985,3 +1045,49 @@ def test_gd_direct_matches_autograd(lams, meas_dtype, gpu, monkeypatch):
     for la, lb in zip(ha, hb):
         assert np.allclose(la, lb, rtol=1e-13, atol=0), (la, lb)
     assert tr.equal(ca, cb) and tr.equal(ya, yb)
+
+
+def test_gd_direct_declines_what_it_cannot_run(gpu, monkeypatch):
+    """_direct_plan hands the autograd loop every call it does not cover exactly: a
+    measurement with an extra leading singleton dimension (the reference's SquareLoss broadcasts
+    it) runs and gives the same iterates as the exact-shape call; coefficients on another device
+    than the operator's are declined too.  With two GPUs, a direct loop on an operator built on
+    cuda:1 while cuda:0 is current equals the cuda:0 one."""
+    from sph_raytracer_amd import Operator, retrieval
+    from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
+    from sph_raytracer_amd.model import FullyDenseModel
+    grid, geom = _orbit(6, (20, 16), kind='circ', grid_shape=(16, 16, 16))
+    x = tr.zeros(grid.shape, dtype=tr.float64, device=gpu)
+    x[:, 8:, :8] = 1
+    op = Operator(grid, geom, device=gpu)
+    meas = op(x)
+    calls = []
+    direct = retrieval._gd_direct
+
+    def spy(*a, **k):
+        calls.append(1)
+        return direct(*a, **k)
+
+    monkeypatch.setattr(retrieval, '_gd_direct', spy)
+    fns = [SquareLoss(), NegRegularizer()]
+    ca, _, ha = retrieval.gd(op, meas.clone(), FullyDenseModel(grid), lr=1e-1, num_iterations=8,
+                             loss_fns=fns, progress_bar=False)
+    assert len(calls) == 1
+    cb, _, hb = retrieval.gd(op, meas.clone()[None], FullyDenseModel(grid), lr=1e-1,
+                             num_iterations=8, loss_fns=fns, progress_bar=False)
+    assert len(calls) == 1                     # the broadcasting call took the autograd loop
+    assert tr.equal(ca, cb)
+    for a, b in zip(ha.values(), hb.values()):
+        assert np.allclose(a, b, rtol=1e-13, atol=0)
+    cpu_coeffs = tr.ones(grid.shape, dtype=tr.float64, requires_grad=True)
+    assert retrieval._direct_plan(op, meas, FullyDenseModel(grid), cpu_coeffs, fns,
+                                  [cpu_coeffs]) is None
+    if tr.cuda.device_count() < 2:
+        pytest.skip('one GPU: the cross-device half needs two')
+    dev1 = tr.device('cuda', 1)
+    with tr.cuda.device(0):
+        op1 = Operator(grid, geom, device=dev1)
+        c1, _, h1 = retrieval.gd(op1, meas.to(dev1), FullyDenseModel(grid), lr=1e-1,
+                                 num_iterations=8, loss_fns=fns, progress_bar=False)
+    assert len(calls) == 2 and c1.device == dev1
+    assert tr.equal(c1.cpu(), ca.cpu())

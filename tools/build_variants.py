@@ -5,7 +5,6 @@
     SPHRT_LIB=sph_raytracer_amd/lib/variants/libsphrt_NAME.so python tools/prof_forward.py
 """
 import os
-import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -20,8 +19,7 @@ def main(specs):
     for spec in specs:
         name, _, flags = spec.partition('=')
         out = os.path.join(VDIR, f'libsphrt_{name}.so')
-        cmd = build.command(out, [f for f in flags.split(',') if f])
-        subprocess.run(cmd, check=True)
+        build.build_lib(out, [f for f in flags.split(',') if f])
         print(out)
 
 
