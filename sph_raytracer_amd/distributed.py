@@ -6,10 +6,13 @@ Rays are independent, so each rank traces and integrates only its own contiguous
   - forward: the image stack, gathered with one all_gather (padded to the largest shard);
   - static adjoint / gradient: one all_reduce(sum) of the volume (1-17 MB);
   - dynamic grids: view i pairs with time slice i, so every rank owns disjoint time slices and
-    its adjoint needs no reduction at all.
+    its adjoint needs no reduction at all (the full adjoint is one all-gather of the slices);
+  - data-parallel retrieval: one all_reduce(sum) of the coefficient gradient per iteration.
 
 The reference has no distributed code; the single-GPU semantics are Operator's (raytracer.py).
 """
+import math
+
 import torch as tr
 import torch.distributed as dist
 
@@ -57,6 +60,41 @@ class ShardedOperator:
         self.device = getattr(self.local, 'device', device)
         self.view_shape = tuple(geom.shape[1:])
 
+    # -- collectives (RCCL for GPU tensors; gloo — CPU runs and one-GPU rehearsals — through host
+    #    copies, since gloo's GPU support is partial) ---------------------------------------------
+    def _host_staged(self, t):
+        return t.is_cuda and dist.get_backend(self.group) != 'nccl'
+
+    def all_reduce(self, t):
+        """In-place sum over the group (one RCCL all_reduce on GPUs)."""
+        if self._host_staged(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def _all_gather_rows(self, local, lead):
+        """Every rank's `local` (lead..., n_local, P) -> (lead..., n_obs, P) on every rank: one
+        all-gather of blocks padded to the largest shard (RCCL all_gather_into_tensor)."""
+        n_loc = self.hi - self.lo
+        width = max(h - l for l, h in self.bounds)
+        pad = tr.zeros(lead + (width, local.shape[-1]), dtype=local.dtype, device=local.device)
+        pad[..., :n_loc, :] = local
+        pad = pad.movedim(len(lead), 0).contiguous()          # (width, *lead, P)
+        out = tr.empty((self.world,) + tuple(pad.shape), dtype=pad.dtype, device=pad.device)
+        if self._host_staged(pad):
+            ho = out.cpu()
+            dist.all_gather(list(ho.unbind(0)), pad.cpu(), group=self.group)
+            out.copy_(ho)
+        elif dist.get_backend(self.group) == 'nccl':
+            dist.all_gather_into_tensor(out, pad, group=self.group)     # one RCCL all-gather
+        else:
+            dist.all_gather(list(out.unbind(0)), pad, group=self.group)
+        parts = [out[r, :h - l] for r, (l, h) in enumerate(self.bounds)]
+        return tr.cat(parts, dim=0).movedim(0, len(lead))         # (*lead, n_obs, P)
+
     # -- forward ---------------------------------------------------------------------------------
     def _local_density(self, density):
         if self.grid.dynamic:     # view i sees time slice i: keep this rank's slices
@@ -66,25 +104,16 @@ class ShardedOperator:
         return density
 
     def __call__(self, density):
-        """This rank's line integrals: (C..., n_local, *view) static / (n_local, *view) dynamic."""
+        """This rank's line integrals: (C..., n_local, *view) static / (n_local, *view) dynamic.
+        Differentiable: the gradient reaches this rank's share (all of a static density, its own
+        time slices of a dynamic one); sum it over ranks (all_reduce) for the full gradient."""
         return self.local(self._local_density(density))
 
     def gather(self, y_local):
         """All-gather the per-rank image stacks -> (C..., n_obs, *view) on every rank."""
         lead = tuple(y_local.shape[:-1 - len(self.view_shape)])
-        n_loc = self.hi - self.lo
-        width = max(h - l for l, h in self.bounds)
-        flat = y_local.detach().reshape(lead + (n_loc, -1))
-        pad = tr.zeros(lead + (width, flat.shape[-1]), dtype=flat.dtype, device=flat.device)
-        pad[..., :n_loc, :] = flat
-        pad = pad.movedim(len(lead), 0).contiguous()          # (width, *lead, P)
-        out = tr.empty((self.world,) + tuple(pad.shape), dtype=pad.dtype, device=pad.device)
-        if dist.get_backend(self.group) == 'nccl':
-            dist.all_gather_into_tensor(out, pad, group=self.group)     # one RCCL all-gather
-        else:
-            dist.all_gather(list(out.unbind(0)), pad, group=self.group)
-        parts = [out[r, :h - l] for r, (l, h) in enumerate(self.bounds)]
-        full = tr.cat(parts, dim=0).movedim(0, len(lead))      # (*lead, n_obs, P)
+        flat = y_local.detach().reshape(lead + (self.hi - self.lo, -1))
+        full = self._all_gather_rows(flat, lead)
         return full.reshape(lead + (self.n_obs,) + self.view_shape)
 
     def forward_full(self, density):
@@ -92,40 +121,72 @@ class ShardedOperator:
         return self.gather(self(density))
 
     # -- adjoint ---------------------------------------------------------------------------------
+    def T_local(self, y_local):
+        """Back-projection of this rank's own views (n_local, *view), no communication: a
+        partial volume (static grid; summed over ranks it is T of the whole stack) or this rank's
+        own time slices (n_local, nr, ne, na) (dynamic grid)."""
+        y = tr.as_tensor(y_local)
+        if not self.grid.dynamic:
+            return self.local.T(y)
+        dshape = (self.hi - self.lo,) + tuple(self.grid.shape[1:])
+        return self.local._apply_adjoint(y, dshape, y.dtype, y.device)
+
     def T(self, line_integrations):
-        """Back-projection of the full (n_obs, *view) stack: each rank back-projects its views,
-        then one all_reduce(sum) of the volume (static grids)."""
-        if self.grid.dynamic:
-            raise NotImplementedError('use T_local: dynamic shards own disjoint time slices')
+        """Back-projection of the full (n_obs, *view) stack on every rank.  Static grid: each
+        rank back-projects its views, then one all_reduce(sum) of the volume.  Dynamic grid
+        (view i <-> time slice i; the reference's Operator.T raises for it, raytracer.py:733):
+        each rank back-projects its views into its own slices, then one all-gather of the
+        slices."""
         y = tr.as_tensor(line_integrations)
-        vol = self.local.T(y[self.lo:self.hi])
-        dist.all_reduce(vol, op=dist.ReduceOp.SUM, group=self.group)
-        return vol
+        vol = self.T_local(y[self.lo:self.hi])
+        if not self.grid.dynamic:
+            return self.all_reduce(vol)
+        g3 = tuple(self.grid.shape[1:])
+        full = self._all_gather_rows(vol.reshape(self.hi - self.lo, -1), ())
+        return full.reshape((self.n_obs,) + g3)
 
     def reduce_grad(self, grad):
         """Sum a replicated parameter's gradient over ranks (data-parallel retrieval)."""
-        dist.all_reduce(grad, op=dist.ReduceOp.SUM, group=self.group)
-        return grad
+        return self.all_reduce(grad)
+
+    @property
+    def n_measurements(self):
+        """Values in the whole (n_obs, *view) stack."""
+        return self.n_obs * math.prod(self.view_shape)
 
 
 def gd(f, y_local, model, coeffs=None, num_iterations=100, loss_fns=None, optim=tr.optim.Adam,
        progress_bar=False, device=None, **kwargs):
     """Data-parallel counterpart of retrieval.gd for a ShardedOperator (static grids).
 
-    Every rank holds replicated coefficients and its own measurement shard ``y_local``.  Each
-    iteration: local forward + local losses, backward, one all_reduce(sum) of the coefficient
-    gradient, identical optimiser step everywhere.  Fidelity losses are weighted by the rank's
-    share of the views so the summed gradient equals the single-GPU gradient of the full-stack
-    mean; regulariser gradients are divided by the world size (every rank computes them).
+    Every rank holds replicated coefficients and its own measurement shard ``y_local`` (its
+    views of the stack).  Each iteration: local forward, local adjoint, one all_reduce(sum) of
+    the coefficient gradient, the identical optimiser step on every rank; the losses are those of
+    the whole stack (SquareLoss: the mean over all n_obs views).
+
+    The static_retrieval.py loop (retrieval._direct_plan: FullyDenseModel, SquareLoss +
+    NegRegularizer, Adam, ...) runs autograd-free as on one GPU (retrieval._gd_direct) with the
+    all_reduce between its adjoint and its Adam launch; anything else takes the autograd loop,
+    where fidelity losses are weighted by the rank's share of the views so the summed gradient
+    equals the single-GPU gradient of the full-stack mean and regulariser gradients are divided
+    by the world size (every rank computes them).
+    Returns (coeffs, the full reconstructed stack, {loss_fn: [values]}).
     """
     from .loss import SquareLoss
-    from .retrieval import detach_loss
+    from .retrieval import _direct_plan, _gd_direct, detach_loss
     loss_fns = [SquareLoss()] if loss_fns is None else loss_fns
     share = (f.hi - f.lo) / f.n_obs
     if coeffs is None:
         coeffs = tr.ones(model.coeffs_shape, dtype=tr.float64, device=device or f.device)
     coeffs.requires_grad_()
     opt = optim([coeffs], **kwargs)
+    plan = _direct_plan(f.local, y_local, model, coeffs, loss_fns, [coeffs]) \
+        if hasattr(f.local, '_csr') else None
+    if plan is not None:
+        coeffs, _, losses = _gd_direct(f.local, y_local, coeffs, loss_fns, opt, plan,
+                                       num_iterations, progress_bar, reduce=f.all_reduce,
+                                       n_total=f.n_measurements)
+        return coeffs, f.gather(f(model(coeffs))), losses
     losses = {fn: [] for fn in loss_fns}
     for _ in range(num_iterations):
         opt.zero_grad()
@@ -139,7 +200,7 @@ def gd(f, y_local, model, coeffs=None, num_iterations=100, loss_fns=None, optim=
             v = tr.as_tensor(detach_loss(val) * (share if fn.kind == 'fidelity' else 1.0),
                              dtype=tr.float64, device=coeffs.device)
             if fn.kind == 'fidelity':
-                dist.all_reduce(v, group=f.group)
+                f.all_reduce(v)
             losses[fn].append(float(v))
         total.backward(retain_graph=True)
         f.reduce_grad(coeffs.grad)

@@ -154,7 +154,8 @@ def _direct_plan(f, y, model, coeffs, loss_fns, optim_vars):
     return sq, neg
 
 
-def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
+def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar, reduce=None,
+               n_total=None):
     """`gd` for `_direct_plan` loops: the same arithmetic as autograd's, op by op, so the
     iterates are the same (the Operator forward, the adjoint of the SquareLoss residual, the
     NegRegularizer's -lam/N on negative voxels, the optimiser step), without building and walking
@@ -169,7 +170,13 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     negated, i.e. (f(d) - y) * (2 * (lam / N)) exactly (scaling by 2 and negation are exact).
     Gradient of lam * mean(|clip(d, max=0)|): -(lam / N) where d < 0, else 0 (sign(0) = 0).
     The two are summed (IEEE addition commutes, so the order autograd accumulates them in does
-    not matter) and handed to the optimiser as coeffs.grad."""
+    not matter) and handed to the optimiser as coeffs.grad.
+
+    Data-parallel use (distributed.gd): `f` is this rank's operator over its share of the views,
+    `y` its share of the measurements, `n_total` the size of the whole stack (the SquareLoss
+    mean's N) and `reduce` an in-place sum over the ranks, applied to the adjoint's gradient
+    before the regulariser and the optimiser step (which are then identical on every rank) and
+    to the SquareLoss sums after the loop."""
     from . import _lib
     sq, neg = plan
     losses = {fn: [] for fn in loss_fns}
@@ -180,7 +187,8 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     if yd.dtype not in (t.float32, t.float64):
         yd = yd.to(coeffs.dtype)
     yd = yd.contiguous()
-    c_sq = sq.lam / yd.numel()
+    n_norm = yd.numel() if n_total is None else n_total     # the SquareLoss mean's N
+    c_sq = sq.lam / n_norm
     c_neg = neg.lam / coeffs.numel() if neg is not None else 0.0
     step = _split_adam(opt, coeffs)
     bar = _Bar(range(num_iterations), progress_bar)
@@ -202,8 +210,8 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
     part_neg = t.empty((rows, pn), dtype=t.float64, device=coeffs.device) if neg is not None else None
     done = 0
 
-    def scaled(parts, n, lam):
-        val = parts.sum(-1) / n
+    def scaled(sums, n, lam):
+        val = sums / n
         return val if _unit(lam) else lam * val
 
     try:
@@ -236,6 +244,8 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                     'sphrt_sq_residual_f64')
                 g = f._apply_adjoint(r_scaled, tuple(d.shape), d.dtype, d.device,
                                      trace_order=order is not None)
+                if reduce is not None:
+                    reduce(g)          # data-parallel: the sum of every rank's adjoint
                 if step is not None:
                     # the regulariser's gradient term and loss partials inside the Adam launch
                     step(g, c_neg, part_neg[it] if neg is not None else None, stream,
@@ -245,9 +255,9 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                     _lib.check(lib.sphrt_neg_reg_f64(_lib.ptr(d), n_vox, c_neg, _lib.ptr(g),
                                                      _lib.ptr(part_neg[it]), stream),
                                'sphrt_neg_reg_f64')
-                if progress_bar:
-                    fv = float(scaled(part_sq[it], n_meas, sq.lam))
-                    rv = float(scaled(part_neg[it], n_vox, neg.lam)) if neg is not None else 0
+                if progress_bar:      # (this rank's share of the SquareLoss when data-parallel)
+                    fv = float(scaled(part_sq[it].sum(), n_norm, sq.lam))
+                    rv = float(scaled(part_neg[it].sum(), n_vox, neg.lam)) if neg is not None else 0
                     bar.describe(f'F:{fv:.1e} R:{rv:.1e} O:0')
                 if step is None:
                     coeffs.grad = g
@@ -255,9 +265,12 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar):
                 done = it + 1
     except KeyboardInterrupt:
         pass
-    losses[sq] = scaled(part_sq[:done], n_meas, sq.lam).cpu().tolist()
+    sums = part_sq[:done].sum(-1)
+    if reduce is not None:
+        reduce(sums)
+    losses[sq] = scaled(sums, n_norm, sq.lam).cpu().tolist()
     if neg is not None:
-        losses[neg] = scaled(part_neg[:done], n_vox, neg.lam).cpu().tolist()
+        losses[neg] = scaled(part_neg[:done].sum(-1), n_vox, neg.lam).cpu().tolist()
     # the reference's bookkeeping: the coefficients once some iteration's total was < inf
     totals = [sum(v) for v in zip(*(losses[fn] for fn in loss_fns))]
     best = coeffs if any(v < float('inf') for v in totals) else None

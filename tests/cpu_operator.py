@@ -65,3 +65,7 @@ class CpuOperator:
 
     def T(self, y):
         return self._adj(tr.as_tensor(y), tuple(self.grid.shape))
+
+    def _apply_adjoint(self, y, dshape, ddtype, ddevice):
+        """Operator._apply_adjoint's contract (any grid, dynamic included)."""
+        return self._adj(tr.as_tensor(y), tuple(dshape)).to(device=ddevice, dtype=ddtype)

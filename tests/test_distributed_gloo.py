@@ -57,6 +57,8 @@ def _worker(rank, world, port, n_obs, out_q):
         dop = ShardedOperator(dgrid, dgeom, operator_factory=lambda g, lg, d: CpuOperator(g, lg))
         xd = tr.rand(dgrid.shape, dtype=tr.float64, generator=g)
         res['dyn'] = dop.forward_full(xd).numpy()
+        yd = tr.rand(dgeom.shape, dtype=tr.float64, generator=g)
+        res['dyn_T'] = dop.T(yd).numpy()          # each rank's slices, all-gathered
         # data-parallel retrieval, 5 Adam steps
         meas = sop.forward_full(x)
         y_loc = meas[sop.lo:sop.hi].clone()
@@ -87,7 +89,10 @@ def _single(n_obs):
     res = {'fwd': op(x).numpy(), 'fwd_mc': op(tr.stack([x, 2 * x])).numpy(), 'adj': op.T(y).numpy()}
     dgrid, dgeom = _geometry(n_obs, dynamic=True)
     xd = tr.rand(dgrid.shape, dtype=tr.float64, generator=g)
-    res['dyn'] = CpuOperator(dgrid, dgeom)(xd).numpy()
+    dop = CpuOperator(dgrid, dgeom)
+    res['dyn'] = dop(xd).numpy()
+    yd = tr.rand(dgeom.shape, dtype=tr.float64, generator=g)
+    res['dyn_T'] = dop._adj(yd, tuple(dgrid.shape)).numpy()
     meas = op(x).detach()
     coeffs, _, losses = gd(op, meas.clone(), FullyDenseModel(grid), num_iterations=5, lr=1e-1,
                            loss_fns=[SquareLoss(), NegRegularizer()], progress_bar=False)
@@ -116,6 +121,7 @@ def test_sharded_matches_single_process(world, n_obs):
         assert got[k].shape == ref[k].shape, k
         assert np.array_equal(got[k], ref[k]), k        # same per-ray sums, just regrouped
     assert np.allclose(got['adj'], ref['adj'], rtol=1e-12, atol=1e-14)
+    assert np.array_equal(got['dyn_T'], ref['dyn_T'])   # disjoint time slices: no reduction
     assert np.allclose(got['gd_loss'], ref['gd_loss'], rtol=1e-10)
     assert np.allclose(got['gd'], ref['gd'], rtol=1e-9, atol=1e-12)
 
