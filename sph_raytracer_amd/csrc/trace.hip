@@ -27,6 +27,7 @@
 #include "common.hpp"
 #include "introsort.hpp"
 #include "solve.hpp"
+#include "walk.hpp"
 
 namespace sphrt {
 
@@ -280,6 +281,9 @@ struct TraceOut {
     unsigned* n_hits;                // workspace: screened hit-ray counter
     HitRay* hits;                    // workspace: hit rays
     unsigned long long* n_over;      // EMIT: rays whose segments exceed their bound
+    unsigned* n_walk;                // workspace: walk-eligible hit-ray counter
+    int32_t* walk_rays;              // workspace: walk-eligible hit rays (walk_kernel)
+    int walk;                        // screen: send eligible rays to the walk (SPHRT_WALK != 0)
 };
 
 // EMIT: ray `ray` has `cnt` segments; its staging slot is [row_ptr[ray], row_ptr[ray + 1]) (the
@@ -776,12 +780,22 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
             for (int64_t c = 0; c < nc; ++c) o.out[c * o.out_chan_stride + ray] = (T)0;
         }
     }
-    const uint64_t m = __ballot(hit);
+    // hits the lane walk can take go to its list (ray ids), the rest to the list trace's
+    const bool walk = hit && o.walk && walk_eligible(G, g, t1c_outer, start_r_ok);
+    const uint64_t mw = __ballot(walk);
+    if (mw != 0) {
+        unsigned wb = 0;
+        if (lane == __builtin_ctzll(mw)) wb = atomicAdd(o.n_walk, (unsigned)__popcll(mw));
+        wb = __shfl(wb, __builtin_ctzll(mw));
+        if (walk) o.walk_rays[wb + __popcll(mw & lanemask_lt(lane))] = (int32_t)ray;
+    }
+    const bool listed = hit && !walk;
+    const uint64_t m = __ballot(listed);
     if (m == 0) return;
     unsigned base = 0;
     if (lane == __builtin_ctzll(m)) base = atomicAdd(o.n_hits, (unsigned)__popcll(m));
     base = __shfl(base, __builtin_ctzll(m));
-    if (hit) {
+    if (listed) {
         HitRay h;
         h.x[0] = x[0]; h.x[1] = x[1]; h.x[2] = x[2];
         h.d[0] = d[0]; h.d[1] = d[1]; h.d[2] = d[2];
@@ -789,6 +803,62 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
         h.ray = (int32_t)ray;
         o.hits[base + __popcll(m & lanemask_lt(lane))] = h;
     }
+}
+
+// ---- the lane walk (walk.hpp): one walk-eligible ray per lane ---------------------------------
+// Merges the four runs by (distance, candidate) and replays trace_one's rules on the merged
+// sequence: crossings before the outer sphere's entry t_lo only update the e / a rows (the start
+// lies outside, so its r row is -1 until the entry), the sequence from t_lo to the exit t_hi is
+// the list, and each segment between consecutive list entries gets the rows' values after the
+// first (trace_one steps 3-4).  A tie — exactly equal distances — of two crossings writing
+// different values into one row (the start entry at t = 0 included) defers the ray to the exact
+// kernel, like ambiguous_ties; a run out of order hands the ray to the list trace (appended to
+// its hit list, traced by trace_kernel afterwards).  Either way the later kernel rewrites the
+// ray's count and segments.  Segments are written straight to the ray's row (FILL / EMIT).
+template <int MODE, typename T>
+__global__ __launch_bounds__(256) void walk_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)*o.n_walk) return;
+    const int64_t ray = o.walk_rays[idx];
+    double x[3], d[3];
+    int s[3];
+    load_ray(R, ray, x, d, s);
+    const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
+    int64_t nseg = 0;
+    int64_t base = 0, cap = INT64_MAX;
+    if (MODE == MODE_FILL || MODE == MODE_EMIT) base = o.row_ptr[ray];
+    if (MODE == MODE_EMIT) cap = o.row_ptr[ray + 1] - base;
+    const T* rho = nullptr;
+    if (MODE == MODE_INTEGRATE)
+        rho = o.density + (o.ray_chan_div > 0 ? (ray / o.ray_chan_div) * o.chan_stride : 0);
+    double acc = 0.0;
+    // 1: tie (exact kernel), 2: out of order (list trace)
+    const int status = walk_ray(G, g, s, [&](int vx, double len) {
+        if (MODE == MODE_FILL || (MODE == MODE_EMIT && nseg < cap)) {
+            o.vox[base + nseg] = vx;
+            o.len[base + nseg] = len;
+        } else if (MODE == MODE_INTEGRATE) {
+            acc += (double)rho[vx] * len;
+        }
+        ++nseg;
+    });
+    if (status == 1) {
+        const unsigned long long q = atomicAdd(o.n_deferred, 1ull);
+        o.deferred[q] = ray;
+        return;
+    }
+    if (status == 2) {
+        HitRay hr;
+        hr.x[0] = x[0]; hr.x[1] = x[1]; hr.x[2] = x[2];
+        hr.d[0] = d[0]; hr.d[1] = d[1]; hr.d[2] = d[2];
+        hr.s[0] = s[0]; hr.s[1] = s[1]; hr.s[2] = s[2];
+        hr.ray = (int32_t)ray;
+        o.hits[atomicAdd(o.n_hits, 1u)] = hr;
+        return;
+    }
+    if (MODE == MODE_COUNT) o.counts[ray] = (int32_t)nseg;
+    if (MODE == MODE_EMIT) (void)emit_slot(o, ray, nseg, true);
+    if (MODE == MODE_INTEGRATE) o.out[ray] = (T)acc;   // (one channel: n_chan 1 or time slices)
 }
 
 // Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
@@ -1284,9 +1354,16 @@ static size_t exact_scratch_bytes(const GridDev& G) {   // lists of large-K grid
     return exact_in_lds(G) ? 0 : (size_t)kExactSerialBlocks * G.K * sizeof(Cand);
 }
 static size_t hits_bytes(int64_t n) { return (((size_t)n * sizeof(HitRay) + 255) / 256) * 256; }
+static size_t walk_bytes(int64_t n) { return (((size_t)n * sizeof(int32_t) + 255) / 256) * 256; }
 static size_t workspace_bytes(const GridDev& G, int64_t n) {
     return kWsHead + (((size_t)n * sizeof(int64_t) + 255) / 256) * 256 + hits_bytes(n) +
-           exact_scratch_bytes(G);
+           walk_bytes(n) + exact_scratch_bytes(G);
+}
+
+// SPHRT_WALK=0 keeps every hit ray on the list trace (A/B studies, tests; read at every launch).
+static bool walk_enabled() {
+    const char* e = getenv("SPHRT_WALK");
+    return !(e && e[0] == '0');
 }
 
 // Which launches of a trace a call makes: screen (hit list; counts/zeros/bounds of the misses)
@@ -1315,6 +1392,10 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     o.n_hits = (unsigned*)(ws + 64);
     o.deferred = (int64_t*)(ws + kWsHead);
     o.hits = (HitRay*)(ws + kWsHead + (((size_t)R.n * sizeof(int64_t) + 255) / 256) * 256);
+    o.n_walk = (unsigned*)(ws + 128);
+    o.walk_rays = (int32_t*)((unsigned char*)o.hits + hits_bytes(R.n));
+    // the walk integrates one channel per ray (a register accumulator)
+    o.walk = walk_enabled() && (MODE != MODE_INTEGRATE || o.n_chan == 1 || o.ray_chan_div > 0);
     Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
     if constexpr (MODE == MODE_BOUND) steps = kScreen;
     if constexpr (MODE == MODE_EMIT) steps = kTrace;
@@ -1328,6 +1409,12 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     }
     if constexpr (MODE == MODE_BOUND) return 0;
     if (!(steps & kTrace)) return 0;
+    if constexpr (MODE != MODE_BOUND) {
+        // the walk first: its out-of-order rays join the list trace's hit list
+        hipLaunchKernelGGL((walk_kernel<MODE, T>), dim3((unsigned)((R.n + 255) / 256)), dim3(256),
+                           0, st, G, R, o);
+        if (int e = check_launch("walk_kernel")) return e;
+    }
     // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
     const int64_t grid = 2048 * kWavesPerBlock / waves;
     hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,

@@ -1091,3 +1091,24 @@ def test_gd_direct_declines_what_it_cannot_run(gpu, monkeypatch):
                                  num_iterations=8, loss_fns=fns, progress_bar=False)
     assert len(calls) == 2 and c1.device == dev1
     assert tr.equal(c1.cpu(), ca.cpu())
+
+
+@pytest.mark.parametrize('kind, n_views, det, grid_shape', [
+    ('rect', 50, (50, 100), (50, 50, 50)),          # C2
+    ('circ', 64, (100, 50), (64, 64, 64)),          # C5 geometry (ring 0 through the origin)
+    ('rect', 12, (128, 256), (128, 128, 128)),      # C3 grid
+    ('circ', 9, (40, 30), (40, 70, 33)),
+])
+def test_walk_equals_list_trace_full_size(kind, n_views, det, grid_shape, gpu, monkeypatch):
+    """At full size the lane walk's CSR equals the list trace's bit for bit (the walk sends
+    tie-ambiguous rays to the exact kernel and rays whose run order fails to the list trace)."""
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(n_views, det, kind=kind, grid_shape=grid_shape)
+    monkeypatch.setenv('SPHRT_WALK', '0')
+    ref = Operator(grid, geom, device=gpu)._csr
+    monkeypatch.setenv('SPHRT_WALK', '1')
+    got = Operator(grid, geom, device=gpu)._csr
+    assert ref['total'] == got['total']
+    for k in ('row_ptr', 'vox', 'len'):
+        assert tr.equal(ref[k][:ref['total'] if k != 'row_ptr' else None],
+                        got[k][:got['total'] if k != 'row_ptr' else None]), k
