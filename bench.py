@@ -104,18 +104,59 @@ def kernel_time_ms(op, x, reps=50):
         return e0.elapsed_time(e1) / reps, 'back-to-back launches, HIP events'
 
 
-def cpu_baseline(cfg, sample_views, reps):
-    """Reference forward (torch CPU on the reference's padded trace) on a bounded sample."""
-    from oracle import ref_forward
-    from sph_raytracer_amd import ConeRectGeom, ConeCircGeom, SphericalGrid
+def cpu_cold_baseline(cfg, sample_views):
+    """The reference's cold path — Operator init (trace_indices, raytracer.py:48-230) + the first
+    forward (:703-713) — restated in torch CPU (oracle/ref_trace.py: the same materialised
+    solves, cat, sort, forward fill, diff and masks, calibrated bitwise and within +-20 % of the
+    reference's wall time, profiles/r03_ref_trace_calibration.json) and timed on this host's
+    cores on a bounded sample of the workload's views."""
+    from oracle import ref_forward, ref_trace
     from sph_raytracer_amd.raytracer import find_starts
+    shape, n_views, det, kind, dtype, _ = cfg
+    grid, geom = _cpu_sample(cfg, sample_views)
+    views = geom.rays.shape[0] if geom.rays.dim() == 4 else 1
+    xs = geom.ray_starts.broadcast_to(geom.rays.shape).reshape(-1, 3).clone()
+    rays = geom.rays.reshape(-1, 3).clone()
+    dyn = grid.dynamic
+    x = torch.rand((views,) + tuple(shape[1:]) if dyn else shape, dtype=dtype)
+    t0 = time.perf_counter()
+    starts = find_starts(grid, xs)
+    regs, lens = ref_trace.trace_dense(grid.r_b, grid.e_b, grid.a_b, xs, rays, starts)
+    hw = geom.rays.shape[-3:-1] if geom.rays.dim() >= 3 else ()
+    regs = regs.reshape((3, views) + tuple(hw) + (-1,)) if dyn else regs
+    lens = lens.reshape((views,) + tuple(hw) + (-1,)) if dyn else lens
+    ref_forward.forward(regs, lens, x, dynamic=dyn)
+    dt = time.perf_counter() - t0
+    n = len(xs)
+    return {'value': n / dt, 'unit': 'rays/s', 'seconds': dt, 'cores': torch.get_num_threads(),
+            'kind': 'port',
+            'sample': f'{views} of {n_views} views ({n} rays, K={lens.shape[-1]}): find_starts + '
+                      f'trace_indices restated in torch CPU (oracle/ref_trace.py) + the '
+                      f'reference forward, once (cold)'}
+
+
+def _cpu_sample(cfg, sample_views):
+    from sph_raytracer_amd import ConeRectGeom, ConeCircGeom, SphericalGrid
     shape, n_views, det, kind, dtype, _ = cfg
     grid = SphericalGrid(shape=shape)
     views = min(sample_views, n_views)
-    thetas = torch.linspace(0, 2 * torch.pi, n_views)[:views]
+    if kind == 'rect1':
+        return grid, ConeRectGeom(det, pos=(5, 0, 0), fov=(45, 45))
+    # evenly spread over the orbit (views differ in hit fraction)
+    idx = torch.linspace(0, n_views - 1, views).round().long()
+    thetas = torch.linspace(0, 2 * torch.pi, n_views)[idx]
     mk = (lambda p: ConeRectGeom(det, pos=p, fov=(45, 45))) if kind.startswith('rect') else \
         (lambda p: ConeCircGeom(shape=det, pos=p, fov=(0, 45)))
-    geom = sum(mk((5 * torch.cos(t), 5 * torch.sin(t), 1)) for t in thetas)
+    return grid, sum(mk((5 * torch.cos(t), 5 * torch.sin(t), 1)) for t in thetas)
+
+
+def cpu_baseline(cfg, sample_views, reps):
+    """Reference forward (torch CPU on the reference's padded trace) on a bounded sample."""
+    from oracle import ref_forward
+    from sph_raytracer_amd.raytracer import find_starts
+    shape, n_views, det, kind, dtype, _ = cfg
+    grid, geom = _cpu_sample(cfg, sample_views)
+    views = geom.rays.shape[0] if geom.rays.dim() == 4 else 1
     xs, rays = geom.ray_starts, geom.rays
     starts = find_starts(grid, xs)
     t0 = time.perf_counter()
@@ -149,6 +190,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sample-views', type=int, default=10)
     ap.add_argument('--cpu-reps', type=int, default=10)
+    ap.add_argument('--cpu-cold-views', type=int, default=None,
+                    help='views of the cold CPU sample (default: 10, C3: 2)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -357,6 +400,13 @@ def main():
             rec['cpu_baseline'] = cpu_baseline(cfg, args.cpu_sample_views, args.cpu_reps)
         except Exception as exc:   # the baseline is informative; never fail the GPU bench on it
             rec['cpu_baseline'] = {'value': None, 'error': repr(exc)}
+        try:
+            cold_views = args.cpu_cold_views or (2 if args.config == 'c3' else 10)
+            cold = cpu_cold_baseline(cfg, cold_views)
+            cold['gpu_ratio'] = rec['cold']['operator_rays_per_s'] / cold['value']
+            rec['cpu_baseline']['cold'] = cold
+        except Exception as exc:
+            rec['cpu_baseline']['cold'] = {'value': None, 'error': repr(exc)}
     else:
         rec['cpu_baseline'] = None
     if rank == 0:
