@@ -816,10 +816,8 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
 // its hit list, traced by trace_kernel afterwards).  Either way the later kernel rewrites the
 // ray's count and segments.  Segments are written straight to the ray's row (FILL / EMIT).
 template <int MODE, typename T>
-__global__ __launch_bounds__(256) void walk_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx >= (int64_t)*o.n_walk) return;
-    const int64_t ray = o.walk_rays[idx];
+__device__ __forceinline__ void walk_one(const GridDev& G, const RaysDev& R, const TraceOut<T>& o,
+                                         const int64_t ray) {
     double x[3], d[3];
     int s[3];
     load_ray(R, ray, x, d, s);
@@ -859,6 +857,15 @@ __global__ __launch_bounds__(256) void walk_kernel(GridDev G, RaysDev R, TraceOu
     if (MODE == MODE_COUNT) o.counts[ray] = (int32_t)nseg;
     if (MODE == MODE_EMIT) (void)emit_slot(o, ray, nseg, true);
     if (MODE == MODE_INTEGRATE) o.out[ray] = (T)acc;   // (one channel: n_chan 1 or time slices)
+}
+
+template <int MODE, typename T>
+__global__ __launch_bounds__(256) void walk_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
+    const int64_t n_walk = (int64_t)*o.n_walk;
+    // lane per ray, grid-stride: neighbouring lanes take neighbouring rays of the list
+    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n_walk;
+         idx += (int64_t)gridDim.x * 256)
+        walk_one<MODE, T>(G, R, o, o.walk_rays[idx]);
 }
 
 // Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
@@ -1411,8 +1418,9 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     if (!(steps & kTrace)) return 0;
     if constexpr (MODE != MODE_BOUND) {
         // the walk first: its out-of-order rays join the list trace's hit list
-        hipLaunchKernelGGL((walk_kernel<MODE, T>), dim3((unsigned)((R.n + 255) / 256)), dim3(256),
-                           0, st, G, R, o);
+        const int64_t wb = (R.n + 255) / 256;
+        hipLaunchKernelGGL((walk_kernel<MODE, T>), dim3((unsigned)(wb < 2048 ? wb : 2048)),
+                           dim3(256), 0, st, G, R, o);
         if (int e = check_launch("walk_kernel")) return e;
     }
     // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...

@@ -7,10 +7,10 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/round
 mkdir -p $OUT
-TAG=${1:-r02}
+TAG=${1:-r03}
 STEPS=${STEPS:-tests,pmc,bench,prof,configs,apply,retrieval}
 if [[ $STEPS == *tests* ]]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
   tail -3 $OUT/gpu_tests.log
 fi
 if [[ $STEPS == *pmc* ]]; then
@@ -35,7 +35,8 @@ if [[ $STEPS == *prof* ]]; then
 fi
 if [[ $STEPS == *configs* ]]; then
   for c in c3 c4 c5; do
-    timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 --cpu-sample-views 1 --cpu-reps 3 > $OUT/bench_$c.json 2> $OUT/bench_$c.err
+    v=10; [ $c = c3 ] && v=4
+    timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 --cpu-sample-views $v --cpu-reps 3 > $OUT/bench_$c.json 2> $OUT/bench_$c.err
     cut -c1-200 $OUT/bench_$c.json
   done
 fi
