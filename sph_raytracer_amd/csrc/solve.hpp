@@ -143,6 +143,16 @@ __device__ __forceinline__ bool cone_may_cross(const GridDev& G, const RayGeo& g
     const bool parallel = __builtin_fabs(aa) < th && !(__builtin_fabs(bb) < th);
     return delta >= 0.0 || parallel;
 }
+// The distance part of cone_root: +inf for a root on the opposite (shadow) nappe or NaN.
+__device__ __forceinline__ double cone_root_t(const GridDev& G, const RayGeo& g, int j, double t) {
+    const double p2 = g.w2 * t + g.x2;
+    const uint8_t f = G.e_flags()[j];
+    const bool cone_up = (f & 1) != 0;
+    const bool exempt = (f & 2) != 0;
+    if (((p2 >= 0.0) != cone_up) && !exempt) t = kInf;   // opposite (shadow) nappe
+    if (__builtin_isnan(t)) t = kInf;
+    return t;
+}
 // Distance/region fix-up of one root t of cone j (region -2 = glancing, keep current region).
 __device__ __forceinline__ void cone_root(const GridDev& G, const RayGeo& g, int j,
                                           double& t, int& reg, int& neg) {
@@ -157,18 +167,14 @@ __device__ __forceinline__ void cone_root(const GridDev& G, const RayGeo& g, int
     neg = prod > 0.0 ? 1 : 0;
     int r = j - neg;
     if (__builtin_fabs(prod) < G.close_tol) r = -2;
-    uint8_t f = G.e_flags()[j];
-    bool cone_up = (f & 1) != 0;
-    bool exempt = (f & 2) != 0;
-    if (((p2 >= 0.0) != cone_up) && !exempt) t = kInf;   // opposite (shadow) nappe
     if (r == G.ne) r = -1;
-    if (__builtin_isnan(t)) t = kInf;
+    t = cone_root_t(G, g, j, t);
     reg = r;
 }
-// Both roots of cone j: slot j ("t1") and slot nbe + j ("t2").
-__device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeo& g, int j,
-                                           double& ta, int& rega, double& tb, int& regb,
-                                           int& nega, int& negb) {
+// The two roots of cone j's quadratic with the reference's snapping and overrides, before the
+// per-root fix-up (slot j "t1", slot nbe + j "t2").
+__device__ __forceinline__ void cone_quadratic(const GridDev& G, const RayGeo& g, int j,
+                                               double& t1, double& t2) {
     const double th = G.close_tol;
     double c2 = G.c2_e()[j];
     double aa = g.w2 * g.w2 - c2;
@@ -178,8 +184,8 @@ __device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeo& g, in
     double delta = bb * bb - (4.0 * aa) * cc;
     if (__builtin_fabs(delta) < th) delta = 0.0;
     double q = __builtin_sqrt(delta);
-    double t1 = (-bb + q) / (2.0 * aa);
-    double t2 = (-bb - q) / (2.0 * aa);
+    t1 = (-bb + q) / (2.0 * aa);
+    t2 = (-bb - q) / (2.0 * aa);
     if (__builtin_fabs(aa) < th && !(__builtin_fabs(bb) < th)) {  // ray parallel to a generator
         t1 = (-cc) / bb;
         t2 = kInf;
@@ -188,6 +194,13 @@ __device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeo& g, in
         t1 = kInf;
         t2 = kInf;
     }
+}
+// Both roots of cone j: slot j ("t1") and slot nbe + j ("t2").
+__device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeo& g, int j,
+                                           double& ta, int& rega, double& tb, int& regb,
+                                           int& nega, int& negb) {
+    double t1, t2;
+    cone_quadratic(G, g, j, t1, t2);
     cone_root(G, g, j, t1, rega, nega);
     cone_root(G, g, j, t2, regb, negb);
     ta = t1;

@@ -860,12 +860,22 @@ __device__ __forceinline__ void walk_one(const GridDev& G, const RaysDev& R, con
 }
 
 template <int MODE, typename T>
-__global__ __launch_bounds__(256) void walk_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
+__global__ __launch_bounds__(256) void walk_kernel(GridDev G, RaysDev R, TraceOut<T> o,
+                                                   int tab_words) {
+    // The boundary tables in LDS: every step of a lane's walk looks one up at its own index (a
+    // serial chain of lookups per lane, unlike the list trace's 64 boundaries per load), so
+    // they must not cost a global-memory round trip each.
+    extern __shared__ double wtab[];
     const int64_t n_walk = (int64_t)*o.n_walk;
-    // lane per ray, grid-stride: neighbouring lanes take neighbouring rays of the list
-    for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n_walk;
-         idx += (int64_t)gridDim.x * 256)
-        walk_one<MODE, T>(G, R, o, o.walk_rays[idx]);
+    if ((int64_t)blockIdx.x * 256 >= n_walk) return;
+    for (int i = threadIdx.x; i < tab_words; i += 256) wtab[i] = G.r_b[i];
+    __syncthreads();
+    GridDev Gs = G;
+    Gs.r_b = wtab;
+    // one ray per lane, neighbouring lanes on neighbouring rays of the list (a grid-stride loop
+    // here costs ~50 VGPRs: 2 instead of 3 waves per SIMD)
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx < n_walk) walk_one<MODE, T>(Gs, R, o, o.walk_rays[idx]);
 }
 
 // Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
@@ -1367,10 +1377,24 @@ static size_t workspace_bytes(const GridDev& G, int64_t n) {
            walk_bytes(n) + exact_scratch_bytes(G);
 }
 
-// SPHRT_WALK=0 keeps every hit ray on the list trace (A/B studies, tests; read at every launch).
+// The walk's boundary tables (sphrt_plan_pack_tables' block: doubles, then the cone flags) in
+// 8-byte words, staged in LDS per workgroup; grids whose tables exceed kWalkTabMax keep the list
+// trace.
+constexpr size_t kWalkTabMax = 32 * 1024;
+static int walk_tab_words(const GridDev& G) {
+    const size_t bytes = ((size_t)G.nbr + 2 * (size_t)G.nbe + 3 * (size_t)G.nba) * 8 + G.nbe;
+    return (int)((bytes + 7) / 8);
+}
+
+// The walk is opt-in (SPHRT_WALK=1, read at every launch): measured on MI355X it is slower than
+// the list trace on every BASELINE config (count pass, us, list / walk: C2 174 / 430, C4 511 /
+// 610, C5 766 / 896, C3 4475 / 5027) — one ray per lane serialises every solve of
+// a ray behind FP64 latency, and lanes advancing different families diverge, where the list
+// trace solves 64 boundaries per instruction.  It stays as a tested alternative (bitwise the
+// list trace's CSR: test_walk_equals_list_trace*, tests/test_walk_host.py).
 static bool walk_enabled() {
     const char* e = getenv("SPHRT_WALK");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }
 
 // Which launches of a trace a call makes: screen (hit list; counts/zeros/bounds of the misses)
@@ -1402,7 +1426,8 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     o.n_walk = (unsigned*)(ws + 128);
     o.walk_rays = (int32_t*)((unsigned char*)o.hits + hits_bytes(R.n));
     // the walk integrates one channel per ray (a register accumulator)
-    o.walk = walk_enabled() && (MODE != MODE_INTEGRATE || o.n_chan == 1 || o.ray_chan_div > 0);
+    o.walk = walk_enabled() && (MODE != MODE_INTEGRATE || o.n_chan == 1 || o.ray_chan_div > 0) &&
+             (size_t)walk_tab_words(G) * 8 <= kWalkTabMax;
     Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
     if constexpr (MODE == MODE_BOUND) steps = kScreen;
     if constexpr (MODE == MODE_EMIT) steps = kTrace;
@@ -1418,9 +1443,10 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     if (!(steps & kTrace)) return 0;
     if constexpr (MODE != MODE_BOUND) {
         // the walk first: its out-of-order rays join the list trace's hit list
-        const int64_t wb = (R.n + 255) / 256;
-        hipLaunchKernelGGL((walk_kernel<MODE, T>), dim3((unsigned)(wb < 2048 ? wb : 2048)),
-                           dim3(256), 0, st, G, R, o);
+        // (sized for every ray: the walk list's length is on the device; blocks past it exit)
+        const int tab_words = walk_tab_words(G);
+        hipLaunchKernelGGL((walk_kernel<MODE, T>), dim3((unsigned)((R.n + 255) / 256)), dim3(256),
+                           (size_t)tab_words * 8, st, G, R, o, tab_words);
         if (int e = check_launch("walk_kernel")) return e;
     }
     // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...

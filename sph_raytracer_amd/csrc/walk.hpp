@@ -1,5 +1,7 @@
 // walk.hpp — the crossings of one ray in increasing distance, one lane per ray, without a list.
 //
+// Opt-in (SPHRT_WALK=1): exact, but slower than the list trace on MI355X (trace.hip
+// walk_enabled).
 // Along a line every boundary family crosses in an order known in advance (SURVEY §7 "merge"):
 //   spheres   the near roots tc - t1c(j) for the outermost shell inwards, then the far roots
 //             tc + t1c(j) outwards (t1c grows with R, and IEEE rounding keeps that order);
@@ -14,8 +16,8 @@
 // one makes the caller hand the ray to the sorting (list) trace instead, so a result is only ever
 // produced from a verified order.  Runs end early only where the geometry rules out further
 // crossings: past the sphere exit, and a plane run at the first half-plane past a crossed one that
-// is not crossed (the azimuth's arc along the line has ended).  The cone runs never end early
-// (see ConeMask).
+// is not crossed (the azimuth's arc along the line has ended).  The cone runs cover index ranges
+// found by solving every cone (see ConeRun).
 #pragma once
 #include "solve.hpp"
 
@@ -98,61 +100,17 @@ __device__ __forceinline__ void sphere_next(const GridDev& G, const RayGeo& g, S
 }
 
 // ---- cones: one stretch of the elevation's monotone pieces ---------------------------------
-// The cones that can give a finite root at all (cone_may_cross: the snapped discriminant is
-// non-negative, or the ray is parallel to a generator) as a bit mask over the cone indices.  Both
-// stretch runs visit every such cone, each keeping the roots on its side of t*: no cone is ever
-// skipped on geometric grounds, because the reference's snapping (|discriminant| < 1e-5 -> 0)
-// gives double roots to cones the line does not reach — on a line near the origin, to nearly all
-// of them (their discriminant is O(dd^2)).  Where such roots break a stretch's order, the order
-// check sends the ray to the list trace.
-constexpr int kWalkConeWords = 4;     // cone masks of up to 256 cones (larger grids: list trace)
-
-struct ConeMask {
-    uint64_t w0, w1, w2, w3;
-};
-
-__device__ __forceinline__ uint64_t mask_word(const ConeMask& m, int w) {
-    return w == 0 ? m.w0 : (w == 1 ? m.w1 : (w == 2 ? m.w2 : m.w3));
-}
-
-__device__ __forceinline__ ConeMask cone_mask(const GridDev& G, const RayGeo& g) {
-    ConeMask m{0, 0, 0, 0};
-    for (int j = 0; j < G.nbe; ++j) {
-        if (!cone_may_cross(G, g, j)) continue;
-        const uint64_t bit = 1ull << (j & 63);
-        const int w = j >> 6;
-        m.w0 |= w == 0 ? bit : 0;
-        m.w1 |= w == 1 ? bit : 0;
-        m.w2 |= w == 2 ? bit : 0;
-        m.w3 |= w == 3 ? bit : 0;
-    }
-    return m;
-}
-
-// First set index >= j (dir > 0) or last <= j (dir < 0); -1 when none.
-__device__ __forceinline__ int mask_next(const ConeMask& m, int j, int dir, int n) {
-    if (j < 0 || j >= n) return -1;
-    if (dir > 0) {
-        for (int w = j >> 6; w < kWalkConeWords; ++w) {
-            uint64_t v = mask_word(m, w);
-            if (w == (j >> 6)) v &= ~0ull << (j & 63);
-            if (v) {
-                const int k = (w << 6) + __builtin_ctzll(v);
-                return k < n ? k : -1;
-            }
-        }
-    } else {
-        for (int w = j >> 6; w >= 0; --w) {
-            uint64_t v = mask_word(m, w);
-            if (w == (j >> 6) && (j & 63) != 63) v &= (2ull << (j & 63)) - 1;
-            if (v) return (w << 6) + 63 - __builtin_clzll(v);
-        }
-    }
-    return -1;
-}
-
+// Every cone is solved up front, all lanes in step, for its roots' distances only
+// (cone_quadratic + cone_root_t: the same operations as cone_solve); each stretch run then covers
+// exactly the index range of the cones with a root on its side of t*, in its direction.  No cone
+// is skipped on geometric grounds — the reference's snapping (|discriminant| < 1e-5 -> 0) gives
+// double roots to cones the line does not reach, on a line near the origin to nearly all of
+// them (their discriminant is O(dd^2)) — and a run ends exactly at its range's last cone instead
+// of searching on, each lane at its own time, through cones that have nothing left for it.
+// Where the snapped roots break a stretch's order, the order check sends the ray to the list
+// trace.
 struct ConeRun {
-    int j, dir;           // next cone to consider, step (+1: angles ascending)
+    int j, dir, end;      // next cone, step (+1: angles ascending), last cone of the range
     int second;           // 0: the stretch [0, split]; 1: (split, inf)
     int done;
     double split;         // t* (+inf: one stretch)
@@ -164,8 +122,8 @@ __device__ __forceinline__ bool cone_in(const ConeRun& c, double t) {
     return __builtin_isfinite(t) && !(t < 0.0) && (c.second ? t > c.split : !(t > c.split));
 }
 
-__device__ __forceinline__ void cone_next(const GridDev& G, const RayGeo& g, const ConeMask& m,
-                                          ConeRun& c, WalkHead& h) {
+__device__ __forceinline__ void cone_next(const GridDev& G, const RayGeo& g, ConeRun& c,
+                                          WalkHead& h) {
     if (c.has_pend) {
         h = c.pend;
         c.has_pend = 0;
@@ -173,16 +131,16 @@ __device__ __forceinline__ void cone_next(const GridDev& G, const RayGeo& g, con
     }
     const int ce0 = 2 * G.nbr;
     while (!c.done) {
-        const int j = mask_next(m, c.j, c.dir, G.nbe);
-        if (j < 0) break;
+        const int j = c.j;
+        if (c.dir > 0 ? j > c.end : j < c.end) break;
+        c.j = j + c.dir;
         double ta, tb;
         int ra, rb, na_, nb_;
         cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
         const bool va = cone_in(c, ta);
         const bool vb = cone_in(c, tb) && !(tb == ta && rb == ra);   // (as the list trace)
-        const WalkHead a{ta, ce0 + j, ra}, b{tb, ce0 + G.nbe + j, rb};
-        c.j = j + c.dir;
         if (!va && !vb) continue;
+        const WalkHead a{ta, ce0 + j, ra}, b{tb, ce0 + G.nbe + j, rb};
         if (va && vb) {
             const bool b_first = head_less(b, a);
             h = b_first ? b : a;
@@ -238,7 +196,7 @@ __device__ __forceinline__ void plane_next(const GridDev& G, const RayGeo& g, Pl
 // strictly ascending (the runs step through them by index).
 __device__ __forceinline__ bool walk_eligible(const GridDev& G, const RayGeo& g, double t1c_outer,
                                               bool start_r_ok) {
-    if (!G.e_asc || !G.a_asc || start_r_ok || G.nbe > 64 * kWalkConeWords) return false;
+    if (!G.e_asc || !G.a_asc || start_r_ok) return false;
     if (!(g.tc - t1c_outer > 0.0)) return false;
     const double sc = __builtin_sqrt(g.nx2);
     const double lz = g.x0 * g.w1 - g.x1 * g.w0;
@@ -246,7 +204,7 @@ __device__ __forceinline__ bool walk_eligible(const GridDev& G, const RayGeo& g,
 }
 
 // The four runs of a walk-eligible ray.  Sphere and plane runs start at their first possible
-// crossing; the cone runs sweep every cone index in their stretch's direction.
+// crossing; the cone runs cover the index range of their stretch's cones.
 __device__ __forceinline__ void walk_setup(const GridDev& G, const RayGeo& g, SphereRun& s,
                                            ConeRun& c1, ConeRun& c2, PlaneRun& p) {
     s.j = G.nbr - 1;
@@ -262,15 +220,37 @@ __device__ __forceinline__ void walk_setup(const GridDev& G, const RayGeo& g, Sp
     const int dir1 = sgn > 0.0 ? -1 : 1;
     c1 = ConeRun{};
     c1.dir = dir1;
-    c1.j = dir1 > 0 ? 0 : G.nbe - 1;
     c1.second = 0;
     c1.split = ts;
     c2 = ConeRun{};
     c2.dir = -dir1;
-    c2.j = -dir1 > 0 ? 0 : G.nbe - 1;
     c2.second = 1;
     c2.split = ts;
-    c2.done = ts < kInf ? 0 : 1;
+    // the index range of each stretch's cones (distances only, every lane in step)
+    int lo1 = G.nbe, hi1 = -1, lo2 = G.nbe, hi2 = -1;
+    for (int j = 0; j < G.nbe; ++j) {
+        if (!cone_may_cross(G, g, j)) continue;
+        double t1, t2;
+        cone_quadratic(G, g, j, t1, t2);
+        t1 = cone_root_t(G, g, j, t1);
+        t2 = cone_root_t(G, g, j, t2);
+        const bool in1 = cone_in(c1, t1) || cone_in(c1, t2);
+        const bool in2 = cone_in(c2, t1) || cone_in(c2, t2);
+        if (in1) {
+            lo1 = j < lo1 ? j : lo1;
+            hi1 = j;
+        }
+        if (in2) {
+            lo2 = j < lo2 ? j : lo2;
+            hi2 = j;
+        }
+    }
+    c1.j = dir1 > 0 ? lo1 : hi1;
+    c1.end = dir1 > 0 ? hi1 : lo1;
+    c1.done = lo1 > hi1;
+    c2.j = dir1 > 0 ? hi2 : lo2;
+    c2.end = dir1 > 0 ? lo2 : hi2;
+    c2.done = lo2 > hi2;
     // azimuth: increasing when L_z > 0; the start's azimuth brought into the table's range
     const double lz = g.x0 * g.w1 - g.x1 * g.w0;
     const double* ab = G.a_b();
@@ -316,11 +296,10 @@ __device__ __forceinline__ int walk_ray(const GridDev& G, const RayGeo& g, const
     ConeRun c1, c2;
     PlaneRun pr;
     walk_setup(G, g, sr, c1, c2, pr);
-    const ConeMask cm = cone_mask(G, g);
     WalkHead hs, h1, h2, hp, hq;            // run heads (named: no indexed array in scratch)
     sphere_next(G, g, sr, hs);
-    cone_next(G, g, cm, c1, h1);
-    cone_next(G, g, cm, c2, h2);
+    cone_next(G, g, c1, h1);
+    cone_next(G, g, c2, h2);
     // the plane run through a two-entry window: the table's first and last half-planes of a full
     // circle (-pi and pi, or 0 and 2 pi) are one plane whose two crossings differ in the last
     // bits either way; the window yields the nearer first
@@ -348,8 +327,21 @@ __device__ __forceinline__ int walk_ray(const GridDev& G, const RayGeo& g, const
         if (!(e.t <= t_hi + margin)) break;
         double tn;
         if (f == 0) { sphere_next(G, g, sr, hs); tn = hs.t; }
-        else if (f == 1) { cone_next(G, g, cm, c1, h1); tn = h1.t; }
-        else if (f == 2) { cone_next(G, g, cm, c2, h2); tn = h2.t; }
+#ifdef SPHRT_WALK_CONE_SHARED
+        else if (f != 3) {
+            // (A/B variant) both stretches through one call: lanes advancing different stretches
+            // share the cone code instead of running it twice under divergence (220 VGPRs)
+            ConeRun c = f == 1 ? c1 : c2;
+            WalkHead hh;
+            cone_next(G, g, c, hh);
+            if (f == 1) { c1 = c; h1 = hh; }
+            else { c2 = c; h2 = hh; }
+            tn = hh.t;
+        }
+#else
+        else if (f == 1) { cone_next(G, g, c1, h1); tn = h1.t; }
+        else if (f == 2) { cone_next(G, g, c2, h2); tn = h2.t; }
+#endif
         else {
             hp = hq;
             plane_next(G, g, pr, hq);

@@ -278,8 +278,13 @@ def _trace_order(geom, rays):
     -> 43.5 us (ConeRect rows are already compact: strips beat every tiling measured).  Only the order of the CSR's rows changes: every
     row reports its geometry ray (sphrt_csr_index ray_ids), outputs stay in geometry order.
     SPHRT_RAY_ORDER=natural keeps the geometry order."""
-    if os.environ.get('SPHRT_RAY_ORDER', 'auto') == 'natural':
+    mode = os.environ.get('SPHRT_RAY_ORDER', 'auto')
+    if mode == 'natural':
         return None
+    shape = tuple(rays.shape[:-1])
+    if mode.startswith('tile:') and len(shape) in (2, 3):     # A/B studies: detector tiles
+        th, tw = (int(v) for v in mode[5:].split(','))
+        return _tile_order(shape[-2], shape[-1], th, tw)
     from .geometry import ConeCircGeom
     geoms = getattr(geom, 'geoms', [geom])
     if not geoms or any(type(g) is not ConeCircGeom for g in geoms):
@@ -288,6 +293,15 @@ def _trace_order(geom, rays):
     if len(shape) not in (2, 3) or shape[-1] <= _WEDGE:
         return None
     return _wedge_order(shape[-2], shape[-1])
+
+
+@functools.lru_cache(maxsize=16)
+def _tile_order(h, w, th, tw):
+    """Pixel order of an (h, w) detector in row-major tiles of th x tw pixels (studies only)."""
+    r = tr.arange(h).repeat_interleave(w)
+    a = tr.arange(w).repeat(h)
+    key = (((r // th) * (-(-w // tw)) + a // tw) * th + r % th) * tw + a % tw
+    return tr.argsort(key)
 
 
 @functools.lru_cache(maxsize=16)
