@@ -277,6 +277,11 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar, 
     return best, f(best), losses
 
 
+def _number(v):
+    """A plain Python scalar hyper-parameter (torch's defaults mix ints and floats: weight_decay=0)."""
+    return isinstance(v, (int, float)) and not isinstance(v, bool)
+
+
 def _split_adam(opt, coeffs):
     """torch.optim.Adam's step on `coeffs` as one csrc/loss.hip launch, or None.
 
@@ -297,8 +302,8 @@ def _split_adam(opt, coeffs):
     grp = opt.param_groups[0]
     if not (not grp.get('amsgrad') and not grp.get('maximize') and not grp.get('capturable')
             and not grp.get('differentiable') and not grp.get('decoupled_weight_decay')
-            and all(isinstance(grp[k], float) for k in ('lr', 'eps', 'weight_decay'))
-            and all(isinstance(b, float) for b in grp['betas'])
+            and all(_number(grp[k]) for k in ('lr', 'eps', 'weight_decay'))
+            and all(_number(b) for b in grp['betas'])
             and len(grp['params']) == 1 and grp['params'][0] is coeffs):
         return None
     fused, foreach = grp.get('fused'), grp.get('foreach')
@@ -310,8 +315,8 @@ def _split_adam(opt, coeffs):
     lib = _lib.load()
     flat = coeffs.detach().view(-1)
     m, v = t.zeros_like(flat), t.zeros_like(flat)
-    b1, b2 = grp['betas']
-    lr, eps, wd = grp['lr'], grp['eps'], grp['weight_decay']
+    b1, b2 = (float(b) for b in grp['betas'])
+    lr, eps, wd = (float(grp[k]) for k in ('lr', 'eps', 'weight_decay'))
     count = [0]
 
     def step(g, c_neg, part, stream, stage_of=None):

@@ -492,3 +492,16 @@ def test_ctypes_structs_match_the_c_header(tmp_path):
         assert got[(cname, 'sizeof')] == ctypes.sizeof(py), cname
         for f in py._fields_:
             assert got[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])
+
+
+def test_split_adam_accepts_torch_defaults():
+    """retrieval._split_adam takes torch.optim.Adam's own defaults (weight_decay=0 is an int) and
+    resolves the implementation torch would pick: fused for fused=True, foreach for a default
+    Adam on a GPU tensor (here: a CPU tensor, so the single-tensor path: no split step)."""
+    import torch
+    from sph_raytracer_amd import retrieval
+    c = torch.zeros(4, dtype=torch.float64, requires_grad=True)
+    opt = torch.optim.Adam([c], lr=0.1)
+    assert opt.param_groups[0]['weight_decay'] == 0 and retrieval._number(0)
+    assert retrieval._split_adam(opt, c) is None          # CPU tensor: torch's single-tensor Adam
+    assert not retrieval._number(True) and not retrieval._number(torch.tensor(0.1))
