@@ -285,6 +285,8 @@ def _trace_order(geom, rays):
     if mode.startswith('tile:') and len(shape) in (2, 3):     # A/B studies: detector tiles
         th, tw = (int(v) for v in mode[5:].split(','))
         return _tile_order(shape[-2], shape[-1], th, tw)
+    if mode.startswith('views:') and len(shape) == 3:          # A/B studies: rows of G views
+        return _view_row_order(shape[0], shape[1], shape[2], int(mode[6:]))
     from .geometry import ConeCircGeom
     geoms = getattr(geom, 'geoms', [geom])
     if not geoms or any(type(g) is not ConeCircGeom for g in geoms):
@@ -293,6 +295,18 @@ def _trace_order(geom, rays):
     if len(shape) not in (2, 3) or shape[-1] <= _WEDGE:
         return None
     return _wedge_order(shape[-2], shape[-1])
+
+
+@functools.lru_cache(maxsize=16)
+def _view_row_order(v, h, w, g):
+    """Order of all (v, h, w) pixels: groups of g consecutive views, inside a group row by row
+    and, inside a row, view by view (studies only: adjacent orbit views cross nearly the same
+    voxels along a row, so a group's rows reuse each other's density lines)."""
+    vi = tr.arange(v).repeat_interleave(h * w)
+    r = tr.arange(h).repeat_interleave(w).repeat(v)
+    c = tr.arange(w).repeat(v * h)
+    key = (((vi // g) * h + r) * g + vi % g) * w + c
+    return tr.argsort(key)
 
 
 @functools.lru_cache(maxsize=16)
@@ -768,10 +782,19 @@ class Operator:
         rays = cone.launch(dev, stg) if cone is not None else self.geom.rays
         perm = _trace_order(self.geom, rays)
         ray_id = None
-        if perm is not None:           # trace in wedges; rows report their geometry ray
+        xs_d, st_d = stg.get(s_xs, xs_h), stg.get(s_st, st_h)
+        if perm is not None and perm.numel() == math.prod(rays.shape[:-1]) and rays.dim() == 4:
+            # an order across views (studies): starts and start voxels follow their rays
+            pd = perm.to(dev, non_blocking=True)
+            full = tuple(rays.shape[:-1])
+            rays = rays.reshape(-1, 3).index_select(0, pd).reshape(rays.shape)
+            xs_d = xs_d.expand(full + (3,)).reshape(-1, 3).index_select(0, pd).reshape(full + (3,))
+            st_d = st_d.expand(full + (4,)).reshape(-1, 4).index_select(0, pd).reshape(full + (4,))
+            xs_h = xs_d
+            ray_id = pd.to(tr.int32)
+        elif perm is not None:         # trace in wedges; rows report their geometry ray
             rays, ray_id = _permute_rays(rays, perm.to(dev, non_blocking=True))
-        batch = _RayBatch(self.grid, xs_h, rays, dev,
-                          staged=(stg.get(s_xs, xs_h), stg.get(s_st, st_h)))
+        batch = _RayBatch(self.grid, xs_h, rays, dev, staged=(xs_d, st_d))
         self._ray_shape = batch.shape
         n = batch.n
         stream = _lib.stream_of(dev)
