@@ -1441,7 +1441,7 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     }
     if constexpr (MODE == MODE_BOUND) return 0;
     if (!(steps & kTrace)) return 0;
-    if constexpr (MODE != MODE_BOUND) {
+    if (MODE != MODE_BOUND && o.walk) {
         // the walk first: its out-of-order rays join the list trace's hit list
         // (sized for every ray: the walk list's length is on the device; blocks past it exit)
         const int tab_words = walk_tab_words(G);

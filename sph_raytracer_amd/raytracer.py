@@ -659,17 +659,16 @@ def _trace_csr(lib, plan, batch, dev, stream):
             total, n_over = tr.stack((row_ptr[n], over[0])).tolist()   # host sync 2
             if n_over == 0:
                 del tws, counts, over
-                # vox, then lengths, each staging array freed after its move: peak = staging
-                # + 12 B per segment (the caching allocator reuses svox's block for seg_len)
+                # voxels and lengths in one pass (one row search per segment for both): peak =
+                # staging + 12 B per segment.  (Two passes, freeing the voxel staging in between,
+                # peaked 4 B per staging slot lower and cost C3 2 x 457 us.)
                 vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
-                _lib.check(lib.sphrt_trace_compact(n, _lib.ptr(bound_ptr), _lib.ptr(svox), None,
-                                                   _lib.ptr(row_ptr), _lib.ptr(vox), None,
-                                                   stream), 'sphrt_trace_compact')
-                del svox
                 seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
-                _lib.check(lib.sphrt_trace_compact(n, _lib.ptr(bound_ptr), None, _lib.ptr(slen),
-                                                   _lib.ptr(row_ptr), None, _lib.ptr(seg_len),
-                                                   stream), 'sphrt_trace_compact')
+                _lib.check(lib.sphrt_trace_compact(n, _lib.ptr(bound_ptr), _lib.ptr(svox),
+                                                   _lib.ptr(slen), _lib.ptr(row_ptr),
+                                                   _lib.ptr(vox), _lib.ptr(seg_len), stream),
+                           'sphrt_trace_compact')
+                del svox, slen
                 return row_ptr, vox, seg_len, total
             del svox, slen
             return (row_ptr,) + fill(total) + (total,)
