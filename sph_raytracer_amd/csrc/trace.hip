@@ -96,11 +96,6 @@ __device__ __forceinline__ int scan_last(int v, int /*lane*/) {
     return wave_scan(v, kNone, [](int a, int b) { return b != kNone ? b : a; });
 }
 
-// ---- sorting of (key = distance bits, pay = candidate<<16 | region+2) pairs ---------------
-__device__ __forceinline__ bool pair_less(uint64_t ka, uint32_t pa, uint64_t kb, uint32_t pb) {
-    return ka < kb || (ka == kb && pa < pb);
-}
-
 // ---- lane exchanges without the LDS crossbar ------------------------------------------------
 // xlane<X>(x): the value x holds in lane (lane ^ X), X a compile-time constant: DPP quad
 // permutes and row (half-)mirrors inside 16 lanes, row shifts for xor 4 / 8, a swizzle for
@@ -135,15 +130,16 @@ __device__ __forceinline__ uint64_t xlane64(uint64_t x, int lane) {
     return (uint64_t)xlane<X>((uint32_t)x, lane) | ((uint64_t)xlane<X>((uint32_t)(x >> 32), lane) << 32);
 }
 
-// One compare-exchange layer of the ascending-only ("flip") bitonic network over 64*M elements,
+// One compare-exchange layer of the ascending-only ("flip") bitonic network over 64*M keys,
 // lane-major: element e = lane*M + i, partner e ^ MASK.  Bits of MASK below M pair registers of
 // the same lane (no lane exchange: the 1-, 2-... layers, which every stage ends with); the rest
 // is a lane xor.  (The register-major order e = i*64 + lane exchanged lanes in all but the top
-// layers: 33 of 36 layers at M = 4 against 21 now.)
+// layers: 33 of 36 layers at M = 4 against 21 now.)  The keys are single 64-bit words (the
+// composite keys below): one compare and two selects per element and layer.
 template <int M>
 constexpr int kLogM = M == 1 ? 0 : M == 2 ? 1 : M == 4 ? 2 : 3;
 template <int M, int MASK>
-__device__ __forceinline__ void cas_layer(uint64_t (&k)[M], uint32_t (&p)[M], int lane) {
+__device__ __forceinline__ void cas_layer(uint64_t (&k)[M], int lane) {
     constexpr int IM = MASK & (M - 1);          // register-index xor
     constexpr int LM = MASK >> kLogM<M>;        // lane xor
     if constexpr (LM == 0) {
@@ -151,80 +147,116 @@ __device__ __forceinline__ void cas_layer(uint64_t (&k)[M], uint32_t (&p)[M], in
         for (int i = 0; i < M; ++i) {
             const int pi = i ^ IM;
             if (pi < i) continue;                   // each in-lane pair once: lower keeps the min
-            // (key, payload) pairs are distinct except the identical padding entries
-            const bool sw = pair_less(k[pi], p[pi], k[i], p[i]);
             const uint64_t ka = k[i], kb = k[pi];
-            const uint32_t pa = p[i], pb = p[pi];
+            const bool sw = kb < ka;
             k[i] = sw ? kb : ka;
-            p[i] = sw ? pb : pa;
             k[pi] = sw ? ka : kb;
-            p[pi] = sw ? pa : pb;
         }
     } else {
         uint64_t nk[M];
-        uint32_t np[M];
 #pragma unroll
         for (int i = 0; i < M; ++i) {
             const int pi = i ^ IM;
             const uint64_t ok = xlane64<LM>(k[pi], lane);
-            const uint32_t op = xlane<LM>(p[pi], lane);
             const int e = lane * M + i;
             const int pe = (lane ^ LM) * M + pi;
-            // "mine < other" is !(other < mine): one comparison per element
-            const bool lt = pair_less(ok, op, k[i], p[i]);
+            // keys are distinct except the identical padding entries
+            const bool lt = ok < k[i];
             const bool take = (e < pe) ? lt : !lt;
             nk[i] = take ? ok : k[i];
-            np[i] = take ? op : p[i];
         }
 #pragma unroll
-        for (int i = 0; i < M; ++i) {
-            k[i] = nk[i];
-            p[i] = np[i];
-        }
+        for (int i = 0; i < M; ++i) k[i] = nk[i];
     }
 }
 
 // half-cleaner layers J, J/2, ..., 1 and the stages KK, 2KK, ... P of the network
 template <int M, int J>
-__device__ __forceinline__ void half_cleaners(uint64_t (&k)[M], uint32_t (&p)[M], int lane) {
+__device__ __forceinline__ void half_cleaners(uint64_t (&k)[M], int lane) {
     if constexpr (J > 0) {
-        cas_layer<M, J>(k, p, lane);
-        half_cleaners<M, J / 2>(k, p, lane);
+        cas_layer<M, J>(k, lane);
+        half_cleaners<M, J / 2>(k, lane);
     }
 }
 template <int M, int KK>
-__device__ __forceinline__ void sort_stages(uint64_t (&k)[M], uint32_t (&p)[M], int lane) {
+__device__ __forceinline__ void sort_stages(uint64_t (&k)[M], int lane) {
     if constexpr (KK <= 64 * M) {
-        cas_layer<M, KK - 1>(k, p, lane);   // flip: mirror partner inside the KK-block
-        half_cleaners<M, KK / 4>(k, p, lane);
-        sort_stages<M, KK * 2>(k, p, lane);
+        cas_layer<M, KK - 1>(k, lane);   // flip: mirror partner inside the KK-block
+        half_cleaners<M, KK / 4>(k, lane);
+        sort_stages<M, KK * 2>(k, lane);
     }
 }
 
+// Register sort of a list of F <= 64*M composite keys (see trace_one: the distance's bits with
+// the low `cmask` bits replaced by the candidate index; pays[cand] holds the replaced bits and
+// the region).  Afterwards keys[e] / pays[e] hold the (distance bits, candidate << 16 | region +
+// 2) pairs in composite-key order, the layout the rest of the trace reads.  That order is the
+// (distance, candidate) order unless two different distances agree above the replaced bits —
+// e.g. the coinciding half-planes a = -pi and a = pi of a full circle, a few ulps apart, which
+// ~5 % of the BASELINE rays cross.  The full distances are checked on the way out; true means
+// some adjacent pair is out of order (fix_near_ties repairs it).
 template <int M>
-__device__ void sort_regs(uint64_t* keys, uint32_t* pays, int F, int lane) {
+__device__ bool sort_regs(uint64_t* keys, uint32_t* pays, int F, int lane, uint64_t cmask) {
     uint64_t k[M];
-    uint32_t p[M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
         const int e = lane * M + i;
-        const bool r = e < F;
-        k[i] = r ? keys[e] : ~0ull;
-        p[i] = r ? pays[e] : ~0u;
+        k[i] = e < F ? keys[e] : ~0ull;
     }
-    sort_stages<M, 2>(k, p, lane);
+    sort_stages<M, 2>(k, lane);
+    uint64_t tb[M];
+    uint32_t py[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const uint32_t cand = (uint32_t)(k[i] & cmask);
+        const uint32_t info = lane * M + i < F ? pays[cand] : 0u;
+        tb[i] = (k[i] & ~cmask) | (uint64_t)(info >> 16);
+        py[i] = (cand << 16) | (info & 0xffffu);
+    }
+    bool bad = false;
+#pragma unroll
+    for (int i = 1; i < M; ++i) bad |= lane * M + i < F && tb[i] < tb[i - 1];
+    const uint64_t prev = (uint64_t)__shfl_up((long long)tb[M - 1], 1);
+    bad |= lane > 0 && lane * M < F && tb[0] < prev;
     wave_sync();
 #pragma unroll
     for (int i = 0; i < M; ++i) {
         const int e = lane * M + i;
         if (e < F) {
-            keys[e] = k[i];
-            pays[e] = p[i];
+            keys[e] = tb[i];
+            pays[e] = py[i];
         }
     }
     wave_sync();
+    return __ballot(bad) != 0;
 }
 
+__device__ __forceinline__ bool pair_less(uint64_t ka, uint32_t pa, uint64_t kb, uint32_t pb) {
+    return ka < kb || (ka == kb && pa < pb);
+}
+
+// Odd-even transposition passes over the (distance bits, payload) pairs in LDS until no adjacent
+// pair is out of order: after the composite-key sort only entries whose distances agree above
+// the candidate bits can be, each inside its (contiguous, small) group, so one or two rounds
+// finish it.  The result is the (distance, candidate) order exactly.
+__device__ void fix_near_ties(uint64_t* keys, uint32_t* pays, int F, int lane) {
+    for (;;) {
+        bool swapped = false;
+        for (int par = 0; par < 2; ++par) {
+            for (int i = 2 * lane + par; i + 1 < F; i += 128) {
+                const uint64_t ka = keys[i], kb = keys[i + 1];
+                const uint32_t pa = pays[i], pb = pays[i + 1];
+                if (pair_less(kb, pb, ka, pa)) {
+                    keys[i] = kb; pays[i] = pb;
+                    keys[i + 1] = ka; pays[i + 1] = pa;
+                    swapped = true;
+                }
+            }
+            wave_sync();
+        }
+        if (__ballot(swapped) == 0) return;
+    }
+}
 __device__ __forceinline__ void cas_lds(uint64_t* keys, uint32_t* pays, int i, int l) {
     uint64_t ki = keys[i], kl = keys[l];
     uint32_t pi = pays[i], pl = pays[l];
@@ -233,8 +265,9 @@ __device__ __forceinline__ void cas_lds(uint64_t* keys, uint32_t* pays, int i, i
         keys[l] = ki; pays[l] = pi;
     }
 }
-// Same network in LDS for long lists; virtual +inf padding beyond F never moves (ascending-only
-// comparators), so storage is exactly F entries.
+// The bitonic network in LDS for long lists (F > 512), on (distance bits, payload) pairs: such
+// rays list their crossings a second time in that layout.  Virtual +inf padding beyond F never
+// moves (ascending-only comparators), so storage is exactly F entries.
 __device__ void sort_lds(uint64_t* keys, uint32_t* pays, int F, int lane) {
     int P = 1;
     while (P < F) P <<= 1;
@@ -393,6 +426,14 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
                           const int lane, const TraceOut<T>& o) {
     // ---- 1. crossings -> LDS list (finite, t >= 0), min finite negative distance ----------
     TRACE_T(ts0);
+    // The list holds composite keys: the distance's bits (t >= 0: ordered as unsigned integers)
+    // with the low `cbits` bits replaced by the candidate index, so the sort moves and compares
+    // one 64-bit word per entry; pays[candidate] keeps the replaced bits and the region.  A list
+    // longer than the register sort takes (F > 512) is listed again as (distance bits, payload)
+    // pairs for the LDS network (pair_fmt).
+    const int cbits = 32 - __builtin_clz((unsigned)(G.K - 1));
+    const uint64_t cmask = (1ull << cbits) - 1ull;
+    bool pair_fmt = false;
     int base = 0;
     double tneg = kInf;
     auto note = [&](double t) {
@@ -402,8 +443,14 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         const uint64_t m = __ballot(has);
         if (has) {
             const int pos = base + __popcll(m & lanemask_lt(lane));
-            keys[pos] = (uint64_t)__double_as_longlong(t + 0.0);  // -0 -> +0
-            pays[pos] = ((uint32_t)cand << 16) | (uint32_t)(reg + 2);
+            const uint64_t tb = (uint64_t)__double_as_longlong(t + 0.0);  // -0 -> +0
+            if (pair_fmt) {
+                keys[pos] = tb;
+                pays[pos] = ((uint32_t)cand << 16) | (uint32_t)(reg + 2);
+            } else {
+                keys[pos] = (tb & ~cmask) | (uint64_t)cand;
+                pays[cand] = ((uint32_t)(tb & cmask) << 16) | (uint32_t)(reg + 2);
+            }
         }
         base += __popcll(m);
     };
@@ -419,9 +466,9 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     auto keep = [&](double t) {
         return __builtin_isfinite(t) && !(t < 0.0) && !(t > t_hi) && !(clip_lo && t < t_lo);
     };
-    double pe_t = -1.0, pa_t = -1.0;      // this lane's last e / a update before t_lo
-    int pe_v = 0, pa_v = 0;
-    bool pe_amb = false, pa_amb = false;  // a second update at that distance, another value
+    double pe_t, pa_t;                    // this lane's last e / a update before t_lo
+    int pe_v, pa_v;
+    bool pe_amb, pa_amb;                  // a second update at that distance, another value
     auto pre = [&](bool v, double t, int reg, double& bt, int& bv, bool& amb) {
         if (v && clip_lo && reg != -2 && !(t < 0.0) && t < t_lo) {
             if (t > bt) {
@@ -435,56 +482,68 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     };
 
     const int nbr = G.nbr, nbe = G.nbe, nba = G.nba;
-    // Families of more than 64 boundaries solve only the 64-wide chunks that can list something:
-    // from the first boundary whose solve can give a finite crossing (sphere_may_cross /
-    // cone_may_cross: exact, the skipped solves would yield +inf only), and chunks without such a
-    // boundary are skipped.  (C5: 65 shells / cones, one chunk instead of two; C3: 129, ~2
-    // instead of 3.)  Families of <= 64 boundaries keep the single chunk (no pre-pass).
-    auto sph_ok = [&](int j) { return sphere_may_cross(G, g, j); };
-    auto cone_ok = [&](int j) { return cone_may_cross(G, g, j); };
-    for (int j0 = nbr > 64 ? first_may_cross(nbr, lane, sph_ok) : 0; j0 < nbr; j0 += 64) {
-        const int j = j0 + lane;
-        const bool v = j < nbr;
-        if (nbr > 64 && __ballot(v && sph_ok(j)) == 0) continue;
-        double ti = kInf, to = kInf;
-        int ri = 0, ro = 0, ni, no;
-        if (v) sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
-        note(ti);
-        note(to);
-        push(v && keep(ti), ti, j, ri);
-        // a double root (tangent sphere, the e = pi/2 "cone") writing the same region twice at
-        // the same distance changes nothing in the forward fill: keep one entry, so the group is
-        // no exact tie (the tie analysis below only runs for real ties)
-        push(v && keep(to) && !(to == ti && ro == ri), to, nbr + j, ro);
+    int F;
+    for (;;) {
+        base = 0;
+        tneg = kInf;
+        pe_t = pa_t = -1.0;
+        pe_v = pa_v = 0;
+        pe_amb = pa_amb = false;
+        // Families of more than 64 boundaries solve only the 64-wide chunks that can list
+        // something: from the first boundary whose solve can give a finite crossing
+        // (sphere_may_cross / cone_may_cross: exact, the skipped solves would yield +inf only),
+        // and chunks without such a boundary are skipped.  (C5: 65 shells / cones, one chunk
+        // instead of two; C3: 129, ~2 instead of 3.)  Families of <= 64 boundaries keep the
+        // single chunk (no pre-pass).
+        auto sph_ok = [&](int j) { return sphere_may_cross(G, g, j); };
+        auto cone_ok = [&](int j) { return cone_may_cross(G, g, j); };
+        for (int j0 = nbr > 64 ? first_may_cross(nbr, lane, sph_ok) : 0; j0 < nbr; j0 += 64) {
+            const int j = j0 + lane;
+            const bool v = j < nbr;
+            if (nbr > 64 && __ballot(v && sph_ok(j)) == 0) continue;
+            double ti = kInf, to = kInf;
+            int ri = 0, ro = 0, ni, no;
+            if (v) sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
+            note(ti);
+            note(to);
+            push(v && keep(ti), ti, j, ri);
+            // a double root (tangent sphere, the e = pi/2 "cone") writing the same region twice at
+            // the same distance changes nothing in the forward fill: keep one entry, so the group is
+            // no exact tie (the tie analysis below only runs for real ties)
+            push(v && keep(to) && !(to == ti && ro == ri), to, nbr + j, ro);
+        }
+        const int ce0 = 2 * nbr;
+        for (int j0 = nbe > 64 ? first_may_cross(nbe, lane, cone_ok) : 0; j0 < nbe; j0 += 64) {
+            const int j = j0 + lane;
+            const bool v = j < nbe;
+            if (nbe > 64 && __ballot(v && cone_ok(j)) == 0) continue;
+            double ta = kInf, tb = kInf;
+            int ra = 0, rb = 0, na_, nb_;
+            if (v) cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
+            note(ta);
+            note(tb);
+            pre(v, ta, ra, pe_t, pe_v, pe_amb);
+            pre(v, tb, rb, pe_t, pe_v, pe_amb);
+            push(v && keep(ta), ta, ce0 + j, ra);
+            push(v && keep(tb) && !(tb == ta && rb == ra), tb, ce0 + nbe + j, rb);
+        }
+        const int ca0 = 2 * nbr + 2 * nbe;
+        for (int j0 = 0; j0 < nba; j0 += 64) {
+            const int j = j0 + lane;
+            const bool v = j < nba;
+            double t = kInf;
+            int r = 0, ng;
+            if (v) plane_solve(G, g, j, t, r, ng);
+            note(t);
+            pre(v, t, r, pa_t, pa_v, pa_amb);
+            push(v && keep(t), t, ca0 + j, r);
+        }
+        push(lane == 0 && !clip_lo, 0.0, G.K - 1, 0);  // the start entry (raytracer.py:111-122)
+        F = base;
+        if (pair_fmt || F <= 512) break;
+        pair_fmt = true;
+        wave_sync();
     }
-    const int ce0 = 2 * nbr;
-    for (int j0 = nbe > 64 ? first_may_cross(nbe, lane, cone_ok) : 0; j0 < nbe; j0 += 64) {
-        const int j = j0 + lane;
-        const bool v = j < nbe;
-        if (nbe > 64 && __ballot(v && cone_ok(j)) == 0) continue;
-        double ta = kInf, tb = kInf;
-        int ra = 0, rb = 0, na_, nb_;
-        if (v) cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
-        note(ta);
-        note(tb);
-        pre(v, ta, ra, pe_t, pe_v, pe_amb);
-        pre(v, tb, rb, pe_t, pe_v, pe_amb);
-        push(v && keep(ta), ta, ce0 + j, ra);
-        push(v && keep(tb) && !(tb == ta && rb == ra), tb, ce0 + nbe + j, rb);
-    }
-    const int ca0 = 2 * nbr + 2 * nbe;
-    for (int j0 = 0; j0 < nba; j0 += 64) {
-        const int j = j0 + lane;
-        const bool v = j < nba;
-        double t = kInf;
-        int r = 0, ng;
-        if (v) plane_solve(G, g, j, t, r, ng);
-        note(t);
-        pre(v, t, r, pa_t, pa_v, pa_amb);
-        push(v && keep(t), t, ca0 + j, r);
-    }
-    push(lane == 0 && !clip_lo, 0.0, G.K - 1, 0);  // the start entry (raytracer.py:111-122)
-    const int F = base;
     tneg = wave_min(tneg);
     // rows entering the outer sphere (start outside): the last pre-entry update group per row
     int e_in = se, a_in = sa;
@@ -522,15 +581,13 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
 #endif
     TRACE_T(ts1);
     TRACE_ADD(0, ts0, ts1);
-    if (F <= 64) sort_regs<1>(keys, pays, F, lane);
-    else if (F <= 128) sort_regs<2>(keys, pays, F, lane);
-#if !defined(SPHRT_TRACE_NO_M4)
-    else if (F <= 256) sort_regs<4>(keys, pays, F, lane);
-#endif
-#if !defined(SPHRT_TRACE_NO_M8)
-    else if (F <= 512) sort_regs<8>(keys, pays, F, lane);   // C3: 15 % of hit rays; 5.3 -> 4.5 ms
-#endif
-    else sort_lds(keys, pays, F, lane);
+    bool near_tie = false;
+    if (pair_fmt) sort_lds(keys, pays, F, lane);
+    else if (F <= 64) near_tie = sort_regs<1>(keys, pays, F, lane, cmask);
+    else if (F <= 128) near_tie = sort_regs<2>(keys, pays, F, lane, cmask);
+    else if (F <= 256) near_tie = sort_regs<4>(keys, pays, F, lane, cmask);
+    else near_tie = sort_regs<8>(keys, pays, F, lane, cmask);  // C3: 15 % of hit rays
+    if (near_tie) fix_near_ties(keys, pays, F, lane);
 
 #if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 2
     if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 2

@@ -51,6 +51,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         res[k] = e0.elapsed_time(e1) * 100
+        if k == 'count_us':       # rays sent to the exact path (the workspace's first word)
+            res['deferred'] = int(ws[:8].cpu().view(torch.int64)[0])
     print(json.dumps(res))
 
 
