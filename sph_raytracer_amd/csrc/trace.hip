@@ -187,23 +187,17 @@ __device__ __forceinline__ void sort_stages(uint64_t (&k)[M], int lane) {
     }
 }
 
-// Register sort of a list of F <= 64*M composite keys (see trace_one: the distance's bits with
-// the low `cmask` bits replaced by the candidate index; pays[cand] holds the replaced bits and
-// the region).  Afterwards keys[e] / pays[e] hold the (distance bits, candidate << 16 | region +
-// 2) pairs in composite-key order, the layout the rest of the trace reads.  That order is the
-// (distance, candidate) order unless two different distances agree above the replaced bits —
+// Sorted composite keys k (lane-major, padding ~0 at the end) -> keys[e] / pays[e] hold the
+// (distance bits, candidate << 16 | region + 2) pairs, the layout the rest of the trace reads
+// (pays[cand] holds the replaced low bits and the region until then).  Composite-key order is
+// the (distance, candidate) order unless two different distances agree above the replaced bits —
 // e.g. the coinciding half-planes a = -pi and a = pi of a full circle, a few ulps apart, which
-// ~5 % of the BASELINE rays cross.  The full distances are checked on the way out; true means
-// some adjacent pair is out of order (fix_near_ties repairs it).
+// ~5 % of the BASELINE rays cross — or a pre-sorted run held equal distances out of candidate
+// order.  The full distances are checked on the way out; true means some adjacent pair is out of
+// order (fix_near_ties repairs it).
 template <int M>
-__device__ bool sort_regs(uint64_t* keys, uint32_t* pays, int F, int lane, uint64_t cmask) {
-    uint64_t k[M];
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-        const int e = lane * M + i;
-        k[i] = e < F ? keys[e] : ~0ull;
-    }
-    sort_stages<M, 2>(k, lane);
+__device__ __forceinline__ bool finish_sort(const uint64_t (&k)[M], uint64_t* keys,
+                                            uint32_t* pays, int F, int lane, uint64_t cmask) {
     uint64_t tb[M];
     uint32_t py[M];
 #pragma unroll
@@ -229,6 +223,66 @@ __device__ bool sort_regs(uint64_t* keys, uint32_t* pays, int F, int lane, uint6
     }
     wave_sync();
     return __ballot(bad) != 0;
+}
+
+// The list trace_one builds (composite keys, see there): the shells' near crossings at
+// keys[0, Sn) in shell order — descending distances — then the cone / half-plane / start entries
+// up to keys[F - Sf), and the shells' far crossings at keys[cap - 1], keys[cap - 2], ... in shell
+// order — ascending distances.
+//
+// Full sort: the bitonic network over all F <= 64*M entries.
+template <int M>
+__device__ bool sort_regs(uint64_t* keys, uint32_t* pays, int F, int Sf, int cap, int lane,
+                          uint64_t cmask) {
+    uint64_t k[M];
+    const int front = F - Sf;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int e = lane * M + i;
+        k[i] = e < front ? keys[e] : e < F ? keys[cap - 1 - (e - front)] : ~0ull;
+    }
+    sort_stages<M, 2>(k, lane);
+    return finish_sort<M>(k, keys, pays, F, lane, cmask);
+}
+
+// Sort + merge: every operation of a shell crossing's distance is monotone in R^2, so the shell
+// entries read as near ones outermost-first then far ones innermost-first are one ascending run
+// (as composite keys, up to equal distances).  Only the other O entries go through a network
+// (64*M2 >= O, a smaller power of two than the whole list's); with them descending behind the
+// shell run and the padding between, the list is bitonic and one merge stage (log2(64 M)
+// half-cleaner layers) sorts it.  C3 (F ~153, ~88 shell entries): 28 + 8 layers on 2 + 4
+// registers instead of 36 on 4.
+template <int M, int M2>
+__device__ bool merge_sort(uint64_t* keys, uint32_t* pays, int F, int Sn, int Sf, int cap,
+                           int lane, uint64_t cmask) {
+    const int S = Sn + Sf, O = F - S;
+    {
+        uint64_t k[M2];
+#pragma unroll
+        for (int i = 0; i < M2; ++i) {
+            const int e = lane * M2 + i;
+            k[i] = e < O ? keys[Sn + e] : ~0ull;
+        }
+        sort_stages<M2, 2>(k, lane);
+        wave_sync();
+#pragma unroll
+        for (int i = 0; i < M2; ++i) {
+            const int e = lane * M2 + i;
+            if (e < O) keys[Sn + e] = k[i];
+        }
+        wave_sync();
+    }
+    constexpr int P = 64 * M;
+    uint64_t k[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int e = lane * M + i;
+        k[i] = e < Sn ? keys[Sn - 1 - e]
+             : e < S ? keys[cap - 1 - (e - Sn)]
+             : e >= P - O ? keys[Sn + (P - 1 - e)] : ~0ull;
+    }
+    half_cleaners<M, 32 * M>(k, lane);
+    return finish_sort<M>(k, keys, pays, F, lane, cmask);
 }
 
 __device__ __forceinline__ bool pair_less(uint64_t ka, uint32_t pa, uint64_t kb, uint32_t pb) {
@@ -423,7 +477,7 @@ __device__ __forceinline__ int first_may_cross(int n, int lane, Ok ok) {
 template <int MODE, typename T>
 __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const int se,
                           const int sa, const int64_t ray, uint64_t* keys, uint32_t* pays,
-                          const int lane, const TraceOut<T>& o) {
+                          const int cap, const int lane, const TraceOut<T>& o) {
     // ---- 1. crossings -> LDS list (finite, t >= 0), min finite negative distance ----------
     TRACE_T(ts0);
     // The list holds composite keys: the distance's bits (t >= 0: ordered as unsigned integers)
@@ -434,15 +488,19 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     const int cbits = 32 - __builtin_clz((unsigned)(G.K - 1));
     const uint64_t cmask = (1ull << cbits) - 1ull;
     bool pair_fmt = false;
-    int base = 0;
+    int base = 0;       // entries from the front
+    int nfar = 0;       // shells' far crossings, from keys[cap - 1] down (composite layout)
+    int s_near = 0;     // shells' near crossings: keys[0, s_near)
     double tneg = kInf;
     auto note = [&](double t) {
         if (t < 0.0 && __builtin_isfinite(t)) tneg = fmin(tneg, t);
     };
-    auto push = [&](bool has, double t, int cand, int reg) {
+    auto push = [&](bool has, double t, int cand, int reg, bool far = false) {
         const uint64_t m = __ballot(has);
+        far = far && !pair_fmt;
         if (has) {
-            const int pos = base + __popcll(m & lanemask_lt(lane));
+            const int rank = __popcll(m & lanemask_lt(lane));
+            const int pos = far ? cap - 1 - (nfar + rank) : base + rank;
             const uint64_t tb = (uint64_t)__double_as_longlong(t + 0.0);  // -0 -> +0
             if (pair_fmt) {
                 keys[pos] = tb;
@@ -452,7 +510,8 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
                 pays[cand] = ((uint32_t)(tb & cmask) << 16) | (uint32_t)(reg + 2);
             }
         }
-        base += __popcll(m);
+        if (far) nfar += __popcll(m);
+        else base += __popcll(m);
     };
     // Only crossings inside the outer sphere's span [t_lo, t_hi] are listed and sorted: after
     // the exit every segment lies outside (the r row stays -1: no sphere is crossed again), and
@@ -485,6 +544,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     int F;
     for (;;) {
         base = 0;
+        nfar = 0;
         tneg = kInf;
         pe_t = pa_t = -1.0;
         pe_v = pa_v = 0;
@@ -510,8 +570,9 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
             // a double root (tangent sphere, the e = pi/2 "cone") writing the same region twice at
             // the same distance changes nothing in the forward fill: keep one entry, so the group is
             // no exact tie (the tie analysis below only runs for real ties)
-            push(v && keep(to) && !(to == ti && ro == ri), to, nbr + j, ro);
+            push(v && keep(to) && !(to == ti && ro == ri), to, nbr + j, ro, true);
         }
+        s_near = base;
         const int ce0 = 2 * nbr;
         for (int j0 = nbe > 64 ? first_may_cross(nbe, lane, cone_ok) : 0; j0 < nbe; j0 += 64) {
             const int j = j0 + lane;
@@ -539,7 +600,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
             push(v && keep(t), t, ca0 + j, r);
         }
         push(lane == 0 && !clip_lo, 0.0, G.K - 1, 0);  // the start entry (raytracer.py:111-122)
-        F = base;
+        F = base + nfar;
         if (pair_fmt || F <= 512) break;
         pair_fmt = true;
         wave_sync();
@@ -582,11 +643,21 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     TRACE_T(ts1);
     TRACE_ADD(0, ts0, ts1);
     bool near_tie = false;
+    const int n_other = F - s_near - nfar;   // entries outside the shells' sorted run
     if (pair_fmt) sort_lds(keys, pays, F, lane);
-    else if (F <= 64) near_tie = sort_regs<1>(keys, pays, F, lane, cmask);
-    else if (F <= 128) near_tie = sort_regs<2>(keys, pays, F, lane, cmask);
-    else if (F <= 256) near_tie = sort_regs<4>(keys, pays, F, lane, cmask);
-    else near_tie = sort_regs<8>(keys, pays, F, lane, cmask);  // C3: 15 % of hit rays
+    else if (F <= 64) near_tie = sort_regs<1>(keys, pays, F, nfar, cap, lane, cmask);
+    else if (F <= 128) {
+        near_tie = n_other <= 64 ? merge_sort<2, 1>(keys, pays, F, s_near, nfar, cap, lane, cmask)
+                                 : sort_regs<2>(keys, pays, F, nfar, cap, lane, cmask);
+    } else if (F <= 256) {
+        near_tie = n_other <= 64 ? merge_sort<4, 1>(keys, pays, F, s_near, nfar, cap, lane, cmask)
+                 : n_other <= 128 ? merge_sort<4, 2>(keys, pays, F, s_near, nfar, cap, lane, cmask)
+                                  : sort_regs<4>(keys, pays, F, nfar, cap, lane, cmask);
+    } else {                                                  // C3: 15 % of hit rays
+        near_tie = n_other <= 128 ? merge_sort<8, 2>(keys, pays, F, s_near, nfar, cap, lane, cmask)
+                 : n_other <= 256 ? merge_sort<8, 4>(keys, pays, F, s_near, nfar, cap, lane, cmask)
+                                  : sort_regs<8>(keys, pays, F, nfar, cap, lane, cmask);
+    }
     if (near_tie) fix_near_ties(keys, pays, F, lane);
 
 #if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 2
@@ -956,7 +1027,7 @@ __global__ __launch_bounds__(256, SPHRT_TRACE_MIN_BLOCKS) void trace_kernel(Grid
          h += (int64_t)gridDim.x * waves) {
         const HitRay& hr = o.hits[__builtin_amdgcn_readfirstlane((int)h)];   // uniform record
         const RayGeo g = make_ray(hr.x[0], hr.x[1], hr.x[2], hr.d[0], hr.d[1], hr.d[2]);
-        trace_one<MODE, T>(G, g, hr.s[0], hr.s[1], hr.s[2], hr.ray, keys, pays, lane, o);
+        trace_one<MODE, T>(G, g, hr.s[0], hr.s[1], hr.s[2], hr.ray, keys, pays, cap, lane, o);
     }
 }
 

@@ -24,12 +24,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='c2')
     ap.add_argument('--out', required=True)
+    ap.add_argument('--counters', default=None, help='comma-separated SQ counters (one pass)')
+    ap.add_argument('--count-pass', action='store_true',
+                    help='profile tools/trace_time.py (the two-pass COUNT kernel, which the '
+                         'SPHRT_TRACE_ABL ablation builds cut short) instead of trace_bench.py')
     args = ap.parse_args()
+    counters = args.counters.split(',') if args.counters else COUNTERS
     d = os.path.join(ROOT, 'gpurun_out', 'pmc_trace')
     shutil.rmtree(d, ignore_errors=True)
-    subprocess.run(['rocprofv3', '--pmc', *COUNTERS, '--kernel-trace', '-d', d, '-o', 'p',
+    subprocess.run(['rocprofv3', '--pmc', *counters, '--kernel-trace', '-d', d, '-o', 'p',
                     '--output-format', 'csv', '--', sys.executable,
-                    os.path.join(ROOT, 'tools', 'trace_bench.py'), args.config, '--reps', '1'],
+                    *([os.path.join(ROOT, 'tools', 'trace_time.py'), args.config] if args.count_pass
+                      else [os.path.join(ROOT, 'tools', 'trace_bench.py'), args.config, '--reps',
+                            '1'])],
                    check=True, cwd=ROOT, stdout=subprocess.DEVNULL)
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
@@ -43,9 +50,14 @@ def main():
             name = r['Kernel_Name'].split('(')[0].replace('void ', '')
             if 'trace_kernel' in name:
                 dur[name].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) * 1e-9)
-    rec = {'config': args.config, 'counters': COUNTERS, 'kernels': {}}
+    rec = {'config': args.config, 'counters': counters, 'lib': os.environ.get('SPHRT_LIB'),
+           'kernels': {}}
     for k, v in vals.items():
         per = {c: sum(x) / len(x) for c, x in v.items()}
+        t = sorted(dur[k])[len(dur[k]) // 2] if dur[k] else None
+        if counters is not COUNTERS:
+            rec['kernels'][k] = {'per_launch': per, 'median_s': t}
+            continue
         f64_flop = 64 * (2 * per['SQ_INSTS_VALU_FMA_F64'] + per['SQ_INSTS_VALU_MUL_F64'] +
                          per['SQ_INSTS_VALU_ADD_F64'] + per['SQ_INSTS_VALU_TRANS_F64'])
         t = sorted(dur[k])[len(dur[k]) // 2] if dur[k] else None
