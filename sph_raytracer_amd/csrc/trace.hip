@@ -371,6 +371,7 @@ struct TraceOut {
     unsigned* n_walk;                // workspace: walk-eligible hit-ray counter
     int32_t* walk_rays;              // workspace: walk-eligible hit rays (walk_kernel)
     int walk;                        // screen: send eligible rays to the walk (SPHRT_WALK != 0)
+    int wedge;                       // solve only the half-planes of a line's azimuth wedge
 };
 
 // EMIT: ray `ray` has `cnt` segments; its staging slot is [row_ptr[ray], row_ptr[ray + 1]) (the
@@ -541,6 +542,63 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     };
 
     const int nbr = G.nbr, nbe = G.nbe, nba = G.nba;
+    // Half-planes: a line's azimuth turns monotonically, by less than pi, so over [0, t_hi] it
+    // sweeps the wedge from A = x_xy to B = (x + t_hi w)_xy (turning with the sign of L, the z
+    // of x cross w).  A half-plane outside that wedge has no crossing in [0, t_hi] — only one
+    // behind the start or past the exit, or none — so, when the ray has no behind-start segment
+    // (start outside the grid: the negative distances are unused), its solve could neither list
+    // an entry nor be a pre-entry update.  With ascending angles the half-planes inside the
+    // wedge are one cyclic run of indices [p_start, p_start + p_count) (mod nba), and only that
+    // run is solved: 1 chunk of 64 instead of 3 at C3 (129 half-planes, a ~150 degree sweep for
+    // rays through the ball), 1 instead of 2 at C5.  The wedge is widened by 1e-6 rad and lines
+    // passing within 1e-6 of the z axis solve every half-plane: a skipped crossing is then far
+    // (> 1e-13) from [0, t_hi] compared with its rounding, and its back-half test is decided by
+    // |p_xy| >= 1e-6.  Exact: test_plane_wedge_exact (CSR bitwise the same without the wedge).
+    int p_start = 0, p_count = nba;
+    {
+        const bool start_ok =
+            sr >= 0 && sr < G.nr && se >= 0 && se < G.ne && sa >= 0 && sa < G.na;
+        const double Lz = g.x0 * g.w1 - g.x1 * g.w0;
+        if (o.wedge && nba > 64 && G.a_asc && !start_ok && __builtin_isfinite(t_hi) &&
+            Lz * Lz >= 1e-12 * (g.w0 * g.w0 + g.w1 * g.w1)) {
+            const double b0 = g.x0 + t_hi * g.w0, b1 = g.x1 + t_hi * g.w1;
+            const double tol_a = 1e-12 * (g.x0 * g.x0 + g.x1 * g.x1) * (Lz * Lz);
+            const double tol_b = 1e-12 * (b0 * b0 + b1 * b1) * (Lz * Lz);
+            int cnt = 0, n_starts = 0, first = -1;
+            uint64_t m0 = 0;
+            bool prev = false;                      // in(j0 - 1)
+            for (int j0 = 0; j0 < nba; j0 += 64) {
+                const int j = j0 + lane;
+                bool in = false;
+                if (j < nba) {
+                    // turn * cross >= -1e-6 |.|, turn = sign(Lz), squared: no square roots
+                    const double u0 = G.cos_a()[j], u1 = G.sin_a()[j];
+                    const double ca = (g.x0 * u1 - g.x1 * u0) * Lz, cb = (u0 * b1 - u1 * b0) * Lz;
+                    in = (ca >= 0.0 || ca * ca <= tol_a) && (cb >= 0.0 || cb * cb <= tol_b);
+                }
+                const uint64_t m = __ballot(in);
+                uint64_t st = m & ~((m << 1) | (prev ? 1ull : 0ull));
+                if (j0 == 0) {
+                    m0 = m;
+                    st &= ~1ull;                    // index 0: decided by in(nba - 1) below
+                }
+                cnt += __popcll(m);
+                n_starts += __popcll(st);
+                if (st && first < 0) first = j0 + __builtin_ctzll(st);
+                prev = (m >> (min(64, nba - j0) - 1)) & 1ull;
+            }
+            if ((m0 & 1ull) && !prev) {
+                ++n_starts;
+                first = 0;
+            }
+            if (cnt == 0) {
+                p_count = 0;
+            } else if (n_starts == 1) {
+                p_start = first;
+                p_count = cnt;
+            }
+        }
+    }
     int F;
     for (;;) {
         base = 0;
@@ -589,9 +647,10 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
             push(v && keep(tb) && !(tb == ta && rb == ra), tb, ce0 + nbe + j, rb);
         }
         const int ca0 = 2 * nbr + 2 * nbe;
-        for (int j0 = 0; j0 < nba; j0 += 64) {
-            const int j = j0 + lane;
-            const bool v = j < nba;
+        for (int k0 = 0; k0 < p_count; k0 += 64) {
+            const bool v = k0 + lane < p_count;
+            int j = p_start + k0 + lane;
+            if (j >= nba) j -= nba;
             double t = kInf;
             int r = 0, ng;
             if (v) plane_solve(G, g, j, t, r, ng);
@@ -1524,6 +1583,12 @@ static bool walk_enabled() {
     const char* e = getenv("SPHRT_WALK");
     return e && e[0] == '1';
 }
+// The half-plane wedge (trace_one) is on unless SPHRT_TRACE_WEDGE=0 (A/B tests: the CSR is the
+// same bit for bit either way).
+static bool wedge_enabled() {
+    const char* e = getenv("SPHRT_TRACE_WEDGE");
+    return !(e && e[0] == '0');
+}
 
 // Which launches of a trace a call makes: screen (hit list; counts/zeros/bounds of the misses)
 // and trace (the hit rays + the deferred exact ones).  BOUND screens only; EMIT traces the hit
@@ -1556,6 +1621,7 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     // the walk integrates one channel per ray (a register accumulator)
     o.walk = walk_enabled() && (MODE != MODE_INTEGRATE || o.n_chan == 1 || o.ray_chan_div > 0) &&
              (size_t)walk_tab_words(G) * 8 <= kWalkTabMax;
+    o.wedge = wedge_enabled();
     Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
     if constexpr (MODE == MODE_BOUND) steps = kScreen;
     if constexpr (MODE == MODE_EMIT) steps = kTrace;

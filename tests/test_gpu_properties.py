@@ -349,6 +349,75 @@ def test_wide_families_vs_oracle(case, gpu):
     assert np.allclose(have, want, rtol=1e-10, atol=1e-12)
 
 
+def _wedge_rays(n, seed):
+    """Lines from outside the unit ball: aimed at random points of it, at points 1e-12..1e-3 off
+    the z axis, nearly vertical, from the azimuth seam (x on the negative x axis), and with
+    their closest approach to the z axis around the 1e-6 threshold of the half-plane wedge."""
+    rng = np.random.default_rng(seed)
+    xs = np.empty((n, 3))
+    d = np.empty((n, 3))
+    for i in range(n):
+        u = rng.normal(size=3)
+        start = u / np.linalg.norm(u) * rng.uniform(1.05, 8)
+        kind = i % 5
+        eps = 10.0 ** rng.uniform(-12, -3)
+        if kind == 0:
+            v = rng.normal(size=3)
+            tgt = v / np.linalg.norm(v) * rng.uniform(0, 1) ** (1 / 3)
+        elif kind == 1:
+            tgt = np.array([eps, eps * rng.uniform(-1, 1), rng.uniform(-0.9, 0.9)])
+        elif kind == 2:
+            start = np.array([rng.uniform(-0.6, 0.6), rng.uniform(-0.6, 0.6), rng.choice([-3, 3])])
+            tgt = start + np.array([eps, eps * rng.uniform(-1, 1), -np.sign(start[2])])
+        elif kind == 3:
+            start = np.array([-rng.uniform(1.5, 6), 0.0, rng.uniform(-1, 1)])
+            tgt = np.array([0.0, rng.uniform(-0.5, 0.5), rng.uniform(-0.5, 0.5)])
+        else:
+            rho = 1e-6 * rng.uniform(0.5, 2)
+            phi = rng.uniform(-np.pi, np.pi)
+            tgt = np.array([rho * np.cos(phi), rho * np.sin(phi), rng.uniform(-0.5, 0.5)])
+            start = tgt + 3 * np.array([-np.sin(phi), np.cos(phi), rng.uniform(-0.3, 0.3)])
+        xs[i] = start
+        d[i] = tgt - start
+    return xs, d
+
+
+@pytest.mark.parametrize('shape, size_a', [((30, 40, 150), None), ((20, 70, 100), (-1.0, 2.5)),
+                                           ((20, 30, 90), (-3.0, 3.0)), ((128, 128, 128), None),
+                                           ((64, 64, 64), None)])
+def test_plane_wedge_exact(shape, size_a, gpu, monkeypatch):
+    """The half-plane wedge (trace.hip: only the cyclic run of half-planes inside the azimuth
+    range a line sweeps over [0, t_hi] is solved) changes nothing: the CSR with it equals the CSR
+    without it (SPHRT_TRACE_WEDGE=0) bit for bit, and the voxel sequences equal the oracle's —
+    full and partial azimuth ranges (one across the +-pi seam); near-axis, vertical, seam and
+    threshold lines.  Lengths against the oracle within 1e-9: ill-conditioned cone roots (lines
+    near the z axis, or nearly parallel to a generator) differ between the device and the C
+    oracle by up to ~1e-11 with or without the wedge, an ulp of a square root amplified."""
+    from oracle import oracle
+    from sph_raytracer_amd import Operator, SphericalGrid, ViewGeom
+    from sph_raytracer_amd.raytracer import find_starts
+    kw = {} if size_a is None else {'size_a': size_a}
+    grid = SphericalGrid(shape=shape, **kw)
+    xs, d = _wedge_rays(5000, sum(shape))
+    geom = ViewGeom(tr.from_numpy(xs), tr.from_numpy(d))
+    got = tuple(t.cpu().numpy() for t in Operator(grid, geom, device=gpu).segments())
+    monkeypatch.setenv('SPHRT_TRACE_WEDGE', '0')
+    full = tuple(t.cpu().numpy() for t in Operator(grid, geom, device=gpu).segments())
+    for a, b in zip(got, full):
+        assert np.array_equal(a, b)
+    oracle.use_mkl_sqrt(False)
+    g = oracle.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy())
+    ref = oracle.trace_segments(g, xs, d, find_starts(grid, tr.from_numpy(xs)).numpy())
+    assert np.array_equal(np.asarray(ref[0]), got[0])
+    assert np.array_equal(np.asarray(ref[1]), got[1])
+    lr = np.asarray(ref[2])
+    err = np.abs(got[2] - lr)
+    k = int(np.argmax(err))
+    ray = int(np.searchsorted(np.asarray(ref[0]), k, side='right') - 1)
+    assert err[k] <= 1e-9, (f'ray {ray} (kind {ray % 5}) x {xs[ray].tolist()} d {d[ray].tolist()}'
+                            f': segment {k - ref[0][ray]} {lr[k]!r} vs {got[2][k]!r}')
+
+
 def test_half_tables_float64(gpu, monkeypatch):
     """C5 geometry (granule tables of up to 1512 entries: float64 forwards stage them in two
     halves, apply.hip HALF): float64 forward and transposed adjoint against the C oracle on the
