@@ -547,13 +547,20 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
 // from a block radix sort of the workgroup's segments by granule (hipCUB, 16 per thread), value
 // = position << 3 | head << 2 | voxel & 3.  O(segments · key bits) per workgroup instead of
 // O(volume): at C3 (2 M voxels, 64 k workgroups) 10.6 ms of bitmap work.  Identical output.
+// 10 bits per pass (rocprim's match ranking): C3's 19-bit granule keys in 2 passes instead of
+// the default 8-bit 3 (local_table_radix_kernel 1324 -> 1240 us; 6 bits: 1404 us).
+#ifndef SPHRT_RADIX_BITS
+#define SPHRT_RADIX_BITS 10
+#endif
 template <int ITEMS, int TM>
 struct RadixTable {
     // the count pass sorts keys only (its values are dead)
     using Sort = typename std::conditional<
-        TM != kTabCount, hipcub::BlockRadixSort<uint32_t, kThreads, ITEMS, uint16_t>,
-        hipcub::BlockRadixSort<uint32_t, kThreads, ITEMS>>::type;
-    using Storage = typename Sort::TempStorage;
+        TM != kTabCount,
+        rocprim::block_radix_sort<uint32_t, kThreads, ITEMS, uint16_t, 1, 1, SPHRT_RADIX_BITS>,
+        rocprim::block_radix_sort<uint32_t, kThreads, ITEMS, rocprim::empty_type, 1, 1,
+                                  SPHRT_RADIX_BITS>>::type;
+    using Storage = typename Sort::storage_type;
 };
 
 // One block's table from a sort of its n <= ITEMS * kThreads segments (block-uniform call).
@@ -580,8 +587,8 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
             val[i] = (uint16_t)((p << 3) | ((x >> 31) << 2) | (v & 3u));
         }
     }
-    if constexpr (TM != kTabCount) typename RT::Sort(ts).Sort(key, val, 0, key_bits);   // blocked:
-    else typename RT::Sort(ts).Sort(key, 0, key_bits);            // thread t: [ITEMS t, ITEMS t + ITEMS)
+    if constexpr (TM != kTabCount) typename RT::Sort().sort(key, val, ts, 0, key_bits);  // blocked:
+    else typename RT::Sort().sort(key, ts, 0, key_bits);         // thread t: [ITEMS t, ITEMS t + ITEMS)
     last_key[tid] = key[ITEMS - 1];
     __syncthreads();
     uint32_t prev = tid > 0 ? last_key[tid - 1] : 0xffffffffu;

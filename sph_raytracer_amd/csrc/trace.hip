@@ -52,6 +52,10 @@ __device__ unsigned long long g_trace_cycles[16];   // 8..12: exact_wave_kernel
 #endif
 constexpr size_t kLdsBytes = 160 * 1024;        // LDS per CU; one workgroup may take all of it
 
+#ifndef SPHRT_SORT_INLINE
+#define SPHRT_SORT_INLINE
+#endif
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -232,7 +236,7 @@ __device__ __forceinline__ bool finish_sort(const uint64_t (&k)[M], uint64_t* ke
 //
 // Full sort: the bitonic network over all F <= 64*M entries.
 template <int M>
-__device__ bool sort_regs(uint64_t* keys, uint32_t* pays, int F, int Sf, int cap, int lane,
+__device__ SPHRT_SORT_INLINE bool sort_regs(uint64_t* keys, uint32_t* pays, int F, int Sf, int cap, int lane,
                           uint64_t cmask) {
     uint64_t k[M];
     const int front = F - Sf;
@@ -253,7 +257,7 @@ __device__ bool sort_regs(uint64_t* keys, uint32_t* pays, int F, int Sf, int cap
 // half-cleaner layers) sorts it.  C3 (F ~153, ~88 shell entries): 28 + 8 layers on 2 + 4
 // registers instead of 36 on 4.
 template <int M, int M2>
-__device__ bool merge_sort(uint64_t* keys, uint32_t* pays, int F, int Sn, int Sf, int cap,
+__device__ SPHRT_SORT_INLINE bool merge_sort(uint64_t* keys, uint32_t* pays, int F, int Sn, int Sf, int cap,
                            int lane, uint64_t cmask) {
     const int S = Sn + Sf, O = F - S;
     {
@@ -442,6 +446,94 @@ __device__ bool ambiguous_ties(const uint64_t* keys, const uint32_t* pays, int F
         grp = __shfl(g, 63);
     }
     return __ballot(amb) != 0;
+}
+
+// Forward fill, lengths and compaction (trace_one phase 3) over a sorted list of F <= 64*M
+// entries read lane-major — lane L holds entries L*M .. L*M + M - 1: each lane carries the
+// region rows through its M entries in registers, and one wave scan per row joins the lanes
+// (the chunk loop scans each row once per 64 entries), one prefix sum places the segments.
+// The rules are the chunk loop's: an entry updates its family's row (the start entry all
+// three), a segment runs to the next entry's distance, and it is kept when its length is
+// positive and finite and its voxel inside the grid.
+struct FillState {
+    int sr, se, sa;        // start voxel (the start entry's update)
+    int r0, e0, a0;        // rows before the first entry
+    int r_lim, e_lim, start_c;
+};
+template <int M, bool STORE>
+__device__ SPHRT_SORT_INLINE int fill_regs(const GridDev& G, const uint64_t* keys, const uint32_t* pays, int F,
+                         int lane, const FillState& fs, double* seg_len, int32_t* seg_vox) {
+    uint64_t kb[M];
+    int ur[M], ue[M], ua[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int e = lane * M + i;
+        kb[i] = e < F ? keys[e] : 0ull;
+        const uint32_t p = e < F ? pays[e] : 0u;
+        const int cand = (int)(p >> 16);
+        const int reg = (int)(p & 0xffffu) - 2;
+        ur[i] = ue[i] = ua[i] = kNone;
+        if (e < F) {
+            if (cand == fs.start_c) {
+                ur[i] = fs.sr; ue[i] = fs.se; ua[i] = fs.sa;
+            } else if (cand < fs.r_lim) {
+                ur[i] = reg;
+            } else if (cand < fs.e_lim) {
+                if (reg != -2) ue[i] = reg;
+            } else {
+                if (reg != -2) ua[i] = reg;
+            }
+        }
+        if (i > 0) {
+            if (ur[i] == kNone) ur[i] = ur[i - 1];
+            if (ue[i] == kNone) ue[i] = ue[i - 1];
+            if (ua[i] == kNone) ua[i] = ua[i - 1];
+        }
+    }
+    // rows entering this lane's entries: the last update in the lanes before it
+    int pr = __shfl_up(scan_last(ur[M - 1], lane), 1);
+    int pe = __shfl_up(scan_last(ue[M - 1], lane), 1);
+    int pa = __shfl_up(scan_last(ua[M - 1], lane), 1);
+    if (lane == 0 || pr == kNone) pr = fs.r0;
+    if (lane == 0 || pe == kNone) pe = fs.e0;
+    if (lane == 0 || pa == kNone) pa = fs.a0;
+    const uint64_t next0 = (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)kb[0], 1) |
+                           ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(kb[0] >> 32), 1) << 32);
+    double len[M];
+    int vox[M];
+    bool ok[M];
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int e = lane * M + i;
+        const int r = ur[i] != kNone ? ur[i] : pr;
+        const int ee = ue[i] != kNone ? ue[i] : pe;
+        const int a = ua[i] != kNone ? ua[i] : pa;
+        const double t = __longlong_as_double((long long)kb[i]);
+        const double tn = e + 1 >= F ? kInf
+                        : __longlong_as_double((long long)(i + 1 < M ? kb[i + 1] : next0));
+        len[i] = tn - t;
+        ok[i] = e < F && len[i] > 0.0 && __builtin_isfinite(len[i]) && r >= 0 && r < G.nr &&
+                ee >= 0 && ee < G.ne && a >= 0 && a < G.na;
+        vox[i] = (r * G.ne + ee) * G.na + a;
+        cnt += ok[i] ? 1 : 0;
+    }
+    const int incl = wave_scan(cnt, 0, [](int x, int y) { return x + y; });
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    if (STORE) {
+        wave_sync();
+        int pos = incl - cnt;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            if (ok[i]) {
+                seg_len[pos] = len[i];
+                seg_vox[pos] = vox[i];
+                ++pos;
+            }
+        }
+        wave_sync();
+    }
+    return total;
 }
 
 __device__ __forceinline__ void load_ray(const RaysDev& R, int64_t i, double* x, double* d,
@@ -754,7 +846,15 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     int32_t* seg_vox = reinterpret_cast<int32_t*>(pays);
     int cr = sr, cE = e_in, cA = a_in;  // state before the first sorted entry
     int nseg = 0;
-    for (int c0 = 0; c0 < F; c0 += 64) {
+    constexpr bool kStore = MODE != MODE_COUNT;
+    const FillState fs{sr, se, sa, sr, e_in, a_in, r_lim, e_lim, start_c};
+    if (!pair_fmt) {                    // F <= 512: the list in registers, lane-major
+        nseg = F <= 64 ? fill_regs<1, kStore>(G, keys, pays, F, lane, fs, seg_len, seg_vox)
+             : F <= 128 ? fill_regs<2, kStore>(G, keys, pays, F, lane, fs, seg_len, seg_vox)
+             : F <= 256 ? fill_regs<4, kStore>(G, keys, pays, F, lane, fs, seg_len, seg_vox)
+                        : fill_regs<8, kStore>(G, keys, pays, F, lane, fs, seg_len, seg_vox);
+    }
+    for (int c0 = 0; pair_fmt && c0 < F; c0 += 64) {
         const int e = c0 + lane;
         const bool real = e < F;
         uint64_t k = 0;
