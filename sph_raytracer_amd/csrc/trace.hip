@@ -8,9 +8,12 @@
 //      non-negative crossings to a per-wave LDS list (ballot + mbcnt compaction); the most
 //      negative finite distance is reduced across the wave (it bounds the behind-start segment);
 //   2. the list is sorted by (distance, candidate index) — a total order equal to a stable sort
-//      of the reference's concatenation — in registers (<= 512 entries) or in LDS;
-//   3. 64-entry chunks are scanned (forward fill of the r/e/a rows), differenced and the
-//      non-zero in-grid segments compacted, in order, back into LDS;
+//      of the reference's concatenation — in registers (<= 512 entries: one 64-bit composite
+//      key per entry; the shells' crossings listed as one pre-sorted run and merged with the
+//      sorted rest in one bitonic stage) or in LDS (longer lists);
+//   3. the sorted list is scanned (forward fill of the r/e/a rows: in registers, lane-major,
+//      for lists of <= 512 entries), differenced and the non-zero in-grid segments compacted, in
+//      order, back into LDS;
 //   4. depending on MODE the segments are counted, copied to the CSR, or integrated against
 //      the density right away (no-store mode).
 // Nothing of size K ever reaches HBM.
