@@ -350,15 +350,18 @@ __device__ void sort_lds(uint64_t* keys, uint32_t* pays, int F, int lane) {
     }
 }
 
-// A screened hit ray as the trace kernel reads it: start, direction, start voxel, ray id (one
-// 64-byte record, read with scalar loads by the wave that traces it: no broadcast index
-// arithmetic and no RaysDev in the trace kernel's registers).
+// A screened hit ray as the trace kernel reads it: its solve set-up (make_ray, evaluated once by
+// the screen lane instead of by all 64 lanes of the tracing wave: six IEEE divisions and four
+// square roots per ray), start voxel and ray id — one 128-byte record, read with scalar loads by
+// the wave that traces it (no broadcast index arithmetic and no RaysDev in the trace kernel's
+// registers).
 struct HitRay {
-    double x[3];
-    double d[3];
+    RayGeo g;
     int32_t s[3];
     int32_t ray;
+    int32_t pad[2];
 };
+static_assert(sizeof(HitRay) == 128, "HitRay is one 128-byte record");
 
 template <typename T>
 struct TraceOut {
@@ -1087,10 +1090,10 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
     base = __shfl(base, __builtin_ctzll(m));
     if (listed) {
         HitRay h;
-        h.x[0] = x[0]; h.x[1] = x[1]; h.x[2] = x[2];
-        h.d[0] = d[0]; h.d[1] = d[1]; h.d[2] = d[2];
+        h.g = g;
         h.s[0] = s[0]; h.s[1] = s[1]; h.s[2] = s[2];
         h.ray = (int32_t)ray;
+        h.pad[0] = h.pad[1] = 0;
         o.hits[base + __popcll(m & lanemask_lt(lane))] = h;
     }
 }
@@ -1137,10 +1140,10 @@ __device__ __forceinline__ void walk_one(const GridDev& G, const RaysDev& R, con
     }
     if (status == 2) {
         HitRay hr;
-        hr.x[0] = x[0]; hr.x[1] = x[1]; hr.x[2] = x[2];
-        hr.d[0] = d[0]; hr.d[1] = d[1]; hr.d[2] = d[2];
+        hr.g = g;
         hr.s[0] = s[0]; hr.s[1] = s[1]; hr.s[2] = s[2];
         hr.ray = (int32_t)ray;
+        hr.pad[0] = hr.pad[1] = 0;
         o.hits[atomicAdd(o.n_hits, 1u)] = hr;
         return;
     }
@@ -1188,7 +1191,7 @@ __global__ __launch_bounds__(256, SPHRT_TRACE_MIN_BLOCKS) void trace_kernel(Grid
     for (int64_t h = (int64_t)blockIdx.x * waves + wid; h < n_hits;
          h += (int64_t)gridDim.x * waves) {
         const HitRay& hr = o.hits[__builtin_amdgcn_readfirstlane((int)h)];   // uniform record
-        const RayGeo g = make_ray(hr.x[0], hr.x[1], hr.x[2], hr.d[0], hr.d[1], hr.d[2]);
+        const RayGeo g = hr.g;
         trace_one<MODE, T>(G, g, hr.s[0], hr.s[1], hr.s[2], hr.ray, keys, pays, cap, lane, o);
     }
 }
