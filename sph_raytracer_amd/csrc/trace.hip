@@ -357,9 +357,9 @@ __device__ void sort_lds(uint64_t* keys, uint32_t* pays, int F, int lane) {
 // registers).
 struct HitRay {
     RayGeo g;
+    double t1c_o;       // half the chord of the outer sphere, sqrt(r_outer^2 - dd^2)
     int32_t s[3];
     int32_t ray;
-    int32_t pad[2];
 };
 static_assert(sizeof(HitRay) == 128, "HitRay is one 128-byte record");
 
@@ -389,7 +389,13 @@ struct TraceOut {
 template <typename T>
 __device__ __forceinline__ int64_t emit_slot(const TraceOut<T>& o, int64_t ray, int64_t cnt,
                                              bool leader) {
-    const int64_t b0 = o.row_ptr[ray], cap = o.row_ptr[ray + 1] - b0;
+    return emit_slot(o, ray, cnt, leader, o.row_ptr[ray], o.row_ptr[ray + 1]);
+}
+// (the same with the slot bounds b0 = row_ptr[ray], b1 = row_ptr[ray + 1] already loaded)
+template <typename T>
+__device__ __forceinline__ int64_t emit_slot(const TraceOut<T>& o, int64_t ray, int64_t cnt,
+                                             bool leader, int64_t b0, int64_t b1) {
+    const int64_t cap = b1 - b0;
     if (leader) o.counts[ray] = (int32_t)cnt;
     if (cnt <= cap) return b0;
     if (leader) atomicAdd(o.n_over, 1ull);
@@ -574,11 +580,17 @@ __device__ __forceinline__ int first_may_cross(int n, int lane, Ok ok) {
 
 // Trace ray `ray` (wave-uniform) with the whole wave.  keys/pays: this wave's LDS list.
 template <int MODE, typename T>
-__device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const int se,
+__device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
+                          const int sr, const int se,
                           const int sa, const int64_t ray, uint64_t* keys, uint32_t* pays,
                           const int cap, const int lane, const TraceOut<T>& o) {
     // ---- 1. crossings -> LDS list (finite, t >= 0), min finite negative distance ----------
     TRACE_T(ts0);
+    // the ray's output slot bounds, loaded now: their round trip overlaps the solves instead of
+    // following the sort
+    int64_t slot0 = 0, slot1 = 0;
+    if (MODE == MODE_FILL || MODE == MODE_EMIT) slot0 = o.row_ptr[ray];
+    if (MODE == MODE_EMIT) slot1 = o.row_ptr[ray + 1];
     // The list holds composite keys: the distance's bits (t >= 0: ordered as unsigned integers)
     // with the low `cbits` bits replaced by the candidate index, so the sort moves and compares
     // one 64-bit word per entry; pays[candidate] keeps the replaced bits and the region.  A list
@@ -591,8 +603,10 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     int nfar = 0;       // shells' far crossings, from keys[cap - 1] down (composite layout)
     int s_near = 0;     // shells' near crossings: keys[0, s_near)
     double tneg = kInf;
+    // the behind-start segment (and so tneg) exists only for a start inside the grid
+    const bool start_ok = sr >= 0 && sr < G.nr && se >= 0 && se < G.ne && sa >= 0 && sa < G.na;
     auto note = [&](double t) {
-        if (t < 0.0 && __builtin_isfinite(t)) tneg = fmin(tneg, t);
+        if (start_ok && t < 0.0 && __builtin_isfinite(t)) tneg = fmin(tneg, t);
     };
     auto push = [&](bool has, double t, int cand, int reg, bool far = false) {
         const uint64_t m = __ballot(has);
@@ -618,7 +632,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     // last cone / half-plane crossing before t_lo (the start entry's values if none).  That
     // entry state is reduced across the wave below; a tie of different values in its last group
     // defers the ray, exactly as a tie inside the list would.  (C2: 85 -> 62 entries per ray.)
-    const double t1c_o = __builtin_sqrt(G.r_outer * G.r_outer - g.dd * g.dd);  // = sphere nr
+    // t1c_o = sqrt(r_outer^2 - dd^2), sphere nr's half chord (from the hit record)
     const double t_lo = g.tc - t1c_o, t_hi = g.tc + t1c_o;
     const bool clip_lo = t_lo > 0.0;
     auto keep = [&](double t) {
@@ -654,8 +668,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     // |p_xy| >= 1e-6.  Exact: test_plane_wedge_exact (CSR bitwise the same without the wedge).
     int p_start = 0, p_count = nba;
     {
-        const bool start_ok =
-            sr >= 0 && sr < G.nr && se >= 0 && se < G.ne && sa >= 0 && sa < G.na;
         const double Lz = g.x0 * g.w1 - g.x1 * g.w0;
         if (o.wedge && nba > 64 && G.a_asc && !start_ok && __builtin_isfinite(t_hi) &&
             Lz * Lz >= 1e-12 * (g.w0 * g.w0 + g.w1 * g.w1)) {
@@ -762,7 +774,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
         pair_fmt = true;
         wave_sync();
     }
-    tneg = wave_min(tneg);
+    if (start_ok) tneg = wave_min(tneg);
     // rows entering the outer sphere (start outside): the last pre-entry update group per row
     int e_in = se, a_in = sa;
     if (clip_lo) {
@@ -845,7 +857,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
 #endif
     TRACE_T(ts3);
     TRACE_ADD(2, ts2, ts3);
-    const bool start_ok = sr >= 0 && sr < G.nr && se >= 0 && se < G.ne && sa >= 0 && sa < G.na;
     // every distance behind the start is integrated in the start voxel (raytracer.py:126,140)
     const int head = (start_ok && tneg < 0.0) ? 1 : 0;
     double* seg_len = reinterpret_cast<double*>(keys);
@@ -921,8 +932,9 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const int sr, const
     if (MODE == MODE_COUNT) {
         if (lane == 0) o.counts[ray] = head + nseg;
     } else if (MODE == MODE_FILL || MODE == MODE_EMIT) {
-        const int64_t r0 = MODE == MODE_FILL ? o.row_ptr[ray]
-                                             : emit_slot(o, ray, head + nseg, lane == 0);
+        const int64_t r0 = MODE == MODE_FILL ? slot0
+                                             : emit_slot(o, ray, head + nseg, lane == 0, slot0,
+                                                         slot1);
         if (r0 < 0) {
             wave_sync();
             return;
@@ -1091,9 +1103,9 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
     if (listed) {
         HitRay h;
         h.g = g;
+        h.t1c_o = t1c_outer;
         h.s[0] = s[0]; h.s[1] = s[1]; h.s[2] = s[2];
         h.ray = (int32_t)ray;
-        h.pad[0] = h.pad[1] = 0;
         o.hits[base + __popcll(m & lanemask_lt(lane))] = h;
     }
 }
@@ -1141,9 +1153,9 @@ __device__ __forceinline__ void walk_one(const GridDev& G, const RaysDev& R, con
     if (status == 2) {
         HitRay hr;
         hr.g = g;
+        hr.t1c_o = __builtin_sqrt(G.r_outer * G.r_outer - g.dd * g.dd);
         hr.s[0] = s[0]; hr.s[1] = s[1]; hr.s[2] = s[2];
         hr.ray = (int32_t)ray;
-        hr.pad[0] = hr.pad[1] = 0;
         o.hits[atomicAdd(o.n_hits, 1u)] = hr;
         return;
     }
@@ -1192,7 +1204,8 @@ __global__ __launch_bounds__(256, SPHRT_TRACE_MIN_BLOCKS) void trace_kernel(Grid
          h += (int64_t)gridDim.x * waves) {
         const HitRay& hr = o.hits[__builtin_amdgcn_readfirstlane((int)h)];   // uniform record
         const RayGeo g = hr.g;
-        trace_one<MODE, T>(G, g, hr.s[0], hr.s[1], hr.s[2], hr.ray, keys, pays, cap, lane, o);
+        trace_one<MODE, T>(G, g, hr.t1c_o, hr.s[0], hr.s[1], hr.s[2], hr.ray, keys, pays, cap,
+                           lane, o);
     }
 }
 
