@@ -171,19 +171,33 @@ __device__ __forceinline__ void cone_root(const GridDev& G, const RayGeo& g, int
     t = cone_root_t(G, g, j, t);
     reg = r;
 }
-// The two roots of cone j's quadratic with the reference's snapping and overrides, before the
-// per-root fix-up (slot j "t1", slot nbe + j "t2").
-__device__ __forceinline__ void cone_quadratic(const GridDev& G, const RayGeo& g, int j,
-                                               double& t1, double& t2) {
+// Cone j's quadratic coefficients with the reference's snapping (|a|, |delta| < close_tol -> 0).
+struct ConeQuad {
+    double aa, bb, cc, delta;
+};
+__device__ __forceinline__ ConeQuad cone_coeffs(const GridDev& G, const RayGeo& g, int j) {
     const double th = G.close_tol;
-    double c2 = G.c2_e()[j];
+    const double c2 = G.c2_e()[j];
     double aa = g.w2 * g.w2 - c2;
-    double bb = 2.0 * (g.w2 * g.x2 - g.wx * c2);
-    double cc = g.x2 * g.x2 - g.nx2 * c2;
+    const double bb = 2.0 * (g.w2 * g.x2 - g.wx * c2);
+    const double cc = g.x2 * g.x2 - g.nx2 * c2;
     if (__builtin_fabs(aa) < th) aa = 0.0;
     double delta = bb * bb - (4.0 * aa) * cc;
     if (__builtin_fabs(delta) < th) delta = 0.0;
-    double q = __builtin_sqrt(delta);
+    return ConeQuad{aa, bb, cc, delta};
+}
+// cone_may_cross on coefficients already computed (the trace solves a chunk from the same ones)
+__device__ __forceinline__ bool cone_q_may_cross(const GridDev& G, const ConeQuad& q) {
+    const double th = G.close_tol;
+    return q.delta >= 0.0 || (__builtin_fabs(q.aa) < th && !(__builtin_fabs(q.bb) < th));
+}
+// The two roots of the quadratic with the reference's overrides, before the per-root fix-up
+// (slot j "t1", slot nbe + j "t2").
+__device__ __forceinline__ void cone_roots_q(const GridDev& G, const ConeQuad& c, double& t1,
+                                             double& t2) {
+    const double th = G.close_tol;
+    const double aa = c.aa, bb = c.bb, cc = c.cc;
+    double q = __builtin_sqrt(c.delta);
     t1 = (-bb + q) / (2.0 * aa);
     t2 = (-bb - q) / (2.0 * aa);
     if (__builtin_fabs(aa) < th && !(__builtin_fabs(bb) < th)) {  // ray parallel to a generator
@@ -195,16 +209,25 @@ __device__ __forceinline__ void cone_quadratic(const GridDev& G, const RayGeo& g
         t2 = kInf;
     }
 }
-// Both roots of cone j: slot j ("t1") and slot nbe + j ("t2").
-__device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeo& g, int j,
-                                           double& ta, int& rega, double& tb, int& regb,
-                                           int& nega, int& negb) {
+__device__ __forceinline__ void cone_quadratic(const GridDev& G, const RayGeo& g, int j,
+                                               double& t1, double& t2) {
+    cone_roots_q(G, cone_coeffs(G, g, j), t1, t2);
+}
+// Both roots of cone j: slot j ("t1") and slot nbe + j ("t2"), from its coefficients.
+__device__ __forceinline__ void cone_solve_q(const GridDev& G, const RayGeo& g, int j,
+                                             const ConeQuad& q, double& ta, int& rega,
+                                             double& tb, int& regb, int& nega, int& negb) {
     double t1, t2;
-    cone_quadratic(G, g, j, t1, t2);
+    cone_roots_q(G, q, t1, t2);
     cone_root(G, g, j, t1, rega, nega);
     cone_root(G, g, j, t2, regb, negb);
     ta = t1;
     tb = t2;
+}
+__device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeo& g, int j,
+                                           double& ta, int& rega, double& tb, int& regb,
+                                           int& nega, int& negb) {
+    cone_solve_q(G, g, j, cone_coeffs(G, g, j), ta, rega, tb, regb, nega, negb);
 }
 
 // ---- azimuth half-planes (a_torch, raytracer.py:505-550) ------------------------------------

@@ -203,8 +203,8 @@ __device__ __forceinline__ void sort_stages(uint64_t (&k)[M], int lane) {
 // order.  The full distances are checked on the way out; true means some adjacent pair is out of
 // order (fix_near_ties repairs it).
 template <int M>
-__device__ __forceinline__ bool finish_sort(const uint64_t (&k)[M], uint64_t* keys,
-                                            uint32_t* pays, int F, int lane, uint64_t cmask) {
+__device__ __forceinline__ int finish_sort(const uint64_t (&k)[M], uint64_t* keys,
+                                           uint32_t* pays, int F, int lane, uint64_t cmask) {
     uint64_t tb[M];
     uint32_t py[M];
 #pragma unroll
@@ -214,11 +214,15 @@ __device__ __forceinline__ bool finish_sort(const uint64_t (&k)[M], uint64_t* ke
         tb[i] = (k[i] & ~cmask) | (uint64_t)(info >> 16);
         py[i] = (cand << 16) | (info & 0xffffu);
     }
-    bool bad = false;
+    bool bad = false, eq = false;
 #pragma unroll
-    for (int i = 1; i < M; ++i) bad |= lane * M + i < F && tb[i] < tb[i - 1];
+    for (int i = 1; i < M; ++i) {
+        bad |= lane * M + i < F && tb[i] < tb[i - 1];
+        eq |= lane * M + i < F && tb[i] == tb[i - 1];
+    }
     const uint64_t prev = (uint64_t)__shfl_up((long long)tb[M - 1], 1);
     bad |= lane > 0 && lane * M < F && tb[0] < prev;
+    eq |= lane > 0 && lane * M < F && tb[0] == prev;
     wave_sync();
 #pragma unroll
     for (int i = 0; i < M; ++i) {
@@ -229,7 +233,9 @@ __device__ __forceinline__ bool finish_sort(const uint64_t (&k)[M], uint64_t* ke
         }
     }
     wave_sync();
-    return __ballot(bad) != 0;
+    // bit 0: adjacent disorder (fix_near_ties); bit 1: equal adjacent distances (ambiguous_ties
+    // has something to look at — after a repair, equal ones may have been apart)
+    return (__ballot(bad) != 0 ? 3 : 0) | (__ballot(eq) != 0 ? 2 : 0);
 }
 
 // The list trace_one builds (composite keys, see there): the shells' near crossings at
@@ -239,7 +245,7 @@ __device__ __forceinline__ bool finish_sort(const uint64_t (&k)[M], uint64_t* ke
 //
 // Full sort: the bitonic network over all F <= 64*M entries.
 template <int M>
-__device__ SPHRT_SORT_INLINE bool sort_regs(uint64_t* keys, uint32_t* pays, int F, int Sf, int cap, int lane,
+__device__ SPHRT_SORT_INLINE int sort_regs(uint64_t* keys, uint32_t* pays, int F, int Sf, int cap, int lane,
                           uint64_t cmask) {
     uint64_t k[M];
     const int front = F - Sf;
@@ -260,7 +266,7 @@ __device__ SPHRT_SORT_INLINE bool sort_regs(uint64_t* keys, uint32_t* pays, int 
 // half-cleaner layers) sorts it.  C3 (F ~153, ~88 shell entries): 28 + 8 layers on 2 + 4
 // registers instead of 36 on 4.
 template <int M, int M2>
-__device__ SPHRT_SORT_INLINE bool merge_sort(uint64_t* keys, uint32_t* pays, int F, int Sn, int Sf, int cap,
+__device__ SPHRT_SORT_INLINE int merge_sort(uint64_t* keys, uint32_t* pays, int F, int Sn, int Sf, int cap,
                            int lane, uint64_t cmask) {
     const int S = Sn + Sf, O = F - S;
     {
@@ -426,6 +432,8 @@ __device__ __forceinline__ int row_value(uint32_t pay, int row, int start_c, con
 // group (the segments inside a group have zero length).  Equal-valued ties — a double root of
 // the e = pi/2 "cone", a tangent sphere, a boundary crossing that re-enters the start voxel —
 // are order-independent and stay on the fast path.
+__device__ bool tie_groups_ambiguous(const uint64_t* keys, const uint32_t* pays, int F, int lane,
+                                     int r_lim, int e_lim, int start_c, const int* sv);
 __device__ bool ambiguous_ties(const uint64_t* keys, const uint32_t* pays, int F, int lane,
                                int r_lim, int e_lim, int start_c, const int* sv) {
     bool any = false;
@@ -434,6 +442,11 @@ __device__ bool ambiguous_ties(const uint64_t* keys, const uint32_t* pays, int F
         any |= __ballot(e < F && keys[e] == keys[e - 1]) != 0;
     }
     if (!any) return false;
+    return tie_groups_ambiguous(keys, pays, F, lane, r_lim, e_lim, start_c, sv);
+}
+// (the analysis itself, for a list known to hold equal adjacent distances)
+__device__ bool tie_groups_ambiguous(const uint64_t* keys, const uint32_t* pays, int F, int lane,
+                                     int r_lim, int e_lim, int start_c, const int* sv) {
     int grp = 0;                          // start of the current tie group (carried)
     int last[3] = {-1, -1, -1};           // last updater of each row so far (carried)
     bool amb = false;
@@ -745,10 +758,12 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
         for (int j0 = nbe > 64 ? first_may_cross(nbe, lane, cone_ok) : 0; j0 < nbe; j0 += 64) {
             const int j = j0 + lane;
             const bool v = j < nbe;
-            if (nbe > 64 && __ballot(v && cone_ok(j)) == 0) continue;
+            ConeQuad q{};
+            if (v) q = cone_coeffs(G, g, j);   // once for the chunk test and the solve
+            if (nbe > 64 && __ballot(v && cone_q_may_cross(G, q)) == 0) continue;
             double ta = kInf, tb = kInf;
             int ra = 0, rb = 0, na_, nb_;
-            if (v) cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
+            if (v) cone_solve_q(G, g, j, q, ta, ra, tb, rb, na_, nb_);
             note(ta);
             note(tb);
             pre(v, ta, ra, pe_t, pe_v, pe_amb);
@@ -811,23 +826,23 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
 #endif
     TRACE_T(ts1);
     TRACE_ADD(0, ts0, ts1);
-    bool near_tie = false;
+    int sflags = 2;          // bit 0: repair the order; bit 1: look for ambiguous ties
     const int n_other = F - s_near - nfar;   // entries outside the shells' sorted run
     if (pair_fmt) sort_lds(keys, pays, F, lane);
-    else if (F <= 64) near_tie = sort_regs<1>(keys, pays, F, nfar, cap, lane, cmask);
+    else if (F <= 64) sflags = sort_regs<1>(keys, pays, F, nfar, cap, lane, cmask);
     else if (F <= 128) {
-        near_tie = n_other <= 64 ? merge_sort<2, 1>(keys, pays, F, s_near, nfar, cap, lane, cmask)
+        sflags = n_other <= 64 ? merge_sort<2, 1>(keys, pays, F, s_near, nfar, cap, lane, cmask)
                                  : sort_regs<2>(keys, pays, F, nfar, cap, lane, cmask);
     } else if (F <= 256) {
-        near_tie = n_other <= 64 ? merge_sort<4, 1>(keys, pays, F, s_near, nfar, cap, lane, cmask)
+        sflags = n_other <= 64 ? merge_sort<4, 1>(keys, pays, F, s_near, nfar, cap, lane, cmask)
                  : n_other <= 128 ? merge_sort<4, 2>(keys, pays, F, s_near, nfar, cap, lane, cmask)
                                   : sort_regs<4>(keys, pays, F, nfar, cap, lane, cmask);
     } else {                                                  // C3: 15 % of hit rays
-        near_tie = n_other <= 128 ? merge_sort<8, 2>(keys, pays, F, s_near, nfar, cap, lane, cmask)
+        sflags = n_other <= 128 ? merge_sort<8, 2>(keys, pays, F, s_near, nfar, cap, lane, cmask)
                  : n_other <= 256 ? merge_sort<8, 4>(keys, pays, F, s_near, nfar, cap, lane, cmask)
                                   : sort_regs<8>(keys, pays, F, nfar, cap, lane, cmask);
     }
-    if (near_tie) fix_near_ties(keys, pays, F, lane);
+    if (sflags & 1) fix_near_ties(keys, pays, F, lane);
 
 #if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 2
     if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 2
@@ -839,7 +854,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     TRACE_ADD(1, ts1, ts2);
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe, start_c = G.K - 1;
     const int start_vals[3] = {sr, se, sa};
-    if (ambiguous_ties(keys, pays, F, lane, r_lim, e_lim, start_c, start_vals)) {
+    if ((sflags & 2) && ambiguous_ties(keys, pays, F, lane, r_lim, e_lim, start_c, start_vals)) {
         if (lane == 0) {
             const unsigned long long q = atomicAdd(o.n_deferred, 1ull);
             o.deferred[q] = ray;
