@@ -563,15 +563,31 @@ __device__ SPHRT_SORT_INLINE int fill_regs(const GridDev& G, const uint64_t* key
 
 __device__ __forceinline__ void load_ray(const RaysDev& R, int64_t i, double* x, double* d,
                                          int* s) {
-    int64_t xo = 0, ro = 0, rem = i;
+    int64_t xo = 0, ro = 0;
+    if (R.n <= 0x7fffffff) {
+        // 32-bit index arithmetic (a 64-bit division is a long software sequence on the GPU)
+        uint32_t rem = (uint32_t)i;
 #pragma unroll
-    for (int dd = kMaxDims - 1; dd >= 0; --dd) {
-        if (dd < R.ndim) {
-            const int64_t sz = R.shape[dd];
-            const int64_t c = rem % sz;
-            rem /= sz;
-            xo += c * R.xs_stride[dd];
-            ro += c * R.rays_stride[dd];
+        for (int dd = kMaxDims - 1; dd >= 0; --dd) {
+            if (dd < R.ndim) {
+                const uint32_t sz = (uint32_t)R.shape[dd];
+                const uint32_t q = rem / sz, c = rem - q * sz;
+                rem = q;
+                xo += (int64_t)c * R.xs_stride[dd];
+                ro += (int64_t)c * R.rays_stride[dd];
+            }
+        }
+    } else {
+        int64_t rem = i;
+#pragma unroll
+        for (int dd = kMaxDims - 1; dd >= 0; --dd) {
+            if (dd < R.ndim) {
+                const int64_t sz = R.shape[dd];
+                const int64_t c = rem % sz;
+                rem /= sz;
+                xo += c * R.xs_stride[dd];
+                ro += c * R.rays_stride[dd];
+            }
         }
     }
     x[0] = R.xs[xo]; x[1] = R.xs[xo + 1]; x[2] = R.xs[xo + 2];
@@ -1049,8 +1065,15 @@ __device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok) {
             const double pa = atan2(ay, ax), dp = atan2(cr, dt);
             const double lo = fmin(pa, pa + dp) - 1e-6, hi = fmax(pa, pa + dp) + 1e-6;
             const double two_pi = 6.283185307179586;
+            // only the shifted windows that can overlap [a_b[0], a_b[nba - 1]] (the others
+            // count nothing; one window of margin either side for rounding): three instead of
+            // five for the usual [-pi, pi] grid
+            const double a_lo = G.a_b()[0], a_hi = G.a_b()[G.nba - 1];
+            const int k0 = max(-2, (int)__builtin_ceil((a_lo - hi) / two_pi) - 1);
+            const int k1 = min(2, (int)__builtin_floor((a_hi - lo) / two_pi) + 1);
             int c = 0;
-            for (int k = -2; k <= 2; ++k) c += count_in(G.a_b(), G.nba, lo + k * two_pi, hi + k * two_pi);
+            for (int k = k0; k <= k1; ++k)
+                c += count_in(G.a_b(), G.nba, lo + k * two_pi, hi + k * two_pi);
             if (__builtin_isfinite(lo) && __builtin_isfinite(hi)) b_a = min(c + 2, G.nba);
         }
     }
