@@ -630,17 +630,148 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
     }
 }
 
+// The same table with the duplicates removed before the sort (blocks of <= 2048 segments): a
+// block's ~1800 segments touch only ~650 distinct granules (C3; at most 1088), so the granules
+// go into an LDS hash set first (open addressing, kHashSlots keys, compare-and-swap insert; a
+// thread's consecutive segments of one granule insert once), the distinct ones are compacted
+// and only they are radix-sorted (4 keys per thread up to 1024 of them, else 8), their sorted
+// positions are written over their hash slots, and every segment reads its rank from its slot.
+// Same tables and loc as radix_table (distinct granules ascending; a segment's rank is its
+// granule's position), whatever order the inserts race in.
+constexpr int kHashSlots = 4096;                 // >= 2 x the 2048 segments: load factor <= 1/2
+template <int ITEMS>
+using HashSort = rocprim::block_radix_sort<uint32_t, kThreads, ITEMS, uint16_t, 1, 1,
+                                           SPHRT_RADIX_BITS>;
+struct HashUniq {                                // distinct granules, compacted
+    uint32_t key[kPass];
+    uint16_t slot[kPass];
+};
+constexpr size_t kHashTail =
+    sizeof(HashUniq) > sizeof(typename HashSort<8>::storage_type)
+        ? (sizeof(HashUniq) > sizeof(typename HashSort<4>::storage_type)
+               ? sizeof(HashUniq) : sizeof(typename HashSort<4>::storage_type))
+        : sizeof(typename HashSort<8>::storage_type);
+constexpr size_t kHashLds = kHashSlots * 4 + kHashTail;
+
+template <int ITEMS, typename TabT>
+__device__ __forceinline__ void hash_sort_rank(int n_tab, uint32_t* hs, HashUniq& u,
+                                               unsigned char* sort_raw, TabT* __restrict__ tab_b,
+                                               int key_bits) {
+    const int tid = threadIdx.x;
+    uint32_t key[ITEMS];
+    uint16_t val[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const int q = tid * ITEMS + i;
+        key[i] = q < n_tab ? u.key[q] : 0xffffffffu;   // padding sorts last
+        val[i] = q < n_tab ? u.slot[q] : (uint16_t)0;
+    }
+    __syncthreads();                                     // the sort storage aliases u
+    auto& ts = *reinterpret_cast<typename HashSort<ITEMS>::storage_type*>(sort_raw);
+    HashSort<ITEMS>().sort(key, val, ts, 0, key_bits);   // blocked: thread t, [ITEMS t, +ITEMS)
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const int q = tid * ITEMS + i;
+        if (q < n_tab) {
+            tab_b[q] = (TabT)key[i];
+            hs[val[i]] = (uint32_t)q;                    // the slot now holds the rank
+        }
+    }
+}
+
+template <int TM, typename TabT>
+__device__ __forceinline__ void hash_table(int64_t* m, const int32_t* __restrict__ vox,
+                                           uint16_t* __restrict__ loc, TabT* __restrict__ tab_b,
+                                           int64_t s0, int n, int key_bits, const StageMap& sm,
+                                           unsigned char* lds, ScanShared& sh,
+                                           unsigned long long* stats) {
+    constexpr int ITEMS = 8;
+    constexpr uint32_t kEmpty = 0xffffffffu;
+    uint32_t* hs = reinterpret_cast<uint32_t*>(lds);
+    HashUniq& u = *reinterpret_cast<HashUniq*>(lds + kHashSlots * 4);
+    const int tid = threadIdx.x;
+    for (int j = tid; j < kHashSlots; j += kThreads) hs[j] = kEmpty;
+    uint32_t x[ITEMS];
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const int p = tid * ITEMS + i;
+        x[i] = p < n ? (uint32_t)vox[s0 + p] : 0u;
+    }
+    __syncthreads();
+    uint16_t slot[ITEMS];
+    uint32_t owned = 0;
+    uint32_t prev_key = kEmpty;
+    uint16_t prev_slot = 0;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const int p = tid * ITEMS + i;
+        uint32_t h = prev_slot;
+        if (p < n) {
+            const uint32_t key = stage_col(x[i] & ~kHead, sm) >> 2;
+            if (key != prev_key) {
+                h = (key * 0x9e3779b1u) >> 20;           // 12-bit multiplicative hash
+                for (;;) {
+                    const uint32_t old = atomicCAS(&hs[h], kEmpty, key);
+                    if (old == kEmpty) { owned |= 1u << i; break; }
+                    if (old == key) break;
+                    h = (h + 1) & (kHashSlots - 1);
+                }
+                prev_key = key;
+            }
+        }
+        slot[i] = prev_slot = (uint16_t)h;
+    }
+    __syncthreads();
+    int n_tab;
+    int base = block_excl_count(__builtin_popcount(owned), n_tab, sh);
+    if (TM != kTabFill) {
+        if (tid == 0) {
+            if (n_tab > kMaxGran) {
+                m[5] = -1;
+                atomicAdd(stats, 1ull);
+            } else {
+                m[5] = n_tab;
+                atomicMax(stats + 1, (unsigned long long)n_tab);
+            }
+        }
+        if (TM == kTabCount || n_tab > kMaxGran) return;
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        if (owned & (1u << i)) {
+            u.key[base] = hs[slot[i]];
+            u.slot[base] = slot[i];
+            ++base;
+        }
+    }
+    __syncthreads();
+    unsigned char* sort_raw = lds + kHashSlots * 4;
+    if (n_tab <= 4 * kThreads) hash_sort_rank<4>(n_tab, hs, u, sort_raw, tab_b, key_bits);
+    else hash_sort_rank<8>(n_tab, hs, u, sort_raw, tab_b, key_bits);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const int p = tid * ITEMS + i;
+        if (p < n) {
+            const uint32_t v = stage_col(x[i] & ~kHead, sm);
+            loc[s0 + p] = loc_code((int)hs[slot[i]], v, (x[i] & kHead) != 0);
+        }
+    }
+}
+
 // Blocks of up to 2048 segments (most: a block owns the rows starting in 1792 segments) sort 8
-// keys per thread, larger ones 16: half the sort work for the common case.
+// keys per thread (or only their distinct granules: hash_table), larger ones 16: half the sort
+// work for the common case.
 template <int TM, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
-    unsigned long long* stats) {
-    constexpr size_t kTs = sizeof(typename RadixTable<16, TM>::Storage) >
-                                   sizeof(typename RadixTable<8, TM>::Storage)
-                               ? sizeof(typename RadixTable<16, TM>::Storage)
-                               : sizeof(typename RadixTable<8, TM>::Storage);
+    unsigned long long* stats, int use_hash) {
+    constexpr size_t kTs0 = sizeof(typename RadixTable<16, TM>::Storage) >
+                                    sizeof(typename RadixTable<8, TM>::Storage)
+                                ? sizeof(typename RadixTable<16, TM>::Storage)
+                                : sizeof(typename RadixTable<8, TM>::Storage);
+    constexpr size_t kTs = kTs0 > kHashLds ? kTs0 : kHashLds;
     __shared__ __attribute__((aligned(16))) unsigned char ts_raw[kTs];
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
@@ -656,7 +787,9 @@ __global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
         return;
     }
     TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
-    if (n <= 8 * kThreads)
+    if (n <= 8 * kThreads && use_hash)
+        hash_table<TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, sh, stats);
+    else if (n <= 8 * kThreads)
         radix_table<8, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key,
                                  sh, stats);
     else
@@ -1477,6 +1610,13 @@ static int granule_key_bits(int64_t n_cols) {
     return b;
 }
 
+// Granule tables of blocks of <= 2048 segments from the hash-deduplicated sort (hash_table);
+// SPHRT_TABLE_SORT=radix sorts every segment instead (radix_table).  Same tables.
+static int table_hash_on() {
+    const char* e = getenv("SPHRT_TABLE_SORT");
+    return !(e && e[0] == 'r');
+}
+
 extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_t* stats,
                                      void* stream) {
     if (!c || !c->vox || !blocks || !stats) return fail("incomplete CSR for the granule tables");
@@ -1497,7 +1637,7 @@ extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_
     }
     hipLaunchKernelGGL((local_table_radix_kernel<kTabCount, int32_t>), dim3((unsigned)c->n_blocks),
                        dim3(kThreads), 0, st, blocks, c->vox, nullptr, nullptr, 0,
-                       granule_key_bits(cols), sm, (unsigned long long*)stats);
+                       granule_key_bits(cols), sm, (unsigned long long*)stats, table_hash_on());
     return check_launch("local_table_radix_kernel<count>");
 }
 
@@ -1530,11 +1670,11 @@ extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, u
     if (u16)
         hipLaunchKernelGGL((local_table_radix_kernel<kTabFill, uint16_t>), dim3((unsigned)c->n_blocks),
                            dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (uint16_t*)tab,
-                           tab_stride, kb, sm, nullptr);
+                           tab_stride, kb, sm, nullptr, table_hash_on());
     else
         hipLaunchKernelGGL((local_table_radix_kernel<kTabFill, int32_t>), dim3((unsigned)c->n_blocks),
                            dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (int32_t*)tab,
-                           tab_stride, kb, sm, nullptr);
+                           tab_stride, kb, sm, nullptr, table_hash_on());
     return check_launch("local_table_radix_kernel<fill>");
 }
 
@@ -1568,10 +1708,12 @@ extern "C" int sphrt_csr_local_build(const sphrt_csr* c, int64_t* blocks, uint16
     const int kb = granule_key_bits(cols);
     if (u16)
         hipLaunchKernelGGL((local_table_radix_kernel<kTabBuild, uint16_t>), g, b, 0, st, blocks,
-                           c->vox, loc, (uint16_t*)tab_wide, kTabWide, kb, sm, s);
+                           c->vox, loc, (uint16_t*)tab_wide, kTabWide, kb, sm, s,
+                           table_hash_on());
     else
         hipLaunchKernelGGL((local_table_radix_kernel<kTabBuild, int32_t>), g, b, 0, st, blocks,
-                           c->vox, loc, (int32_t*)tab_wide, kTabWide, kb, sm, s);
+                           c->vox, loc, (int32_t*)tab_wide, kTabWide, kb, sm, s,
+                           table_hash_on());
     return check_launch("local_table_radix_kernel<build>");
 }
 

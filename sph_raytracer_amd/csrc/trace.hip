@@ -1645,6 +1645,13 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
 // [row_ptr[r0], row_ptr[r0 + 64]): lane i holds ray r0 + i's row pointer and slot, and every lane
 // copies segments lane, lane + 64, ... of the range, finding its ray by a 6-step binary search
 // over the lanes' row pointers — independent loads and stores, no per-row serial loop.
+#ifndef SPHRT_COMPACT_BLOCKS
+#define SPHRT_COMPACT_BLOCKS 8192   // workgroups of the compaction (waves stride over the rays)
+#endif
+#ifndef SPHRT_COMPACT_U
+#define SPHRT_COMPACT_U 4
+#endif
+constexpr int kCompactU = SPHRT_COMPACT_U;   // 64-segment chunks per step, loads before stores
 __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* __restrict__ slot,
                                                       const int64_t* __restrict__ row_ptr,
                                                       const int32_t* __restrict__ svox,
@@ -1666,12 +1673,12 @@ __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* 
         // before any store (one memory round trip per 256 segments, not per 64)
         const int32_t total = (int32_t)(end - a0);
         const int64_t dl = b - a;                             // slot - row start of lane's ray
-        for (int32_t q0 = 0; q0 < total; q0 += 256) {
-            int64_t src[4];
-            int32_t vv[4];
-            double ll[4];
+        for (int32_t q0 = 0; q0 < total; q0 += 64 * kCompactU) {
+            int64_t src[kCompactU];
+            int32_t vv[kCompactU];
+            double ll[kCompactU];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < kCompactU; ++u) {
                 const int32_t pos = q0 + 64 * u + lane;
                 int lo = 0;
 #pragma unroll
@@ -1682,13 +1689,13 @@ __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* 
                 src[u] = a0 + pos + __shfl(dl, lo);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < kCompactU; ++u) {
                 const bool in = q0 + 64 * u + lane < total;
                 if (vox && in) vv[u] = svox[src[u]];
                 if (len && in) ll[u] = slen[src[u]];
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < kCompactU; ++u) {
                 const int32_t pos = q0 + 64 * u + lane;
                 if (pos < total) {
                     if (vox) vox[a0 + pos] = vv[u];
@@ -1888,7 +1895,8 @@ extern "C" int sphrt_trace_compact(int64_t n, const int64_t* bound_ptr, const in
         return fail("null compact argument");
     StreamGuard guard(stream);
     const int64_t waves = (n + 63) / 64;
-    const int64_t blocks = (waves + 3) / 4 < 8192 ? (waves + 3) / 4 : 8192;
+    const int64_t cap = SPHRT_COMPACT_BLOCKS;
+    const int64_t blocks = (waves + 3) / 4 < cap ? (waves + 3) / 4 : cap;
     hipLaunchKernelGGL(compact_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                        n, bound_ptr, row_ptr, svox, slen, vox, len);
     return check_launch("compact_kernel");

@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Operator construction + first forward (the reference's cold definition, as bench.py's
+`operator_seconds`) on a bench config, median of --reps warm repetitions; for A/B runs of
+environment switches (e.g. SPHRT_TABLE_SORT=radix) and under rocprofv3 for the kernel split.
+
+    python tools/operator_time.py --config c3 [--reps 7]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='c3')
+    ap.add_argument('--reps', type=int, default=7)
+    args = ap.parse_args()
+    import bench
+    from sph_raytracer_amd import Operator
+    dev = torch.device('cuda', 0)
+    cfg = bench.CONFIGS[args.config]
+    grid, geom = bench.build_geometry(cfg, 0, 1)
+    x = torch.rand(cfg[0], dtype=cfg[4], device=dev)
+    op = Operator(grid, geom, device=dev)        # warm-up: HIP and allocator initialisation
+    op(x)
+    del op
+    times = []
+    for _ in range(args.reps):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        op = Operator(grid, geom, device=dev)
+        op(x)
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+        del op
+    times.sort()
+    env = {k: v for k, v in os.environ.items() if k.startswith('SPHRT_')}
+    print(json.dumps({'config': args.config, 'operator_ms_median': 1e3 * times[len(times) // 2],
+                      'operator_ms_min': 1e3 * times[0], 'reps': args.reps, 'env': env}))
+
+
+if __name__ == '__main__':
+    main()
