@@ -637,7 +637,7 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
 // and only they are radix-sorted (4 keys per thread up to 1024 of them, else 8), their sorted
 // positions are written over their hash slots, and every segment reads its rank from its slot.
 // Same tables and loc as radix_table (distinct granules ascending; a segment's rank is its
-// granule's position), whatever order the inserts race in.
+// granule's position), whatever order the inserts race in.  Opt-in (table_hash_on): slower at C3.
 constexpr int kHashSlots = 4096;                 // >= 2 x the 2048 segments: load factor <= 1/2
 template <int ITEMS>
 using HashSort = rocprim::block_radix_sort<uint32_t, kThreads, ITEMS, uint16_t, 1, 1,
@@ -1610,11 +1610,14 @@ static int granule_key_bits(int64_t n_cols) {
     return b;
 }
 
-// Granule tables of blocks of <= 2048 segments from the hash-deduplicated sort (hash_table);
-// SPHRT_TABLE_SORT=radix sorts every segment instead (radix_table).  Same tables.
+// Granule tables of blocks of <= 2048 segments from the sort of every segment (radix_table), or
+// with SPHRT_TABLE_SORT=hash from the hash-deduplicated sort (hash_table).  Same tables.  The
+// hash set measured slower at C3 (local_table_radix_kernel 1268 -> 1503 us: the compare-and-swap
+// inserts and twice the LDS cost more than the smaller sort saves; C4's Operator 1.70 -> 1.66 ms,
+// within box spread), so it is opt-in.
 static int table_hash_on() {
     const char* e = getenv("SPHRT_TABLE_SORT");
-    return !(e && e[0] == 'r');
+    return e && e[0] == 'h';
 }
 
 extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_t* stats,

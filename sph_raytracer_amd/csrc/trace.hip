@@ -1645,8 +1645,11 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
 // [row_ptr[r0], row_ptr[r0 + 64]): lane i holds ray r0 + i's row pointer and slot, and every lane
 // copies segments lane, lane + 64, ... of the range, finding its ray by a 6-step binary search
 // over the lanes' row pointers — independent loads and stores, no per-row serial loop.
+// Workgroups of the compaction (waves stride over the rays past it).  Uncapped by default: one
+// step of 64 rays per wave, C3 compact_kernel 700 -> 599 us against a cap of 8192 workgroups
+// (8 chunks per step: 660 us; both: 629 us).
 #ifndef SPHRT_COMPACT_BLOCKS
-#define SPHRT_COMPACT_BLOCKS 8192   // workgroups of the compaction (waves stride over the rays)
+#define SPHRT_COMPACT_BLOCKS (1 << 30)
 #endif
 #ifndef SPHRT_COMPACT_U
 #define SPHRT_COMPACT_U 4

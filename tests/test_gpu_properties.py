@@ -819,7 +819,7 @@ def test_onepass_tables_equal_twopass(grid_shape, staged, gpu, monkeypatch):
 @pytest.mark.parametrize('case', ['orbit', 'orbit_staged', 'random_rays', 'dynamic'])
 def test_hash_tables_equal_radix(case, gpu, monkeypatch):
     """Granule tables of blocks <= 2048 segments built from the hash-deduplicated sort
-    (apply.hip hash_table, the default) equal the sort of every segment (SPHRT_TABLE_SORT=radix)
+    (apply.hip hash_table, SPHRT_TABLE_SORT=hash) equal the sort of every segment (the default)
     bitwise: block records, loc, tables, stride, fallback count — orbits above 2^19 voxels
     (natural and brick-staged columns), random lines (blocks of 1025-2046 distinct granules: the
     8-key sort of the distinct granules, and blocks over kMaxGran: the fallback) and a
