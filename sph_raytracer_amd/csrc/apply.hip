@@ -192,6 +192,13 @@ __global__ __launch_bounds__(256) void block_runs_kernel(const int64_t* __restri
     if (over || over_e) atomicAdd(stats, 1ull);
 }
 
+// Raise *p to v.  Most workgroups' values are below the running maximum, so a plain load of it
+// (possibly stale, which is safe: the maximum only grows) skips their atomic — every one of the
+// table kernels' 64 k workgroups (C3) would otherwise queue an atomic on the same address.
+__device__ __forceinline__ void atomic_max_sparse(unsigned long long* p, unsigned long long v) {
+    if (v > __atomic_load_n(p, __ATOMIC_RELAXED)) atomicMax(p, v);
+}
+
 // ---- block-level scans (256 threads = 4 waves) -----------------------------------------------
 struct ScanShared {
     int cnt[4];
@@ -519,7 +526,7 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
                 atomicAdd(stats, 1ull);
             } else {
                 m[5] = n_tab;
-                atomicMax(stats + 1, (unsigned long long)n_tab);
+                atomic_max_sparse(stats + 1, (unsigned long long)n_tab);
             }
         }
         if (TM == kTabCount || n_tab > kMaxGran) return;
@@ -587,8 +594,10 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
             val[i] = (uint16_t)((p << 3) | ((x >> 31) << 2) | (v & 3u));
         }
     }
+#ifndef SPHRT_TAB_ABL_SORT   // ablation build only (wrong tables): the sort's share of the kernel
     if constexpr (TM != kTabCount) typename RT::Sort().sort(key, val, ts, 0, key_bits);  // blocked:
     else typename RT::Sort().sort(key, ts, 0, key_bits);         // thread t: [ITEMS t, ITEMS t + ITEMS)
+#endif
     last_key[tid] = key[ITEMS - 1];
     __syncthreads();
     uint32_t prev = tid > 0 ? last_key[tid - 1] : 0xffffffffu;
@@ -609,7 +618,7 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
                 atomicAdd(stats, 1ull);
             } else {
                 m[5] = n_tab;
-                atomicMax(stats + 1, (unsigned long long)n_tab);
+                atomic_max_sparse(stats + 1, (unsigned long long)n_tab);
             }
         }
         if (TM == kTabCount || n_tab > kMaxGran) return;
@@ -731,7 +740,7 @@ __device__ __forceinline__ void hash_table(int64_t* m, const int32_t* __restrict
                 atomicAdd(stats, 1ull);
             } else {
                 m[5] = n_tab;
-                atomicMax(stats + 1, (unsigned long long)n_tab);
+                atomic_max_sparse(stats + 1, (unsigned long long)n_tab);
             }
         }
         if (TM == kTabCount || n_tab > kMaxGran) return;
