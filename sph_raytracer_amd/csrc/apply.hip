@@ -771,17 +771,25 @@ __device__ __forceinline__ void hash_table(int64_t* m, const int32_t* __restrict
 // Blocks of up to 2048 segments (most: a block owns the rows starting in 1792 segments) sort 8
 // keys per thread (or only their distinct granules: hash_table), larger ones 16: half the sort
 // work for the common case.
-template <int TM, typename TabT = int32_t>
-__global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
+// (HASH: the hash-set variant, its own instantiation so that its LDS does not cost the default
+// kernel occupancy.)  Two launches: BIG = false takes the blocks of <= 2048 segments (8 keys per
+// thread), BIG = true the larger ones (16 keys) and marks those over kLocalMax; each workgroup of
+// a launch whose block belongs to the other exits at once.  Apart, the common kernel is not sized
+// for the 16-key sort's registers.
+#ifndef SPHRT_TAB_WAVES
+#define SPHRT_TAB_WAVES 1   // minimum waves per SIMD the 8-key table kernel's registers aim for
+#endif
+template <int TM, typename TabT, bool HASH, bool BIG>
+constexpr size_t table_lds() {
+    constexpr size_t r = sizeof(typename RadixTable<BIG ? 16 : 8, TM>::Storage);
+    return HASH && !BIG && kHashLds > r ? kHashLds : r;
+}
+template <int TM, typename TabT = int32_t, bool HASH = false, bool BIG = false>
+__global__ __launch_bounds__(kThreads, BIG ? 1 : SPHRT_TAB_WAVES) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
-    unsigned long long* stats, int use_hash) {
-    constexpr size_t kTs0 = sizeof(typename RadixTable<16, TM>::Storage) >
-                                    sizeof(typename RadixTable<8, TM>::Storage)
-                                ? sizeof(typename RadixTable<16, TM>::Storage)
-                                : sizeof(typename RadixTable<8, TM>::Storage);
-    constexpr size_t kTs = kTs0 > kHashLds ? kTs0 : kHashLds;
-    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[kTs];
+    unsigned long long* stats) {
+    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, HASH, BIG>()];
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
     int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
@@ -789,21 +797,22 @@ __global__ __launch_bounds__(kThreads) void local_table_radix_kernel(
     if (TM == kTabFill && m[5] < 0) return;
     const int64_t n = s1 - s0;
     if (n > kLocalMax) {
-        if (TM != kTabFill && threadIdx.x == 0) {
+        if (BIG && TM != kTabFill && threadIdx.x == 0) {
             m[5] = -1;
             atomicAdd(stats, 1ull);
         }
         return;
     }
+    if ((n > 8 * kThreads) != BIG) return;
     TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
-    if (n <= 8 * kThreads && use_hash)
-        hash_table<TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, sh, stats);
-    else if (n <= 8 * kThreads)
-        radix_table<8, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key,
-                                 sh, stats);
-    else
+    if constexpr (BIG)
         radix_table<16, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key,
                                   sh, stats);
+    else if constexpr (HASH)
+        hash_table<TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, sh, stats);
+    else
+        radix_table<8, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key,
+                                 sh, stats);
 }
 
 // Wide tables (one-pass build, kTabWide entries per block) -> the final stride.
@@ -1629,6 +1638,24 @@ static int table_hash_on() {
     return e && e[0] == 'h';
 }
 
+template <int TM, typename TabT>
+static auto pick_table_kernel(bool hash) {
+    return hash ? local_table_radix_kernel<TM, TabT, true, false>
+                : local_table_radix_kernel<TM, TabT, false, false>;
+}
+
+// The table kernel's two launches (blocks of <= 2048 segments, then the larger ones).
+template <int TM, typename TabT>
+static int launch_tables(bool hash, unsigned nb, hipStream_t st, int64_t* blocks,
+                         const int32_t* vox, uint16_t* loc, TabT* tab, int64_t stride, int kb,
+                         const StageMap& sm, unsigned long long* stats) {
+    hipLaunchKernelGGL((pick_table_kernel<TM, TabT>(hash)), dim3(nb), dim3(kThreads), 0, st,
+                       blocks, vox, loc, tab, stride, kb, sm, stats);
+    hipLaunchKernelGGL((local_table_radix_kernel<TM, TabT, false, true>), dim3(nb), dim3(kThreads),
+                       0, st, blocks, vox, loc, tab, stride, kb, sm, stats);
+    return check_launch("local_table_radix_kernel");
+}
+
 extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_t* stats,
                                      void* stream) {
     if (!c || !c->vox || !blocks || !stats) return fail("incomplete CSR for the granule tables");
@@ -1647,10 +1674,9 @@ extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_
                            0, words, sm, (unsigned long long*)stats);
         return check_launch("local_table_bitmap_kernel<count>");
     }
-    hipLaunchKernelGGL((local_table_radix_kernel<kTabCount, int32_t>), dim3((unsigned)c->n_blocks),
-                       dim3(kThreads), 0, st, blocks, c->vox, nullptr, nullptr, 0,
-                       granule_key_bits(cols), sm, (unsigned long long*)stats, table_hash_on());
-    return check_launch("local_table_radix_kernel<count>");
+    return launch_tables<kTabCount, int32_t>(table_hash_on(), (unsigned)c->n_blocks, st, blocks,
+                                             c->vox, nullptr, nullptr, 0, granule_key_bits(cols),
+                                             sm, (unsigned long long*)stats);
 }
 
 extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, uint16_t* loc,
@@ -1679,15 +1705,13 @@ extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, u
         return check_launch("local_table_bitmap_kernel<fill>");
     }
     const int kb = granule_key_bits(cols);
+    const bool hash = table_hash_on();
+    const unsigned nb = (unsigned)c->n_blocks;
     if (u16)
-        hipLaunchKernelGGL((local_table_radix_kernel<kTabFill, uint16_t>), dim3((unsigned)c->n_blocks),
-                           dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (uint16_t*)tab,
-                           tab_stride, kb, sm, nullptr, table_hash_on());
-    else
-        hipLaunchKernelGGL((local_table_radix_kernel<kTabFill, int32_t>), dim3((unsigned)c->n_blocks),
-                           dim3(kThreads), 0, st, (int64_t*)blocks, c->vox, loc, (int32_t*)tab,
-                           tab_stride, kb, sm, nullptr, table_hash_on());
-    return check_launch("local_table_radix_kernel<fill>");
+        return launch_tables<kTabFill, uint16_t>(hash, nb, st, (int64_t*)blocks, c->vox, loc,
+                                                 (uint16_t*)tab, tab_stride, kb, sm, nullptr);
+    return launch_tables<kTabFill, int32_t>(hash, nb, st, (int64_t*)blocks, c->vox, loc,
+                                            (int32_t*)tab, tab_stride, kb, sm, nullptr);
 }
 
 extern "C" int sphrt_csr_local_build(const sphrt_csr* c, int64_t* blocks, uint16_t* loc,
@@ -1718,15 +1742,12 @@ extern "C" int sphrt_csr_local_build(const sphrt_csr* c, int64_t* blocks, uint16
         return check_launch("local_table_bitmap_kernel<build>");
     }
     const int kb = granule_key_bits(cols);
+    const bool hash = table_hash_on();
     if (u16)
-        hipLaunchKernelGGL((local_table_radix_kernel<kTabBuild, uint16_t>), g, b, 0, st, blocks,
-                           c->vox, loc, (uint16_t*)tab_wide, kTabWide, kb, sm, s,
-                           table_hash_on());
-    else
-        hipLaunchKernelGGL((local_table_radix_kernel<kTabBuild, int32_t>), g, b, 0, st, blocks,
-                           c->vox, loc, (int32_t*)tab_wide, kTabWide, kb, sm, s,
-                           table_hash_on());
-    return check_launch("local_table_radix_kernel<build>");
+        return launch_tables<kTabBuild, uint16_t>(hash, g.x, st, blocks, c->vox, loc,
+                                                  (uint16_t*)tab_wide, kTabWide, kb, sm, s);
+    return launch_tables<kTabBuild, int32_t>(hash, g.x, st, blocks, c->vox, loc,
+                                             (int32_t*)tab_wide, kTabWide, kb, sm, s);
 }
 
 extern "C" int sphrt_csr_local_pack(const sphrt_csr* c, const int64_t* blocks,
