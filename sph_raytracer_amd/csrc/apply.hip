@@ -772,24 +772,23 @@ __device__ __forceinline__ void hash_table(int64_t* m, const int32_t* __restrict
 // keys per thread (or only their distinct granules: hash_table), larger ones 16: half the sort
 // work for the common case.
 // (HASH: the hash-set variant, its own instantiation so that its LDS does not cost the default
-// kernel occupancy.)  Two launches: BIG = false takes the blocks of <= 2048 segments (8 keys per
-// thread), BIG = true the larger ones (16 keys) and marks those over kLocalMax; each workgroup of
-// a launch whose block belongs to the other exits at once.  Apart, the common kernel is not sized
-// for the 16-key sort's registers.
+// kernel occupancy.)  Blocks of more than 2048 segments (the last row's overhang; few) are left
+// to local_table_big_kernel: apart, this kernel is sized for the 8-key sort's registers (72
+// VGPRs, 7 waves per SIMD instead of 4 with the 16-key sort inline: C3 1244 -> 1120 us).
 #ifndef SPHRT_TAB_WAVES
-#define SPHRT_TAB_WAVES 1   // minimum waves per SIMD the 8-key table kernel's registers aim for
+#define SPHRT_TAB_WAVES 7   // minimum waves per SIMD the 8-key table kernel's registers aim for
 #endif
-template <int TM, typename TabT, bool HASH, bool BIG>
+template <int TM, typename TabT, bool HASH, int ITEMS>
 constexpr size_t table_lds() {
-    constexpr size_t r = sizeof(typename RadixTable<BIG ? 16 : 8, TM>::Storage);
-    return HASH && !BIG && kHashLds > r ? kHashLds : r;
+    constexpr size_t r = sizeof(typename RadixTable<ITEMS, TM>::Storage);
+    return HASH && kHashLds > r ? kHashLds : r;
 }
-template <int TM, typename TabT = int32_t, bool HASH = false, bool BIG = false>
-__global__ __launch_bounds__(kThreads, BIG ? 1 : SPHRT_TAB_WAVES) void local_table_radix_kernel(
+template <int TM, typename TabT = int32_t, bool HASH = false>
+__global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
     unsigned long long* stats) {
-    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, HASH, BIG>()];
+    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, HASH, 8>()];
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
     int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
@@ -797,22 +796,53 @@ __global__ __launch_bounds__(kThreads, BIG ? 1 : SPHRT_TAB_WAVES) void local_tab
     if (TM == kTabFill && m[5] < 0) return;
     const int64_t n = s1 - s0;
     if (n > kLocalMax) {
-        if (BIG && TM != kTabFill && threadIdx.x == 0) {
+        if (TM != kTabFill && threadIdx.x == 0) {
             m[5] = -1;
             atomicAdd(stats, 1ull);
         }
         return;
     }
-    if ((n > 8 * kThreads) != BIG) return;
+    if (n > 8 * kThreads) return;                 // local_table_big_kernel's
     TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
-    if constexpr (BIG)
-        radix_table<16, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key,
-                                  sh, stats);
-    else if constexpr (HASH)
+    if constexpr (HASH)
         hash_table<TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, sh, stats);
     else
         radix_table<8, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key,
                                  sh, stats);
+}
+
+// The blocks of 2049..kLocalMax segments: workgroup g looks at blocks [256 g, 256 g + 256) one
+// per thread and sorts the big ones among them in turn (16 keys per thread).  A grid of
+// n_blocks / 256 workgroups, nearly all of which find none.
+template <int TM, typename TabT = int32_t>
+__global__ __launch_bounds__(kThreads) void local_table_big_kernel(
+    int64_t* __restrict__ blocks, int64_t n_blocks, const int32_t* __restrict__ vox,
+    uint16_t* __restrict__ loc, TabT* __restrict__ tab, int64_t tab_stride, int key_bits,
+    StageMap sm, unsigned long long* stats) {
+    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, false, 16>()];
+    __shared__ uint32_t last_key[kThreads];
+    __shared__ ScanShared sh;
+    __shared__ int n_big;
+    __shared__ int32_t big[kThreads];
+    if (threadIdx.x == 0) n_big = 0;
+    __syncthreads();
+    const int64_t b = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (b < n_blocks) {
+        const int64_t* m = blocks + kBlockFields * b;
+        const int64_t n = m[3] - m[2];
+        if (n > 8 * kThreads && n <= kLocalMax && (TM != kTabFill || m[5] >= 0))
+            big[atomicAdd(&n_big, 1)] = threadIdx.x;
+    }
+    __syncthreads();
+    const int nb = n_big;
+    for (int i = 0; i < nb; ++i) {
+        const int64_t bb = (int64_t)blockIdx.x * kThreads + big[i];
+        int64_t* m = blocks + kBlockFields * bb;
+        const int64_t s0 = m[2];
+        radix_table<16, TM, TabT>(m, vox, loc, tab + bb * tab_stride, s0, (int)(m[3] - s0),
+                                  key_bits, sm, ts_raw, last_key, sh, stats);
+        __syncthreads();                          // the sort storage is reused by the next one
+    }
 }
 
 // Wide tables (one-pass build, kTabWide entries per block) -> the final stride.
@@ -1640,8 +1670,7 @@ static int table_hash_on() {
 
 template <int TM, typename TabT>
 static auto pick_table_kernel(bool hash) {
-    return hash ? local_table_radix_kernel<TM, TabT, true, false>
-                : local_table_radix_kernel<TM, TabT, false, false>;
+    return hash ? local_table_radix_kernel<TM, TabT, true> : local_table_radix_kernel<TM, TabT, false>;
 }
 
 // The table kernel's two launches (blocks of <= 2048 segments, then the larger ones).
@@ -1651,8 +1680,9 @@ static int launch_tables(bool hash, unsigned nb, hipStream_t st, int64_t* blocks
                          const StageMap& sm, unsigned long long* stats) {
     hipLaunchKernelGGL((pick_table_kernel<TM, TabT>(hash)), dim3(nb), dim3(kThreads), 0, st,
                        blocks, vox, loc, tab, stride, kb, sm, stats);
-    hipLaunchKernelGGL((local_table_radix_kernel<TM, TabT, false, true>), dim3(nb), dim3(kThreads),
-                       0, st, blocks, vox, loc, tab, stride, kb, sm, stats);
+    hipLaunchKernelGGL((local_table_big_kernel<TM, TabT>), dim3((nb + kThreads - 1) / kThreads),
+                       dim3(kThreads), 0, st, blocks, (int64_t)nb, vox, loc, tab, stride, kb, sm,
+                       stats);
     return check_launch("local_table_radix_kernel");
 }
 

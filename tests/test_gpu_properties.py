@@ -117,6 +117,25 @@ def test_granule_tables_radix_build(gpu):
     _check_granule_tables(grid, geom, Operator(grid, geom, device=gpu), gpu, tab_bytes=4)
 
 
+def test_granule_tables_big_blocks(gpu):
+    """A narrow bundle of lines through the centre of a grid above 2^19 voxels: rows of ~400
+    segments give blocks of more than 2048 segments (the last row's overhang), whose tables come
+    from the separate 16-key launch (local_table_big_kernel); the same checks, and such blocks
+    exist."""
+    from sph_raytracer_amd import Operator, SphericalGrid, ViewGeom
+    grid = SphericalGrid(shape=(96, 80, 90))
+    rng = np.random.default_rng(11)
+    xs = np.tile([1.5, 0.01, 0.02], (20000, 1))
+    d = rng.normal(size=(20000, 3)) * 0.03 - xs
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    geom = ViewGeom(tr.from_numpy(xs), tr.from_numpy(d))
+    op = Operator(grid, geom, device=gpu)
+    blk = op._csr['blocks'].cpu().numpy().reshape(-1, 6)
+    n = blk[:, 3] - blk[:, 2]
+    assert ((n > 2048) & (n <= 4096) & (blk[:, 5] >= 0)).sum() > 0
+    _check_granule_tables(grid, geom, op, gpu, tab_bytes=4)
+
+
 def test_granule_tables_partial_last_granule(gpu):
     """Voxel and ray counts that are not multiples of 4 (the last granule is partial): the table
     forward / transposed adjoint take the chunk-first order with the partial tail copied lane by
