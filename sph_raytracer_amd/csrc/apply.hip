@@ -811,9 +811,11 @@ __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_k
                                  sh, stats);
 }
 
-// The blocks of 2049..kLocalMax segments: workgroup g looks at blocks [256 g, 256 g + 256) one
-// per thread and sorts the big ones among them in turn (16 keys per thread).  A grid of
-// n_blocks / 256 workgroups, nearly all of which find none.
+// The blocks of 2049..kLocalMax segments: workgroup g looks at blocks [kBigScan g, kBigScan g +
+// kBigScan) one per thread and sorts the big ones among them in turn (16 keys per thread).  A
+// grid of n_blocks / kBigScan workgroups (C3: ~6 % of the blocks are big; 256 blocks per
+// workgroup left ~25 sorts in series per workgroup, 110 us).
+constexpr int kBigScan = 32;
 template <int TM, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads) void local_table_big_kernel(
     int64_t* __restrict__ blocks, int64_t n_blocks, const int32_t* __restrict__ vox,
@@ -823,11 +825,11 @@ __global__ __launch_bounds__(kThreads) void local_table_big_kernel(
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
     __shared__ int n_big;
-    __shared__ int32_t big[kThreads];
+    __shared__ int32_t big[kBigScan];
     if (threadIdx.x == 0) n_big = 0;
     __syncthreads();
-    const int64_t b = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (b < n_blocks) {
+    const int64_t b = (int64_t)blockIdx.x * kBigScan + threadIdx.x;
+    if (threadIdx.x < kBigScan && b < n_blocks) {
         const int64_t* m = blocks + kBlockFields * b;
         const int64_t n = m[3] - m[2];
         if (n > 8 * kThreads && n <= kLocalMax && (TM != kTabFill || m[5] >= 0))
@@ -836,7 +838,7 @@ __global__ __launch_bounds__(kThreads) void local_table_big_kernel(
     __syncthreads();
     const int nb = n_big;
     for (int i = 0; i < nb; ++i) {
-        const int64_t bb = (int64_t)blockIdx.x * kThreads + big[i];
+        const int64_t bb = (int64_t)blockIdx.x * kBigScan + big[i];
         int64_t* m = blocks + kBlockFields * bb;
         const int64_t s0 = m[2];
         radix_table<16, TM, TabT>(m, vox, loc, tab + bb * tab_stride, s0, (int)(m[3] - s0),
@@ -1680,7 +1682,7 @@ static int launch_tables(bool hash, unsigned nb, hipStream_t st, int64_t* blocks
                          const StageMap& sm, unsigned long long* stats) {
     hipLaunchKernelGGL((pick_table_kernel<TM, TabT>(hash)), dim3(nb), dim3(kThreads), 0, st,
                        blocks, vox, loc, tab, stride, kb, sm, stats);
-    hipLaunchKernelGGL((local_table_big_kernel<TM, TabT>), dim3((nb + kThreads - 1) / kThreads),
+    hipLaunchKernelGGL((local_table_big_kernel<TM, TabT>), dim3((nb + kBigScan - 1) / kBigScan),
                        dim3(kThreads), 0, st, blocks, (int64_t)nb, vox, loc, tab, stride, kb, sm,
                        stats);
     return check_launch("local_table_radix_kernel");
