@@ -1224,6 +1224,9 @@ __global__ __launch_bounds__(256) void walk_kernel(GridDev G, RaysDev R, TraceOu
 // Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
 // image looks like.  Every lane evaluates the (wave-uniform) ray set-up itself.
 template <int MODE, typename T>
+#ifndef SPHRT_TRACE_GRID
+#define SPHRT_TRACE_GRID 2048   // trace workgroups of kWavesPerBlock waves (scaled for fewer)
+#endif
 #ifndef SPHRT_TRACE_MIN_BLOCKS
 #define SPHRT_TRACE_MIN_BLOCKS 4
 #endif
@@ -1811,7 +1814,7 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
         if (int e = check_launch("walk_kernel")) return e;
     }
     // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
-    const int64_t grid = 2048 * kWavesPerBlock / waves;
+    const int64_t grid = SPHRT_TRACE_GRID * kWavesPerBlock / waves;
     hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,
                        o, cap);
     if (int e = check_launch("trace_kernel")) return e;
