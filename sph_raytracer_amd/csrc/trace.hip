@@ -1224,8 +1224,13 @@ __global__ __launch_bounds__(256) void walk_kernel(GridDev G, RaysDev R, TraceOu
 // Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
 // image looks like.  Every lane evaluates the (wave-uniform) ray set-up itself.
 template <int MODE, typename T>
+// Trace workgroups of kWavesPerBlock waves (scaled for fewer).  Each wave drains a fixed stride
+// of the hit list, so more, shorter-lived workgroups let the dispatcher balance the rays' unequal
+// costs: one-pass emit, µs, grid 2048 / 4096 / 8192 / 16384 (same box, rocprofv3): C3 3495 /
+// 3317 / 3238 / 3200, C5 579 / 575 / 555 / 534, C4 380 / 358 / 352 / 351, C2 129 / 124 / 124 /
+// 127 (profiles/r03_trace_grid_sweep.json).
 #ifndef SPHRT_TRACE_GRID
-#define SPHRT_TRACE_GRID 2048   // trace workgroups of kWavesPerBlock waves (scaled for fewer)
+#define SPHRT_TRACE_GRID 16384
 #endif
 #ifndef SPHRT_TRACE_MIN_BLOCKS
 #define SPHRT_TRACE_MIN_BLOCKS 4
