@@ -1654,13 +1654,14 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
 // copies segments lane, lane + 64, ... of the range, finding its ray by a 6-step binary search
 // over the lanes' row pointers — independent loads and stores, no per-row serial loop.
 // Workgroups of the compaction (waves stride over the rays past it).  Uncapped by default: one
-// step of 64 rays per wave, C3 compact_kernel 700 -> 599 us against a cap of 8192 workgroups
-// (8 chunks per step: 660 us; both: 629 us).
+// step of 64 rays per wave, C3 compact_kernel 774 -> 707 us against a cap of 8192 workgroups on
+// one box.  8 chunks of 64 segments per step (loads before stores) instead of 4: C3 699 -> 669
+// us and 700 -> 660 us on two boxes.
 #ifndef SPHRT_COMPACT_BLOCKS
 #define SPHRT_COMPACT_BLOCKS (1 << 30)
 #endif
 #ifndef SPHRT_COMPACT_U
-#define SPHRT_COMPACT_U 4
+#define SPHRT_COMPACT_U 8
 #endif
 constexpr int kCompactU = SPHRT_COMPACT_U;   // 64-segment chunks per step, loads before stores
 __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* __restrict__ slot,
@@ -1680,8 +1681,8 @@ __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* 
         const int64_t end = row_ptr[r0 + 64 < n ? r0 + 64 : n];
         const int32_t rel = (int32_t)(a - a0);                // < 2^31: 64 rows of <= K segments
         // uniform trip count: every lane takes part in every shuffle (a shuffle from a lane that
-        // left a divergent loop would read nothing); 4 chunks of 64 per step, their loads issued
-        // before any store (one memory round trip per 256 segments, not per 64)
+        // left a divergent loop would read nothing); kCompactU chunks of 64 per step, their loads issued
+        // before any store (one memory round trip per 64 * kCompactU segments, not per 64)
         const int32_t total = (int32_t)(end - a0);
         const int64_t dl = b - a;                             // slot - row start of lane's ray
         for (int32_t q0 = 0; q0 < total; q0 += 64 * kCompactU) {
