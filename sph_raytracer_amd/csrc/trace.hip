@@ -1655,8 +1655,8 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
 // over the lanes' row pointers — independent loads and stores, no per-row serial loop.
 // Workgroups of the compaction (waves stride over the rays past it).  Uncapped by default: one
 // step of 64 rays per wave, C3 compact_kernel 774 -> 707 us against a cap of 8192 workgroups on
-// one box.  8 chunks of 64 segments per step (loads before stores) instead of 4: C3 699 -> 669
-// us and 700 -> 660 us on two boxes.
+// one box.  8 chunks of 64 segments per step (loads before stores) instead of 4: C3 699 -> 669,
+// 700 -> 660 and 694 -> 688 us on three boxes.
 #ifndef SPHRT_COMPACT_BLOCKS
 #define SPHRT_COMPACT_BLOCKS (1 << 30)
 #endif
