@@ -181,6 +181,53 @@ def cpu_baseline(cfg, sample_views, reps):
             'host_cpus': os.cpu_count()}
 
 
+def spawn_ranks(n):
+    """Run this script as `n` child ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one
+    GPU each), as torch.distributed.run would; rank 0 prints the JSON line.  Returns the exit
+    status: non-zero as soon as any rank fails (the others are then stopped).  The parent never
+    initialises the GPU (torch.cuda.device_count() does not, on this image)."""
+    import socket
+    import subprocess
+    one_dev = os.environ.get('SPHRT_BENCH_ONE_DEVICE') == '1'
+    have = torch.cuda.device_count()
+    if not one_dev and have < n:
+        log(f'bench.py --gpus {n}: only {have} GPU(s) visible; run on a node with {n} GPUs '
+            f'(or set SPHRT_BENCH_ONE_DEVICE=1 to rehearse {n} gloo ranks on cuda:0)')
+        return 2
+    with socket.socket() as sk:
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        if one_dev:
+            env.setdefault('SPHRT_BENCH_BACKEND', 'gloo')   # one device cannot hold 2 RCCL ranks
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    status = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                pending.remove(p)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 1
+                    log(f'bench.py: rank {procs.index(p)} exited with {rc}; stopping the others')
+                    for q in pending:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return status
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -193,6 +240,11 @@ def main():
     ap.add_argument('--cpu-cold-views', type=int, default=None,
                     help='views of the cold CPU sample (default: 10, C3: 2)')
     args = ap.parse_args()
+
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # `python bench.py --gpus N` without a launcher: start the N ranks here, before this
+        # process touches the GPU (a process that has initialised HIP must never be replaced)
+        sys.exit(spawn_ranks(args.gpus))
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -222,6 +274,13 @@ def main():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
+
+    def max_over_ranks(vals):
+        # host floats -> their max over ranks (RCCL: a device tensor; gloo: a host one)
+        on = dev if dist.get_backend() == 'nccl' else 'cpu'
+        tt = torch.tensor(vals, dtype=torch.float64, device=on)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return tt.tolist()
 
     # ---- cold: geometry + trace + first forward ----------------------------------------------
     torch.cuda.reset_peak_memory_stats(dev)
@@ -258,9 +317,7 @@ def main():
     dt = time.perf_counter() - t0
     gather = None
     if dist is not None:
-        tt = torch.tensor([dt, t_cold], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt, t_cold = tt.tolist()
+        dt, t_cold = max_over_ranks([dt, t_cold])
         # the final image stack: one RCCL all-gather over xGMI, after the loop (north_star), timed
         # on its own; the gathered stack is checked against this rank's own shard
         y_loc = op(x)
@@ -269,12 +326,13 @@ def main():
         full = sop.gather(y_loc)
         torch.cuda.synchronize(dev)
         t_g = time.perf_counter() - t0
-        tt = torch.tensor([t_g], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_g, = max_over_ranks([t_g])
         ok = bool(torch.equal(full[sop.lo:sop.hi], y_loc))
-        gather = {'ms': tt.item() * 1e3, 'bytes': full.numel() * full.element_size(),
+        gather = {'ms': t_g * 1e3, 'bytes': full.numel() * full.element_size(),
                   'stack_shape': list(full.shape), 'matches_local_shard': ok,
-                  'what': 'one all-gather of the image stack after the timed loop (RCCL all_gather_into_tensor)'}
+                  'backend': dist.get_backend(),
+                  'what': 'one all-gather of the image stack after the timed loop (RCCL '
+                          'all_gather_into_tensor; gloo rehearsals: host-staged)'}
     peak_gb = torch.cuda.max_memory_allocated(dev) / 1e9
 
     # cold path again in a warm process (the reference's 34k rays/s was also taken after
@@ -295,9 +353,7 @@ def main():
     t_warm_cold = sorted(colds)[1]
     t_op_cold = sorted(op_colds)[1]
     if dist is not None:
-        tt = torch.tensor([t_warm_cold, t_op_cold], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_warm_cold, t_op_cold = tt.tolist()
+        t_warm_cold, t_op_cold = max_over_ranks([t_warm_cold, t_op_cold])
 
     # drop-in use with host tensors (the reference's device='cpu' default): H2D density, D2H image
     x_host = x.cpu()
@@ -333,9 +389,7 @@ def main():
         barrier()
         t_adj = (time.perf_counter() - t0) / adj_steps
         if dist is not None:
-            tt = torch.tensor([t_adj], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            t_adj = tt.item()
+            t_adj, = max_over_ranks([t_adj])
         n_vox = math.prod(shape[-3:])
         adj_bytes = n_vox * (x.element_size() + 4) + total_seg * (4 + 2 * x.element_size())
         adjoint = {'ms_per_step': t_adj * 1e3, 'rays_per_s': n_rays * world / t_adj,

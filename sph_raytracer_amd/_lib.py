@@ -125,12 +125,20 @@ def load():
             '`python -m sph_raytracer_amd.build` (hipcc --offload-arch=gfx950). '
             'There is no CPU fallback.')
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-    for name, res, args in _SIGNATURES:
-        fn = getattr(lib, name)
-        fn.restype = res
-        fn.argtypes = args
+    # the source-hash check first: a stale library may lack exports this tree binds, and that
+    # must read as "rebuild", not as an AttributeError from the signature loop
+    lib.sphrt_version.restype = ctypes.c_char_p
+    lib.sphrt_version.argtypes = []
     if not os.environ.get('SPHRT_LIB'):   # an A/B variant may come from other sources
         _check_hash(lib.sphrt_version().decode(), LIB_PATH)
+    for name, res, args in _SIGNATURES:
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            raise RuntimeError(f'sph_raytracer_amd: {LIB_PATH} does not export {name}; rebuild '
+                               'with `python -m sph_raytracer_amd.build`') from None
+        fn.restype = res
+        fn.argtypes = args
     _lib = lib
     return lib
 

@@ -182,11 +182,20 @@ def gd(f, y_local, model, coeffs=None, num_iterations=100, loss_fns=None, optim=
     opt = optim([coeffs], **kwargs)
     plan = _direct_plan(f.local, y_local, model, coeffs, loss_fns, [coeffs]) \
         if hasattr(f.local, '_csr') else None
-    if plan is not None:
-        coeffs, _, losses = _gd_direct(f.local, y_local, coeffs, loss_fns, opt, plan,
-                                       num_iterations, progress_bar, reduce=f.all_reduce,
-                                       n_total=f.n_measurements)
-        return coeffs, f.gather(f(model(coeffs))), losses
+    # the two loops issue different collectives: every rank takes the direct loop or none does
+    flag = tr.tensor([1.0 if plan is not None else 0.0], dtype=tr.float64, device=coeffs.device)
+    if f._host_staged(flag):
+        h = flag.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MIN, group=f.group)
+        flag.copy_(h)
+    else:
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=f.group)
+    if plan is not None and flag.item() == 1.0:
+        best, y_best, losses = _gd_direct(f.local, y_local, coeffs, loss_fns, opt, plan,
+                                          num_iterations, progress_bar, reduce=f.all_reduce,
+                                          n_total=f.n_measurements)
+        # this rank's forward of the returned coefficients is already computed: gather it
+        return best, f.gather(y_best), losses
     losses = {fn: [] for fn in loss_fns}
     for _ in range(num_iterations):
         opt.zero_grad()

@@ -782,7 +782,7 @@ class Operator:
         perm = _trace_order(self.geom, rays)
         ray_id = None
         xs_d, st_d = stg.get(s_xs, xs_h), stg.get(s_st, st_h)
-        if perm is not None and perm.numel() == math.prod(rays.shape[:-1]) and rays.dim() == 4:
+        if perm is not None and rays.dim() == 4 and perm.numel() > math.prod(rays.shape[-3:-1]):
             # an order across views (studies): starts and start voxels follow their rays
             pd = perm.to(dev, non_blocking=True)
             full = tuple(rays.shape[:-1])

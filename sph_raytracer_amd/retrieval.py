@@ -264,7 +264,10 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar, 
                     opt.step()
                 done = it + 1
     except KeyboardInterrupt:
-        pass
+        if reduce is not None:
+            # data-parallel: the other ranks may have stopped at another iteration, and the
+            # loss sums below are reduced over equal lengths only — stop every rank loudly
+            raise
     sums = part_sq[:done].sum(-1)
     if reduce is not None:
         reduce(sums)
@@ -308,8 +311,11 @@ def _split_adam(opt, coeffs):
         return None
     fused, foreach = grp.get('fused'), grp.get('foreach')
     if not fused and foreach is None:       # torch's own resolution (Optimizer defaults)
-        from torch.optim.optimizer import _default_to_fused_or_foreach
-        _, foreach = _default_to_fused_or_foreach([coeffs], False, use_fused=False)
+        try:   # a private torch helper: if it moves or changes, the generic opt.step() runs
+            from torch.optim.optimizer import _default_to_fused_or_foreach
+            _, foreach = _default_to_fused_or_foreach([coeffs], False, use_fused=False)
+        except (ImportError, TypeError):
+            return None
     if not fused and not foreach:
         return None
     lib = _lib.load()

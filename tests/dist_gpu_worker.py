@@ -2,7 +2,8 @@
 
 Launched as a plain child process per rank (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the
 environment), every rank on cuda:0 over gloo (a one-GPU box cannot give two RCCL ranks one
-device).  Each rank checks its results itself (a failed check exits non-zero) and rank 0 writes
+device), or — SPHRT_DIST_BACKEND=nccl, world size 1 — over RCCL with device tensors, so the
+all_gather_into_tensor / device all_reduce branches of distributed.py run (counted, and required).  Each rank checks its results itself (a failed check exits non-zero) and rank 0 writes
 the measured differences to $SPHRT_DIST_OUT as JSON.
 """
 import json
@@ -32,7 +33,24 @@ def rel(a, b):
 def main():
     dev = tr.device('cuda', 0)
     tr.cuda.set_device(dev)
-    dist.init_process_group('gloo')
+    backend = os.environ.get('SPHRT_DIST_BACKEND', 'gloo')
+    seen = {'all_gather_into_tensor': 0, 'all_reduce_cuda': 0}
+    if backend == 'nccl':
+        dist.init_process_group('nccl', device_id=dev)
+        # count the device-side collectives the RCCL path issues (distributed.py)
+        agit, ar = dist.all_gather_into_tensor, dist.all_reduce
+
+        def agit_spy(out, inp, *a, **k):
+            seen['all_gather_into_tensor'] += int(inp.is_cuda)
+            return agit(out, inp, *a, **k)
+
+        def ar_spy(t, *a, **k):
+            seen['all_reduce_cuda'] += int(t.is_cuda)
+            return ar(t, *a, **k)
+
+        dist.all_gather_into_tensor, dist.all_reduce = agit_spy, ar_spy
+    else:
+        dist.init_process_group('gloo')
     rank = dist.get_rank()
     from sph_raytracer_amd import Operator, retrieval
     from sph_raytracer_amd.distributed import ShardedOperator, gd as dgd
@@ -107,6 +125,10 @@ def main():
            'gd_stack': 1e-12, 'gd_sqloss': 1e-12, 'gd_negloss_abs': 1e-15}
     bad = {k: res[k] for k, t in tol.items() if not res[k] <= t}
     res['rank'] = rank
+    res['backend'] = backend
+    res['collectives'] = dict(seen)
+    if backend == 'nccl' and not (seen['all_gather_into_tensor'] and seen['all_reduce_cuda']):
+        bad['rccl_path_not_taken'] = dict(seen)
     if rank == 0 and os.environ.get('SPHRT_DIST_OUT'):
         with open(os.environ['SPHRT_DIST_OUT'], 'w') as fh:
             json.dump(res, fh)

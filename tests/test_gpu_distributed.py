@@ -1,4 +1,5 @@
-"""ShardedOperator with the real HIP Operator: 2 and 3 ranks, all on cuda:0 over gloo.
+"""ShardedOperator with the real HIP Operator: 2 and 3 ranks, all on cuda:0 over gloo, and one
+rank over RCCL ("nccl": device-tensor all_gather_into_tensor and all_reduce).
 
 Each rank is a plain child process (tests/dist_gpu_worker.py).  Against a single-GPU Operator of
 the same geometry: the all-gathered forward stack (float64 within 1e-13 relative, float32 1e-6:
@@ -26,14 +27,15 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize('world', [2, 3])
-def test_sharded_hip_operator_matches_single_gpu(world, gpu, tmp_path):
+@pytest.mark.parametrize('world,backend', [(2, 'gloo'), (3, 'gloo'), (1, 'nccl')])
+def test_sharded_hip_operator_matches_single_gpu(world, backend, gpu, tmp_path):
     out = tmp_path / 'dist.json'
     port = _port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
-                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), SPHRT_DIST_OUT=str(out))
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), SPHRT_DIST_OUT=str(out),
+                   SPHRT_DIST_BACKEND=backend)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, 'dist_gpu_worker.py')],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                       text=True))
@@ -50,3 +52,6 @@ def test_sharded_hip_operator_matches_single_gpu(world, gpu, tmp_path):
     res = json.loads(out.read_text())
     print(json.dumps(res, indent=1))
     assert res['gd_drop'] < 0.05
+    if backend == 'nccl':     # the RCCL branches ran (device all-gather and all-reduce)
+        assert res['collectives']['all_gather_into_tensor'] > 0, res['collectives']
+        assert res['collectives']['all_reduce_cuda'] > 0, res['collectives']
