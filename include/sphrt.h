@@ -97,6 +97,12 @@ const char *sphrt_version(void);
  * (the reference normalises the caller's tensor in place, raytracer.py:281/365). */
 int sphrt_solve(const sphrt_plan *plan, const sphrt_rays *rays, int family,
                 double *t, int32_t *region, int8_t *neg, void *stream);
+/* The same solves in float32 (r_torch / e_torch / a_torch with ftype=torch.float32): starts and
+ * directions rounded to float, every operation in float.  The plan must hold the float32 tables
+ * (boundaries, cos/sin evaluated by torch in float32, stored exactly as doubles) and the float32
+ * thresholds (close_tol = 1e-6 ** (1/3), plane_par_tol = 1e-6: raytracer.py:233-246, 521). */
+int sphrt_solve_f32(const sphrt_plan *plan, const sphrt_rays *rays, int family,
+                    float *t, int32_t *region, int8_t *neg, void *stream);
 
 /* ---- trace to compact CSR (replaces trace_indices, raytracer.py:48-230) -------------------- */
 /* Every trace call takes a caller-allocated device workspace of
@@ -118,6 +124,21 @@ int sphrt_scan_counts(const int32_t *counts, int64_t n, int64_t *row_ptr, void *
 int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64_t *row_ptr,
                      int32_t *vox, double *len, void *workspace, size_t workspace_size,
                      void *stream);
+
+/* Reference-mode trace: the options the fast trace does not take (Operator(..., ftype=float32)
+ * and / or invalid=True, raytracer.py:48-173).  Every ray runs the reference algorithm verbatim
+ * on the device: all K candidates, its (unstable) introsort order, the forward fill and the
+ * length differences.  flags: SPHRT_TRACE_F32 — solves and differences in float32 (a float32
+ * plan, as for sphrt_solve_f32; lengths are float32 values stored as doubles);
+ * SPHRT_TRACE_INVALID — no masking (raytracer.py:155 `if not invalid`): every non-zero length is
+ * kept, inf and NaN included, with its voxel wrapped the way the reference's forward indexes it
+ * (region -1 reads the last shell / cone / wedge).  row_ptr == NULL: count pass (`counts`, int32
+ * per ray); else fill pass into (vox, len) at row_ptr.  Workspace: sphrt_trace_workspace_bytes. */
+#define SPHRT_TRACE_F32 1
+#define SPHRT_TRACE_INVALID 2
+int sphrt_trace_reference(const sphrt_plan *plan, const sphrt_rays *rays, int flags,
+                          int32_t *counts, const int64_t *row_ptr, int32_t *vox, double *len,
+                          void *workspace, size_t workspace_size, void *stream);
 
 /* One-pass trace (the same CSR as count + fill, tracing every ray once instead of twice):
  *  1. sphrt_trace_bound: screens the rays and writes an upper bound of every ray's segment count

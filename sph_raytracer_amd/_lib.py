@@ -64,6 +64,9 @@ _SIGNATURES = [
     ('sphrt_last_error', ctypes.c_char_p, []),
     ('sphrt_version', ctypes.c_char_p, []),
     ('sphrt_solve', c_int, [c_vp, ctypes.POINTER(RayBatch), c_int, c_vp, c_vp, c_vp, c_vp]),
+    ('sphrt_solve_f32', c_int, [c_vp, ctypes.POINTER(RayBatch), c_int, c_vp, c_vp, c_vp, c_vp]),
+    ('sphrt_trace_reference', c_int, [c_vp, ctypes.POINTER(RayBatch), c_int, c_vp, c_vp, c_vp,
+                                      c_vp, c_vp, ctypes.c_size_t, c_vp]),
     ('sphrt_trace_workspace_bytes', ctypes.c_size_t, [c_vp, c_i64]),
     ('sphrt_trace_count', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_vp, ctypes.c_size_t,
                                   c_vp]),
@@ -110,6 +113,7 @@ _SIGNATURES = [
                                           c_i64, c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
 ]
 EXPORTED = [s[0] for s in _SIGNATURES]
+TRACE_F32, TRACE_INVALID = 1, 2        # sphrt_trace_reference flags (sphrt.h)
 
 _lib = None
 

@@ -19,7 +19,7 @@ CSRC = os.path.join(HERE, 'csrc')
 OUT = os.path.join(HERE, 'lib', 'libsphrt.so')
 FAST_OUT = os.path.join(HERE, 'lib', '_sphrt_fast.so')   # CPython entry for steady-state calls
 SOURCES = ['api.hip', 'trace.hip', 'apply.hip', 'transpose.hip', 'rays.hip', 'loss.hip']
-HEADERS = ['common.hpp', 'solve.hpp', 'introsort.hpp', 'stage.hpp', 'walk.hpp']
+HEADERS = ['common.hpp', 'solve.hpp', 'introsort.hpp', 'stage.hpp']
 ARCH = os.environ.get('SPHRT_ARCH', 'gfx950')
 
 

@@ -594,10 +594,8 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
             val[i] = (uint16_t)((p << 3) | ((x >> 31) << 2) | (v & 3u));
         }
     }
-#ifndef SPHRT_TAB_ABL_SORT   // ablation build only (wrong tables): the sort's share of the kernel
     if constexpr (TM != kTabCount) typename RT::Sort().sort(key, val, ts, 0, key_bits);  // blocked:
     else typename RT::Sort().sort(key, ts, 0, key_bits);         // thread t: [ITEMS t, ITEMS t + ITEMS)
-#endif
     last_key[tid] = key[ITEMS - 1];
     __syncthreads();
     uint32_t prev = tid > 0 ? last_key[tid - 1] : 0xffffffffu;
@@ -639,156 +637,25 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
     }
 }
 
-// The same table with the duplicates removed before the sort (blocks of <= 2048 segments): a
-// block's ~1800 segments touch only ~650 distinct granules (C3; at most 1088), so the granules
-// go into an LDS hash set first (open addressing, kHashSlots keys, compare-and-swap insert; a
-// thread's consecutive segments of one granule insert once), the distinct ones are compacted
-// and only they are radix-sorted (4 keys per thread up to 1024 of them, else 8), their sorted
-// positions are written over their hash slots, and every segment reads its rank from its slot.
-// Same tables and loc as radix_table (distinct granules ascending; a segment's rank is its
-// granule's position), whatever order the inserts race in.  Opt-in (table_hash_on): slower at C3.
-constexpr int kHashSlots = 4096;                 // >= 2 x the 2048 segments: load factor <= 1/2
-template <int ITEMS>
-using HashSort = rocprim::block_radix_sort<uint32_t, kThreads, ITEMS, uint16_t, 1, 1,
-                                           SPHRT_RADIX_BITS>;
-struct HashUniq {                                // distinct granules, compacted
-    uint32_t key[kPass];
-    uint16_t slot[kPass];
-};
-constexpr size_t kHashTail =
-    sizeof(HashUniq) > sizeof(typename HashSort<8>::storage_type)
-        ? (sizeof(HashUniq) > sizeof(typename HashSort<4>::storage_type)
-               ? sizeof(HashUniq) : sizeof(typename HashSort<4>::storage_type))
-        : sizeof(typename HashSort<8>::storage_type);
-constexpr size_t kHashLds = kHashSlots * 4 + kHashTail;
-
-template <int ITEMS, typename TabT>
-__device__ __forceinline__ void hash_sort_rank(int n_tab, uint32_t* hs, HashUniq& u,
-                                               unsigned char* sort_raw, TabT* __restrict__ tab_b,
-                                               int key_bits) {
-    const int tid = threadIdx.x;
-    uint32_t key[ITEMS];
-    uint16_t val[ITEMS];
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const int q = tid * ITEMS + i;
-        key[i] = q < n_tab ? u.key[q] : 0xffffffffu;   // padding sorts last
-        val[i] = q < n_tab ? u.slot[q] : (uint16_t)0;
-    }
-    __syncthreads();                                     // the sort storage aliases u
-    auto& ts = *reinterpret_cast<typename HashSort<ITEMS>::storage_type*>(sort_raw);
-    HashSort<ITEMS>().sort(key, val, ts, 0, key_bits);   // blocked: thread t, [ITEMS t, +ITEMS)
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const int q = tid * ITEMS + i;
-        if (q < n_tab) {
-            tab_b[q] = (TabT)key[i];
-            hs[val[i]] = (uint32_t)q;                    // the slot now holds the rank
-        }
-    }
-}
-
-template <int TM, typename TabT>
-__device__ __forceinline__ void hash_table(int64_t* m, const int32_t* __restrict__ vox,
-                                           uint16_t* __restrict__ loc, TabT* __restrict__ tab_b,
-                                           int64_t s0, int n, int key_bits, const StageMap& sm,
-                                           unsigned char* lds, ScanShared& sh,
-                                           unsigned long long* stats) {
-    constexpr int ITEMS = 8;
-    constexpr uint32_t kEmpty = 0xffffffffu;
-    uint32_t* hs = reinterpret_cast<uint32_t*>(lds);
-    HashUniq& u = *reinterpret_cast<HashUniq*>(lds + kHashSlots * 4);
-    const int tid = threadIdx.x;
-    for (int j = tid; j < kHashSlots; j += kThreads) hs[j] = kEmpty;
-    uint32_t x[ITEMS];
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const int p = tid * ITEMS + i;
-        x[i] = p < n ? (uint32_t)vox[s0 + p] : 0u;
-    }
-    __syncthreads();
-    uint16_t slot[ITEMS];
-    uint32_t owned = 0;
-    uint32_t prev_key = kEmpty;
-    uint16_t prev_slot = 0;
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const int p = tid * ITEMS + i;
-        uint32_t h = prev_slot;
-        if (p < n) {
-            const uint32_t key = stage_col(x[i] & ~kHead, sm) >> 2;
-            if (key != prev_key) {
-                h = (key * 0x9e3779b1u) >> 20;           // 12-bit multiplicative hash
-                for (;;) {
-                    const uint32_t old = atomicCAS(&hs[h], kEmpty, key);
-                    if (old == kEmpty) { owned |= 1u << i; break; }
-                    if (old == key) break;
-                    h = (h + 1) & (kHashSlots - 1);
-                }
-                prev_key = key;
-            }
-        }
-        slot[i] = prev_slot = (uint16_t)h;
-    }
-    __syncthreads();
-    int n_tab;
-    int base = block_excl_count(__builtin_popcount(owned), n_tab, sh);
-    if (TM != kTabFill) {
-        if (tid == 0) {
-            if (n_tab > kMaxGran) {
-                m[5] = -1;
-                atomicAdd(stats, 1ull);
-            } else {
-                m[5] = n_tab;
-                atomic_max_sparse(stats + 1, (unsigned long long)n_tab);
-            }
-        }
-        if (TM == kTabCount || n_tab > kMaxGran) return;
-    }
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        if (owned & (1u << i)) {
-            u.key[base] = hs[slot[i]];
-            u.slot[base] = slot[i];
-            ++base;
-        }
-    }
-    __syncthreads();
-    unsigned char* sort_raw = lds + kHashSlots * 4;
-    if (n_tab <= 4 * kThreads) hash_sort_rank<4>(n_tab, hs, u, sort_raw, tab_b, key_bits);
-    else hash_sort_rank<8>(n_tab, hs, u, sort_raw, tab_b, key_bits);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < ITEMS; ++i) {
-        const int p = tid * ITEMS + i;
-        if (p < n) {
-            const uint32_t v = stage_col(x[i] & ~kHead, sm);
-            loc[s0 + p] = loc_code((int)hs[slot[i]], v, (x[i] & kHead) != 0);
-        }
-    }
-}
-
 // Blocks of up to 2048 segments (most: a block owns the rows starting in 1792 segments) sort 8
-// keys per thread (or only their distinct granules: hash_table), larger ones 16: half the sort
-// work for the common case.
-// (HASH: the hash-set variant, its own instantiation so that its LDS does not cost the default
-// kernel occupancy.)  Blocks of more than 2048 segments (the last row's overhang; few) are left
+// keys per thread, larger ones 16: half the sort work for the common case.  (An LDS hash set
+// that deduplicated the granules before a smaller sort measured slower at C3, 1268 -> 1503 us,
+// and was removed in round 4.)  Blocks of more than 2048 segments (the last row's overhang; few) are left
 // to local_table_big_kernel: apart, this kernel is sized for the 8-key sort's registers (72
 // VGPRs, 7 waves per SIMD instead of 4 with the 16-key sort inline: C3 1244 -> 1120 us).
 #ifndef SPHRT_TAB_WAVES
 #define SPHRT_TAB_WAVES 7   // minimum waves per SIMD the 8-key table kernel's registers aim for
 #endif
-template <int TM, typename TabT, bool HASH, int ITEMS>
+template <int TM, typename TabT, int ITEMS>
 constexpr size_t table_lds() {
-    constexpr size_t r = sizeof(typename RadixTable<ITEMS, TM>::Storage);
-    return HASH && kHashLds > r ? kHashLds : r;
+    return sizeof(typename RadixTable<ITEMS, TM>::Storage);
 }
-template <int TM, typename TabT = int32_t, bool HASH = false>
+template <int TM, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
     unsigned long long* stats) {
-    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, HASH, 8>()];
+    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, 8>()];
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
     int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
@@ -804,11 +671,8 @@ __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_k
     }
     if (n > 8 * kThreads) return;                 // local_table_big_kernel's
     TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
-    if constexpr (HASH)
-        hash_table<TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, sh, stats);
-    else
-        radix_table<8, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key,
-                                 sh, stats);
+    radix_table<8, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key, sh,
+                             stats);
 }
 
 // The blocks of 2049..kLocalMax segments: workgroup g looks at blocks [kBigScan g, kBigScan g +
@@ -821,7 +685,7 @@ __global__ __launch_bounds__(kThreads) void local_table_big_kernel(
     int64_t* __restrict__ blocks, int64_t n_blocks, const int32_t* __restrict__ vox,
     uint16_t* __restrict__ loc, TabT* __restrict__ tab, int64_t tab_stride, int key_bits,
     StageMap sm, unsigned long long* stats) {
-    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, false, 16>()];
+    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, 16>()];
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
     __shared__ int n_big;
@@ -884,23 +748,14 @@ __device__ __forceinline__ T lds_at(const T* dens, uint32_t x) {
 
 // One DMA lane: granule g (its index in the channel; the byte offset is 32-bit: volumes under
 // 4 GiB per channel), into the round whose first table entry is e0.
-// SPHRT_FWD_ABL_GRAN=m (diagnostic builds only, wrong results): granule indices masked with m, so
-// the DMA reads a volume of (m+1) granules — the forward without density misses.
 template <typename T>
 __device__ __forceinline__ void stage_one(const T* __restrict__ rho, int32_t g, int e0, int lane,
                                           T* dens) {
     constexpr int G = kGranLanes<T>;
-#ifdef SPHRT_FWD_ABL_GRAN
-    g &= SPHRT_FWD_ABL_GRAN;
-#endif
     const char* src = reinterpret_cast<const char*>(rho) + (uint32_t)g * (16u * G) +
                       16 * (lane % G);
-#ifndef SPHRT_FWD_ABL_NODMA      // diagnostic builds only: no granule DMA (wrong results)
     __builtin_amdgcn_global_load_lds((const void*)src,
         (__attribute__((address_space(3))) void*)(dens + 4 * (e0 + 1)), 16, 0, 0);
-#else
-    (void)src;
-#endif
 }
 
 // The volume's last granule, if partial (voxel count not a multiple of 4), can only be the
@@ -1226,21 +1081,12 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     // Empty rays integrate to zero: this workgroup's share of the list is fetched now and
     // written at the very end, off the critical path.
     const int64_t e_lo = m[0];
-#ifdef SPHRT_FWD_ABL_EMPTY
-    const int e_n = 0;
-#else
     const int e_n = (fallback_only || RUNS) ? 0 : (int)(m[1] - e_lo);
-#endif
     // (unconditional load: empty_ray holds n_rays + 1 entries; a predicated load would make
     // the wait-count model drain every load before the granule DMA)
-#ifdef SPHRT_FWD_ABL_EMPTY   // diagnostic builds only: no empty-ray zeroing (wrong results)
-    constexpr int kEmptyLoads = 0;
-    int32_t r_empty = 0;
-#else
     constexpr int kEmptyLoads = RUNS ? 0 : 1;
     int32_t r_empty = 0;
     if constexpr (!RUNS) r_empty = empty_ray[e_lo + min(tid, max(e_n - 1, 0))];
-#endif
     auto zero_empty = [&]() {
         if constexpr (RUNS) {      // empty j of the share -> its ray through the ranges
             const int ne = __builtin_amdgcn_readlane(rrec, 1);
@@ -1372,11 +1218,6 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
                 return r;
             };
             int32_t r_prev, r_first, r_second;
-#ifdef SPHRT_FWD_ABL_ROWS    // diagnostic builds only: rows' rays without loads (wrong results)
-            r_prev = (int32_t)imax64(ri - 1, 0);
-            r_first = (int32_t)imin64(ri, n_rays - 1);
-            r_second = (int32_t)imin64(ri + 1, n_rays - 1);
-#else
             if constexpr (RUNS) {
                 const int32_t r0 = __builtin_amdgcn_readlane(rrec, 3);
                 r_prev = r0 + qb - 1;
@@ -1395,7 +1236,6 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
                 r_first = row_ray[imin64(ri, n_rays - 1)];
                 r_second = row_ray[imin64(ri + 1, n_rays - 1)];
             }
-#endif
             auto row_of = [&](int i) -> int64_t {     // ray of the row after i own heads
                 if constexpr (RUNS) return i < 0 ? r_prev : i == 0 ? r_first : ray_of_row(qb + i);
                 return i < 0 ? r_prev : i == 0 ? r_first : rows[i];
@@ -1469,14 +1309,8 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             }
             bool tot_has;
             Stitch tot_sum;
-#ifdef SPHRT_FWD_ABL_SEGSCAN   // diagnostic builds only: no segmented scan (wrong results)
-            const double ex = 0.0;
-            tot_has = true;
-            tot_sum = (Stitch)tail;
-#else
             const Stitch ex = block_excl_segsum1<W, Stitch>(hmask != 0, (Stitch)tail, tot_has, tot_sum,
                                                  sh.has[par], sh.sum[par]);
-#endif
             par ^= 1;
             FWD_STAMP(4);
             // the run open at this thread's start: the segmented prefix of the earlier threads,
@@ -1660,27 +1494,12 @@ static int granule_key_bits(int64_t n_cols) {
     return b;
 }
 
-// Granule tables of blocks of <= 2048 segments from the sort of every segment (radix_table), or
-// with SPHRT_TABLE_SORT=hash from the hash-deduplicated sort (hash_table).  Same tables.  The
-// hash set measured slower at C3 (local_table_radix_kernel 1268 -> 1503 us: the compare-and-swap
-// inserts and twice the LDS cost more than the smaller sort saves; C4's Operator 1.70 -> 1.66 ms,
-// within box spread), so it is opt-in.
-static int table_hash_on() {
-    const char* e = getenv("SPHRT_TABLE_SORT");
-    return e && e[0] == 'h';
-}
-
-template <int TM, typename TabT>
-static auto pick_table_kernel(bool hash) {
-    return hash ? local_table_radix_kernel<TM, TabT, true> : local_table_radix_kernel<TM, TabT, false>;
-}
-
 // The table kernel's two launches (blocks of <= 2048 segments, then the larger ones).
 template <int TM, typename TabT>
-static int launch_tables(bool hash, unsigned nb, hipStream_t st, int64_t* blocks,
-                         const int32_t* vox, uint16_t* loc, TabT* tab, int64_t stride, int kb,
-                         const StageMap& sm, unsigned long long* stats) {
-    hipLaunchKernelGGL((pick_table_kernel<TM, TabT>(hash)), dim3(nb), dim3(kThreads), 0, st,
+static int launch_tables(unsigned nb, hipStream_t st, int64_t* blocks, const int32_t* vox,
+                         uint16_t* loc, TabT* tab, int64_t stride, int kb, const StageMap& sm,
+                         unsigned long long* stats) {
+    hipLaunchKernelGGL((local_table_radix_kernel<TM, TabT>), dim3(nb), dim3(kThreads), 0, st,
                        blocks, vox, loc, tab, stride, kb, sm, stats);
     hipLaunchKernelGGL((local_table_big_kernel<TM, TabT>), dim3((nb + kBigScan - 1) / kBigScan),
                        dim3(kThreads), 0, st, blocks, (int64_t)nb, vox, loc, tab, stride, kb, sm,
@@ -1706,7 +1525,7 @@ extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_
                            0, words, sm, (unsigned long long*)stats);
         return check_launch("local_table_bitmap_kernel<count>");
     }
-    return launch_tables<kTabCount, int32_t>(table_hash_on(), (unsigned)c->n_blocks, st, blocks,
+    return launch_tables<kTabCount, int32_t>((unsigned)c->n_blocks, st, blocks,
                                              c->vox, nullptr, nullptr, 0, granule_key_bits(cols),
                                              sm, (unsigned long long*)stats);
 }
@@ -1737,12 +1556,11 @@ extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, u
         return check_launch("local_table_bitmap_kernel<fill>");
     }
     const int kb = granule_key_bits(cols);
-    const bool hash = table_hash_on();
     const unsigned nb = (unsigned)c->n_blocks;
     if (u16)
-        return launch_tables<kTabFill, uint16_t>(hash, nb, st, (int64_t*)blocks, c->vox, loc,
+        return launch_tables<kTabFill, uint16_t>(nb, st, (int64_t*)blocks, c->vox, loc,
                                                  (uint16_t*)tab, tab_stride, kb, sm, nullptr);
-    return launch_tables<kTabFill, int32_t>(hash, nb, st, (int64_t*)blocks, c->vox, loc,
+    return launch_tables<kTabFill, int32_t>(nb, st, (int64_t*)blocks, c->vox, loc,
                                             (int32_t*)tab, tab_stride, kb, sm, nullptr);
 }
 
@@ -1774,11 +1592,10 @@ extern "C" int sphrt_csr_local_build(const sphrt_csr* c, int64_t* blocks, uint16
         return check_launch("local_table_bitmap_kernel<build>");
     }
     const int kb = granule_key_bits(cols);
-    const bool hash = table_hash_on();
     if (u16)
-        return launch_tables<kTabBuild, uint16_t>(hash, g.x, st, blocks, c->vox, loc,
+        return launch_tables<kTabBuild, uint16_t>(g.x, st, blocks, c->vox, loc,
                                                   (uint16_t*)tab_wide, kTabWide, kb, sm, s);
-    return launch_tables<kTabBuild, int32_t>(hash, g.x, st, blocks, c->vox, loc,
+    return launch_tables<kTabBuild, int32_t>(g.x, st, blocks, c->vox, loc,
                                              (int32_t*)tab_wide, kTabWide, kb, sm, s);
 }
 

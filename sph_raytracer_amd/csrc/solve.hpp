@@ -1,4 +1,6 @@
-// solve.hpp — per-ray boundary-crossing solves on gfx950, FP64.
+// solve.hpp — per-ray boundary-crossing solves on gfx950, in the trace's precision F: FP64 (the
+// reference default and every fast path) or FP32 (Operator(..., ftype=torch.float32): the same
+// expressions evaluated in float, as torch runs them on float32 tensors).
 //
 // Restates the arithmetic of the reference's materialised torch solvers one crossing at a time, in
 // registers.  Every expression keeps the reference's operation order; this translation unit is
@@ -40,40 +42,53 @@ struct GridDev {
     }
 };
 
-// Everything a crossing solve needs about one ray.
-struct RayGeo {
-    double x0, x1, x2;     // start point
-    double u0, u1, u2;     // direction normalised once here (r_torch, raytracer.py:281)
-    double w0, w1, w2;     // normalised again (e_torch, raytracer.py:365; a_torch reuses it)
-    double tc;             // dot(-x, u)                       (raytracer.py:288)
-    double dd;             // sqrt(|x|^2 - tc^2)               (raytracer.py:289)
-    double nx2;            // linalg.norm(x)**2                (raytracer.py:375)
-    double wx;             // dot(w, x)                        (raytracer.py:374)
+// Everything a crossing solve needs about one ray, in the trace's precision F.
+template <typename F>
+struct RayGeoT {
+    F x0, x1, x2;     // start point
+    F u0, u1, u2;     // direction normalised once here (r_torch, raytracer.py:281)
+    F w0, w1, w2;     // normalised again (e_torch, raytracer.py:365; a_torch reuses it)
+    F tc;             // dot(-x, u)                       (raytracer.py:288)
+    F dd;             // sqrt(|x|^2 - tc^2)               (raytracer.py:289)
+    F nx2;            // linalg.norm(x)**2                (raytracer.py:375)
+    F wx;             // dot(w, x)                        (raytracer.py:374)
 };
+using RayGeo = RayGeoT<double>;
+
+// Correctly rounded square root and single-rounding fused multiply-add in either precision
+// (float: HIP's default correctly rounded sqrtf, as IEEE; torch CPU's float32 sqrt agrees with it
+// on all but ~2e-5 of the crossings the f32 fixtures hold, by one ulp).
+__device__ __forceinline__ double sq_rt(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ float sq_rt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float fmad(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fabs_(double x) { return __builtin_fabs(x); }
+__device__ __forceinline__ float fabs_(float x) { return __builtin_fabsf(x); }
 
 // torch.linalg.norm over the last axis of length 3: fused sum of squares, IEEE sqrt.
-__device__ __forceinline__ double vnorm(double a, double b, double c) {
-    return __builtin_sqrt(__builtin_fma(c, c, __builtin_fma(b, b, a * a)));
+template <typename F>
+__device__ __forceinline__ F vnorm(F a, F b, F c) {
+    return sq_rt(fmad(c, c, fmad(b, b, a * a)));
 }
 // einsum '...j,...j->...' / '...c,...bc->...b': sequential, unfused.
-__device__ __forceinline__ double dot_seq(double a0, double a1, double a2,
-                                          double b0, double b1, double b2) {
-    double s = a0 * b0 + a1 * b1;
+template <typename F>
+__device__ __forceinline__ F dot_seq(F a0, F a1, F a2, F b0, F b1, F b2) {
+    F s = a0 * b0 + a1 * b1;
     return s + a2 * b2;
 }
 
-__device__ __forceinline__ RayGeo make_ray(double x0, double x1, double x2,
-                                           double d0, double d1, double d2) {
-    RayGeo g;
+template <typename F>
+__device__ __forceinline__ RayGeoT<F> make_ray(F x0, F x1, F x2, F d0, F d1, F d2) {
+    RayGeoT<F> g;
     g.x0 = x0; g.x1 = x1; g.x2 = x2;
-    double n1 = vnorm(d0, d1, d2);
+    F n1 = vnorm(d0, d1, d2);
     g.u0 = d0 / n1; g.u1 = d1 / n1; g.u2 = d2 / n1;
-    double n2 = vnorm(g.u0, g.u1, g.u2);
+    F n2 = vnorm(g.u0, g.u1, g.u2);
     g.w0 = g.u0 / n2; g.w1 = g.u1 / n2; g.w2 = g.u2 / n2;
     g.tc = dot_seq(-x0, -x1, -x2, g.u0, g.u1, g.u2);
-    double xx = dot_seq(x0, x1, x2, x0, x1, x2);
-    g.dd = __builtin_sqrt(xx - g.tc * g.tc);
-    double nx = vnorm(x0, x1, x2);
+    F xx = dot_seq(x0, x1, x2, x0, x1, x2);
+    g.dd = sq_rt(xx - g.tc * g.tc);
+    F nx = vnorm(x0, x1, x2);
     g.nx2 = nx * nx;
     g.wx = dot_seq(g.w0, g.w1, g.w2, x0, x1, x2);
     return g;
@@ -82,9 +97,10 @@ __device__ __forceinline__ RayGeo make_ray(double x0, double x1, double x2,
 // The per-family API: called on their own, e_torch normalises its input once
 // (raytracer.py:365) and a_torch not at all (raytracer.py:471-552), so the cone/plane direction
 // is u resp. the raw input, not the twice-normalised w that trace_indices hands them.
-__device__ __forceinline__ RayGeo make_ray_family(double x0, double x1, double x2, double d0,
-                                                  double d1, double d2, int family) {
-    RayGeo g = make_ray(x0, x1, x2, d0, d1, d2);
+template <typename F>
+__device__ __forceinline__ RayGeoT<F> make_ray_family(F x0, F x1, F x2, F d0, F d1, F d2,
+                                                      int family) {
+    RayGeoT<F> g = make_ray(x0, x1, x2, d0, d1, d2);
     if (family == 1) {
         g.w0 = g.u0; g.w1 = g.u1; g.w2 = g.u2;
     } else if (family == 2) {
@@ -96,28 +112,28 @@ __device__ __forceinline__ RayGeo make_ray_family(double x0, double x1, double x
 
 // ---- spheres (r_torch, raytracer.py:288-323) ------------------------------------------------
 // Region entered at distance t on sphere j: j - [u . p(t) < 0], j == nr -> -1 (outside).
-__device__ __forceinline__ int sphere_region(const RayGeo& g, double t, int j, int nr,
-                                             int& neg) {
-    double p0 = g.u0 * t + g.x0;
-    double p1 = g.u1 * t + g.x1;
-    double p2 = g.u2 * t + g.x2;
-    neg = dot_seq(g.u0, g.u1, g.u2, p0, p1, p2) < 0.0 ? 1 : 0;
+template <typename F>
+__device__ __forceinline__ int sphere_region(const RayGeoT<F>& g, F t, int j, int nr, int& neg) {
+    F p0 = g.u0 * t + g.x0;
+    F p1 = g.u1 * t + g.x1;
+    F p2 = g.u2 * t + g.x2;
+    neg = dot_seq(g.u0, g.u1, g.u2, p0, p1, p2) < F(0) ? 1 : 0;
     int reg = j - neg;
     return reg == nr ? -1 : reg;
 }
 // Both crossings of sphere j.  NaN distances (no crossing) become +inf.
-__device__ __forceinline__ void sphere_solve(const GridDev& G, const RayGeo& g, int j,
-                                             double& t_in, int& reg_in,
-                                             double& t_out, int& reg_out,
+template <typename F>
+__device__ __forceinline__ void sphere_solve(const GridDev& G, const RayGeoT<F>& g, int j,
+                                             F& t_in, int& reg_in, F& t_out, int& reg_out,
                                              int& neg_in, int& neg_out) {
-    double R = G.r_b[j];
-    double t1c = __builtin_sqrt(R * R - g.dd * g.dd);
+    F R = (F)G.r_b[j];
+    F t1c = sq_rt(R * R - g.dd * g.dd);
     t_in = g.tc - t1c;
     t_out = g.tc + t1c;
     reg_in = sphere_region(g, t_in, j, G.nr, neg_in);
     reg_out = sphere_region(g, t_out, j, G.nr, neg_out);
-    if (__builtin_isnan(t_in)) t_in = kInf;
-    if (__builtin_isnan(t_out)) t_out = kInf;
+    if (__builtin_isnan(t_in)) t_in = (F)kInf;
+    if (__builtin_isnan(t_out)) t_out = (F)kInf;
 }
 
 // False exactly when sphere_solve(j) yields no finite distance: R*R - dd*dd < 0 (or NaN) makes
@@ -128,120 +144,117 @@ __device__ __forceinline__ bool sphere_may_cross(const GridDev& G, const RayGeo&
 }
 
 // ---- cones (e_torch, raytracer.py:373-466) --------------------------------------------------
-// False exactly when cone_solve(j) yields two +inf roots through a NaN square root: the
-// (snapped) discriminant is negative or NaN and the ray is not parallel to a generator (the only
-// override that makes a root finite).  The coefficients repeat cone_solve's operations.
-__device__ __forceinline__ bool cone_may_cross(const GridDev& G, const RayGeo& g, int j) {
-    const double th = G.close_tol;
-    const double c2 = G.c2_e()[j];
-    double aa = g.w2 * g.w2 - c2;
-    const double bb = 2.0 * (g.w2 * g.x2 - g.wx * c2);
-    const double cc = g.x2 * g.x2 - g.nx2 * c2;
-    if (__builtin_fabs(aa) < th) aa = 0.0;
-    double delta = bb * bb - (4.0 * aa) * cc;
-    if (__builtin_fabs(delta) < th) delta = 0.0;
-    const bool parallel = __builtin_fabs(aa) < th && !(__builtin_fabs(bb) < th);
-    return delta >= 0.0 || parallel;
-}
 // The distance part of cone_root: +inf for a root on the opposite (shadow) nappe or NaN.
-__device__ __forceinline__ double cone_root_t(const GridDev& G, const RayGeo& g, int j, double t) {
-    const double p2 = g.w2 * t + g.x2;
+template <typename F>
+__device__ __forceinline__ F cone_root_t(const GridDev& G, const RayGeoT<F>& g, int j, F t) {
+    const F p2 = g.w2 * t + g.x2;
     const uint8_t f = G.e_flags()[j];
     const bool cone_up = (f & 1) != 0;
     const bool exempt = (f & 2) != 0;
-    if (((p2 >= 0.0) != cone_up) && !exempt) t = kInf;   // opposite (shadow) nappe
-    if (__builtin_isnan(t)) t = kInf;
+    if (((p2 >= F(0)) != cone_up) && !exempt) t = (F)kInf;   // opposite (shadow) nappe
+    if (__builtin_isnan(t)) t = (F)kInf;
     return t;
 }
 // Distance/region fix-up of one root t of cone j (region -2 = glancing, keep current region).
-__device__ __forceinline__ void cone_root(const GridDev& G, const RayGeo& g, int j,
-                                          double& t, int& reg, int& neg) {
-    double p0 = g.w0 * t + g.x0;
-    double p1 = g.w1 * t + g.x1;
-    double p2 = g.w2 * t + g.x2;
+template <typename F>
+__device__ __forceinline__ void cone_root(const GridDev& G, const RayGeoT<F>& g, int j, F& t,
+                                          int& reg, int& neg) {
+    F p0 = g.w0 * t + g.x0;
+    F p1 = g.w1 * t + g.x1;
+    F p2 = g.w2 * t + g.x2;
     // torch.cross(p, (-p1, p0, 0)) with torch CPU's fused pattern
-    double n0 = __builtin_fma(p1, 0.0, -(p2 * p0));
-    double n1 = __builtin_fma(p2, -p1, -(p0 * 0.0));
-    double n2 = __builtin_fma(p0, p0, -(p1 * (-p1)));
-    double prod = dot_seq(g.w0, g.w1, g.w2, n0, n1, n2);
-    neg = prod > 0.0 ? 1 : 0;
+    const F z = F(0);
+    F n0 = fmad(p1, z, -(p2 * p0));
+    F n1 = fmad(p2, -p1, -(p0 * z));
+    F n2 = fmad(p0, p0, -(p1 * (-p1)));
+    F prod = dot_seq(g.w0, g.w1, g.w2, n0, n1, n2);
+    neg = prod > z ? 1 : 0;
     int r = j - neg;
-    if (__builtin_fabs(prod) < G.close_tol) r = -2;
+    if (fabs_(prod) < (F)G.close_tol) r = -2;
     if (r == G.ne) r = -1;
     t = cone_root_t(G, g, j, t);
     reg = r;
 }
-// Cone j's quadratic coefficients with the reference's snapping (|a|, |delta| < close_tol -> 0).
-struct ConeQuad {
-    double aa, bb, cc, delta;
+// Cone j's quadratic coefficients with the reference's snapping (|a|, |delta| < close_tol -> 0;
+// the comparison in F, as torch compares a tensor with a Python float in the tensor's dtype).
+template <typename F>
+struct ConeQuadT {
+    F aa, bb, cc, delta;
 };
-__device__ __forceinline__ ConeQuad cone_coeffs(const GridDev& G, const RayGeo& g, int j) {
-    const double th = G.close_tol;
-    const double c2 = G.c2_e()[j];
-    double aa = g.w2 * g.w2 - c2;
-    const double bb = 2.0 * (g.w2 * g.x2 - g.wx * c2);
-    const double cc = g.x2 * g.x2 - g.nx2 * c2;
-    if (__builtin_fabs(aa) < th) aa = 0.0;
-    double delta = bb * bb - (4.0 * aa) * cc;
-    if (__builtin_fabs(delta) < th) delta = 0.0;
-    return ConeQuad{aa, bb, cc, delta};
+using ConeQuad = ConeQuadT<double>;
+template <typename F>
+__device__ __forceinline__ ConeQuadT<F> cone_coeffs(const GridDev& G, const RayGeoT<F>& g, int j) {
+    const F th = (F)G.close_tol;
+    const F c2 = (F)G.c2_e()[j];
+    F aa = g.w2 * g.w2 - c2;
+    const F bb = F(2) * (g.w2 * g.x2 - g.wx * c2);
+    const F cc = g.x2 * g.x2 - g.nx2 * c2;
+    if (fabs_(aa) < th) aa = F(0);
+    F delta = bb * bb - (F(4) * aa) * cc;
+    if (fabs_(delta) < th) delta = F(0);
+    return ConeQuadT<F>{aa, bb, cc, delta};
 }
-// cone_may_cross on coefficients already computed (the trace solves a chunk from the same ones)
-__device__ __forceinline__ bool cone_q_may_cross(const GridDev& G, const ConeQuad& q) {
-    const double th = G.close_tol;
-    return q.delta >= 0.0 || (__builtin_fabs(q.aa) < th && !(__builtin_fabs(q.bb) < th));
+// False exactly when cone_solve(j) yields two +inf roots through a NaN square root: the
+// (snapped) discriminant is negative or NaN and the ray is not parallel to a generator (the only
+// override that makes a root finite).
+template <typename F>
+__device__ __forceinline__ bool cone_q_may_cross(const GridDev& G, const ConeQuadT<F>& q) {
+    const F th = (F)G.close_tol;
+    return q.delta >= F(0) || (fabs_(q.aa) < th && !(fabs_(q.bb) < th));
+}
+__device__ __forceinline__ bool cone_may_cross(const GridDev& G, const RayGeo& g, int j) {
+    return cone_q_may_cross(G, cone_coeffs(G, g, j));
 }
 // The two roots of the quadratic with the reference's overrides, before the per-root fix-up
 // (slot j "t1", slot nbe + j "t2").
-__device__ __forceinline__ void cone_roots_q(const GridDev& G, const ConeQuad& c, double& t1,
-                                             double& t2) {
-    const double th = G.close_tol;
-    const double aa = c.aa, bb = c.bb, cc = c.cc;
-    double q = __builtin_sqrt(c.delta);
-    t1 = (-bb + q) / (2.0 * aa);
-    t2 = (-bb - q) / (2.0 * aa);
-    if (__builtin_fabs(aa) < th && !(__builtin_fabs(bb) < th)) {  // ray parallel to a generator
+template <typename F>
+__device__ __forceinline__ void cone_roots_q(const GridDev& G, const ConeQuadT<F>& c, F& t1,
+                                             F& t2) {
+    const F th = (F)G.close_tol;
+    const F aa = c.aa, bb = c.bb, cc = c.cc;
+    F q = sq_rt(c.delta);
+    t1 = (-bb + q) / (F(2) * aa);
+    t2 = (-bb - q) / (F(2) * aa);
+    if (fabs_(aa) < th && !(fabs_(bb) < th)) {  // ray parallel to a generator
         t1 = (-cc) / bb;
-        t2 = kInf;
+        t2 = (F)kInf;
     }
-    if (aa == 0.0 && bb == 0.0 && cc == 0.0) {                     // ray lies on the cone
-        t1 = kInf;
-        t2 = kInf;
+    if (aa == F(0) && bb == F(0) && cc == F(0)) {   // ray lies on the cone
+        t1 = (F)kInf;
+        t2 = (F)kInf;
     }
-}
-__device__ __forceinline__ void cone_quadratic(const GridDev& G, const RayGeo& g, int j,
-                                               double& t1, double& t2) {
-    cone_roots_q(G, cone_coeffs(G, g, j), t1, t2);
 }
 // Both roots of cone j: slot j ("t1") and slot nbe + j ("t2"), from its coefficients.
-__device__ __forceinline__ void cone_solve_q(const GridDev& G, const RayGeo& g, int j,
-                                             const ConeQuad& q, double& ta, int& rega,
-                                             double& tb, int& regb, int& nega, int& negb) {
-    double t1, t2;
+template <typename F>
+__device__ __forceinline__ void cone_solve_q(const GridDev& G, const RayGeoT<F>& g, int j,
+                                             const ConeQuadT<F>& q, F& ta, int& rega, F& tb,
+                                             int& regb, int& nega, int& negb) {
+    F t1, t2;
     cone_roots_q(G, q, t1, t2);
     cone_root(G, g, j, t1, rega, nega);
     cone_root(G, g, j, t2, regb, negb);
     ta = t1;
     tb = t2;
 }
-__device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeo& g, int j,
-                                           double& ta, int& rega, double& tb, int& regb,
-                                           int& nega, int& negb) {
+template <typename F>
+__device__ __forceinline__ void cone_solve(const GridDev& G, const RayGeoT<F>& g, int j, F& ta,
+                                           int& rega, F& tb, int& regb, int& nega, int& negb) {
     cone_solve_q(G, g, j, cone_coeffs(G, g, j), ta, rega, tb, regb, nega, negb);
 }
 
 // ---- azimuth half-planes (a_torch, raytracer.py:505-550) ------------------------------------
-__device__ __forceinline__ void plane_solve(const GridDev& G, const RayGeo& g, int j,
-                                            double& t, int& reg, int& neg) {
-    double ca = G.cos_a()[j], sa = G.sin_a()[j];
-    double msa = -sa;
+template <typename F>
+__device__ __forceinline__ void plane_solve(const GridDev& G, const RayGeoT<F>& g, int j, F& t,
+                                            int& reg, int& neg) {
+    const F ca = (F)G.cos_a()[j], sa = (F)G.sin_a()[j];
+    const F msa = -sa, z = F(0);
     // einsum '...bc,...jc->...b' against plane normal (-sin, cos, 0): fused chain
-    double num = __builtin_fma(0.0, g.x2, __builtin_fma(ca, g.x1, msa * g.x0));
-    double den = __builtin_fma(0.0, g.w2, __builtin_fma(ca, g.w1, msa * g.w0));
-    double tt = (-num) / den;
-    double cz = __builtin_fma(ca, g.w1, -(sa * g.w0));   // z of cross(plane, ray)
-    if (__builtin_fabs(cz) <= G.plane_par_tol) tt = kInf;  // parallel to the plane
-    int ng = cz < 0.0 ? 1 : 0;
+    F num = fmad(z, g.x2, fmad(ca, g.x1, msa * g.x0));
+    F den = fmad(z, g.w2, fmad(ca, g.w1, msa * g.w0));
+    F tt = (-num) / den;
+    F cz = fmad(ca, g.w1, -(sa * g.w0));   // z of cross(plane, ray)
+    if (fabs_(cz) <= (F)G.plane_par_tol) tt = (F)kInf;  // parallel to the plane
+    int ng = cz < z ? 1 : 0;
     int r = j - ng;
     if (G.a_wrap) {
         r %= G.na;
@@ -249,10 +262,10 @@ __device__ __forceinline__ void plane_solve(const GridDev& G, const RayGeo& g, i
     } else if (r == G.na) {
         r = -1;
     }
-    double p0 = tt * g.w0 + g.x0;
-    double p1 = tt * g.w1 + g.x1;
-    if (__builtin_fma(sa, p1, ca * p0) < 0.0) tt = kInf;   // back half of the plane
-    if (__builtin_isnan(tt)) tt = kInf;
+    F p0 = tt * g.w0 + g.x0;
+    F p1 = tt * g.w1 + g.x1;
+    if (fmad(sa, p1, ca * p0) < z) tt = (F)kInf;   // back half of the plane
+    if (__builtin_isnan(tt)) tt = (F)kInf;
     t = tt;
     reg = r;
     neg = ng;

@@ -30,7 +30,6 @@
 #include "common.hpp"
 #include "introsort.hpp"
 #include "solve.hpp"
-#include "walk.hpp"
 
 namespace sphrt {
 
@@ -384,9 +383,6 @@ struct TraceOut {
     unsigned* n_hits;                // workspace: screened hit-ray counter
     HitRay* hits;                    // workspace: hit rays
     unsigned long long* n_over;      // EMIT: rays whose segments exceed their bound
-    unsigned* n_walk;                // workspace: walk-eligible hit-ray counter
-    int32_t* walk_rays;              // workspace: walk-eligible hit rays (walk_kernel)
-    int walk;                        // screen: send eligible rays to the walk (SPHRT_WALK != 0)
     int wedge;                       // solve only the half-planes of a line's azimuth wedge
 };
 
@@ -834,12 +830,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     wave_sync();
 
     // ---- 2. sort by (distance, candidate) ------------------------------------------------
-#if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 1
-    if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 1
-        if (lane == 0) o.counts[ray] = F;
-        return;
-    }
-#endif
     TRACE_T(ts1);
     TRACE_ADD(0, ts0, ts1);
     int sflags = 2;          // bit 0: repair the order; bit 1: look for ambiguous ties
@@ -860,12 +850,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     }
     if (sflags & 1) fix_near_ties(keys, pays, F, lane);
 
-#if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 2
-    if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 2
-        if (lane == 0) o.counts[ray] = F;
-        return;
-    }
-#endif
     TRACE_T(ts2);
     TRACE_ADD(1, ts1, ts2);
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe, start_c = G.K - 1;
@@ -880,12 +864,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     }
 
     // ---- 3. forward fill, lengths, compaction ----------------------------------------------
-#if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 3
-    if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 3
-        if (lane == 0) o.counts[ray] = F;
-        return;
-    }
-#endif
     TRACE_T(ts3);
     TRACE_ADD(2, ts2, ts3);
     // every distance behind the start is integrated in the start voxel (raytracer.py:126,140)
@@ -952,12 +930,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     }
 
     // ---- 4. emit ---------------------------------------------------------------------------
-#if defined(SPHRT_TRACE_ABL) && SPHRT_TRACE_ABL == 4
-    if (MODE == MODE_COUNT) {                   // ablation build (tools): stop after phase 4
-        if (lane == 0) o.counts[ray] = F;
-        return;
-    }
-#endif
     TRACE_T(ts4);
     TRACE_ADD(3, ts3, ts4);
     if (MODE == MODE_COUNT) {
@@ -1123,16 +1095,7 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
             for (int64_t c = 0; c < nc; ++c) o.out[c * o.out_chan_stride + ray] = (T)0;
         }
     }
-    // hits the lane walk can take go to its list (ray ids), the rest to the list trace's
-    const bool walk = hit && o.walk && walk_eligible(G, g, t1c_outer, start_r_ok);
-    const uint64_t mw = __ballot(walk);
-    if (mw != 0) {
-        unsigned wb = 0;
-        if (lane == __builtin_ctzll(mw)) wb = atomicAdd(o.n_walk, (unsigned)__popcll(mw));
-        wb = __shfl(wb, __builtin_ctzll(mw));
-        if (walk) o.walk_rays[wb + __popcll(mw & lanemask_lt(lane))] = (int32_t)ray;
-    }
-    const bool listed = hit && !walk;
+    const bool listed = hit;
     const uint64_t m = __ballot(listed);
     if (m == 0) return;
     unsigned base = 0;
@@ -1146,79 +1109,6 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
         h.ray = (int32_t)ray;
         o.hits[base + __popcll(m & lanemask_lt(lane))] = h;
     }
-}
-
-// ---- the lane walk (walk.hpp): one walk-eligible ray per lane ---------------------------------
-// Merges the four runs by (distance, candidate) and replays trace_one's rules on the merged
-// sequence: crossings before the outer sphere's entry t_lo only update the e / a rows (the start
-// lies outside, so its r row is -1 until the entry), the sequence from t_lo to the exit t_hi is
-// the list, and each segment between consecutive list entries gets the rows' values after the
-// first (trace_one steps 3-4).  A tie — exactly equal distances — of two crossings writing
-// different values into one row (the start entry at t = 0 included) defers the ray to the exact
-// kernel, like ambiguous_ties; a run out of order hands the ray to the list trace (appended to
-// its hit list, traced by trace_kernel afterwards).  Either way the later kernel rewrites the
-// ray's count and segments.  Segments are written straight to the ray's row (FILL / EMIT).
-template <int MODE, typename T>
-__device__ __forceinline__ void walk_one(const GridDev& G, const RaysDev& R, const TraceOut<T>& o,
-                                         const int64_t ray) {
-    double x[3], d[3];
-    int s[3];
-    load_ray(R, ray, x, d, s);
-    const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
-    int64_t nseg = 0;
-    int64_t base = 0, cap = INT64_MAX;
-    if (MODE == MODE_FILL || MODE == MODE_EMIT) base = o.row_ptr[ray];
-    if (MODE == MODE_EMIT) cap = o.row_ptr[ray + 1] - base;
-    const T* rho = nullptr;
-    if (MODE == MODE_INTEGRATE)
-        rho = o.density + (o.ray_chan_div > 0 ? (ray / o.ray_chan_div) * o.chan_stride : 0);
-    double acc = 0.0;
-    // 1: tie (exact kernel), 2: out of order (list trace)
-    const int status = walk_ray(G, g, s, [&](int vx, double len) {
-        if (MODE == MODE_FILL || (MODE == MODE_EMIT && nseg < cap)) {
-            o.vox[base + nseg] = vx;
-            o.len[base + nseg] = len;
-        } else if (MODE == MODE_INTEGRATE) {
-            acc += (double)rho[vx] * len;
-        }
-        ++nseg;
-    });
-    if (status == 1) {
-        const unsigned long long q = atomicAdd(o.n_deferred, 1ull);
-        o.deferred[q] = ray;
-        return;
-    }
-    if (status == 2) {
-        HitRay hr;
-        hr.g = g;
-        hr.t1c_o = __builtin_sqrt(G.r_outer * G.r_outer - g.dd * g.dd);
-        hr.s[0] = s[0]; hr.s[1] = s[1]; hr.s[2] = s[2];
-        hr.ray = (int32_t)ray;
-        o.hits[atomicAdd(o.n_hits, 1u)] = hr;
-        return;
-    }
-    if (MODE == MODE_COUNT) o.counts[ray] = (int32_t)nseg;
-    if (MODE == MODE_EMIT) (void)emit_slot(o, ray, nseg, true);
-    if (MODE == MODE_INTEGRATE) o.out[ray] = (T)acc;   // (one channel: n_chan 1 or time slices)
-}
-
-template <int MODE, typename T>
-__global__ __launch_bounds__(256) void walk_kernel(GridDev G, RaysDev R, TraceOut<T> o,
-                                                   int tab_words) {
-    // The boundary tables in LDS: every step of a lane's walk looks one up at its own index (a
-    // serial chain of lookups per lane, unlike the list trace's 64 boundaries per load), so
-    // they must not cost a global-memory round trip each.
-    extern __shared__ double wtab[];
-    const int64_t n_walk = (int64_t)*o.n_walk;
-    if ((int64_t)blockIdx.x * 256 >= n_walk) return;
-    for (int i = threadIdx.x; i < tab_words; i += 256) wtab[i] = G.r_b[i];
-    __syncthreads();
-    GridDev Gs = G;
-    Gs.r_b = wtab;
-    // one ray per lane, neighbouring lanes on neighbouring rays of the list (a grid-stride loop
-    // here costs ~50 VGPRs: 2 instead of 3 waves per SIMD)
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (idx < n_walk) walk_one<MODE, T>(Gs, R, o, o.walk_rays[idx]);
 }
 
 // Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
@@ -1256,18 +1146,22 @@ __global__ __launch_bounds__(256, SPHRT_TRACE_MIN_BLOCKS) void trace_kernel(Grid
 }
 
 // ---- per-family solves for the r_torch / e_torch / a_torch API ------------------------------
-__global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int family, double* t,
+// F: float64, or float32 for ftype=torch.float32 (inputs rounded to float as torch.asarray(...,
+// dtype=float32) does, every operation in float).
+template <typename F>
+__global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int family, F* t,
                                                     int32_t* region, int8_t* neg) {
     const int64_t ray = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (ray >= R.n) return;
     double x[3], d[3];
     int s[3];
     load_ray(R, ray, x, d, s);
-    const RayGeo g = make_ray_family(x[0], x[1], x[2], d[0], d[1], d[2], family);
+    const RayGeoT<F> g = make_ray_family<F>((F)x[0], (F)x[1], (F)x[2], (F)d[0], (F)d[1], (F)d[2],
+                                            family);
     if (family == 0) {
         const int w = 2 * G.nbr;
         for (int j = 0; j < G.nbr; ++j) {
-            double ti, to;
+            F ti, to;
             int ri, ro, ni, no;
             sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
             t[ray * w + j] = ti; region[ray * w + j] = ri; neg[ray * w + j] = (int8_t)ni;
@@ -1277,7 +1171,7 @@ __global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int fa
     } else if (family == 1) {
         const int w = 2 * G.nbe;
         for (int j = 0; j < G.nbe; ++j) {
-            double ta, tb;
+            F ta, tb;
             int ra, rb, na_, nb_;
             cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
             t[ray * w + j] = ta; region[ray * w + j] = ra; neg[ray * w + j] = (int8_t)na_;
@@ -1287,7 +1181,7 @@ __global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int fa
     } else {
         const int w = G.nba;
         for (int j = 0; j < G.nba; ++j) {
-            double tt;
+            F tt;
             int r, ng;
             plane_solve(G, g, j, tt, r, ng);
             t[ray * w + j] = tt; region[ray * w + j] = r; neg[ray * w + j] = (int8_t)ng;
@@ -1298,36 +1192,64 @@ __global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int fa
 // ---- exact path for deferred rays: one wave per ray, the reference algorithm verbatim -----
 // Candidates in the reference's concatenation order (raytracer.py:92, 117-122), solved by the
 // lanes in parallel.  Returns through `put(c, t, region)`.
-template <class Put>
-__device__ __forceinline__ void exact_candidates(const GridDev& G, const RayGeo& g, int lane,
+// F: the solves' precision (double; float for ftype=torch.float32 traces), the distances handed
+// to `put` as doubles (exact for float).
+template <typename F, class Put>
+__device__ __forceinline__ void exact_candidates(const GridDev& G, const RayGeoT<F>& g, int lane,
                                                  Put put) {
     const int nbr = G.nbr, nbe = G.nbe, nba = G.nba;
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe;
     for (int j = lane; j < nbr; j += 64) {
-        double ti, to;
+        F ti, to;
         int ri, ro, ni, no;
         sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
-        put(j, ti, ri);
-        put(nbr + j, to, ro);
+        put(j, (double)ti, ri);
+        put(nbr + j, (double)to, ro);
     }
     for (int j = lane; j < nbe; j += 64) {
-        double ta, tb;
+        F ta, tb;
         int ra, rb, na_, nb_;
         cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
-        put(r_lim + j, ta, ra);
-        put(r_lim + nbe + j, tb, rb);
+        put(r_lim + j, (double)ta, ra);
+        put(r_lim + nbe + j, (double)tb, rb);
     }
     for (int j = lane; j < nba; j += 64) {
-        double t;
+        F t;
         int r, ng;
         plane_solve(G, g, j, t, r, ng);
-        put(e_lim + j, t, r);
+        put(e_lim + j, (double)t, r);
     }
     if (lane == 0) put(G.K - 1, 0.0, 0);
 }
 
+// A sorted entry's segment under the trace's options: its length (tn - t in F: float32 traces
+// difference their float32 distances, raytracer.py:150-151 in the trace's dtype) and whether it
+// is kept; its voxel index.  Default (raytracer.py:155-173): kept when positive, finite and inside
+// the grid.  INV (Operator(..., invalid=True)): nothing is masked — every non-zero length is kept,
+// inf and NaN included, with its regions wrapped as the reference's forward reads them
+// (density[r, e, a] with r = -1 is the last shell: Python's negative indexing).
+template <typename F>
+__device__ __forceinline__ double seg_length(double tn, double t) {
+    return (double)((F)tn - (F)t);
+}
+template <bool INV>
+__device__ __forceinline__ bool seg_keep(const GridDev& G, double len, int r, int e, int a) {
+    if (INV) return len != 0.0;                // (NaN != 0: kept)
+    return len > 0.0 && __builtin_isfinite(len) && r >= 0 && r < G.nr && e >= 0 && e < G.ne &&
+           a >= 0 && a < G.na;
+}
+template <bool INV>
+__device__ __forceinline__ int seg_voxel(const GridDev& G, int r, int e, int a) {
+    if (INV) {
+        r = r < 0 ? r + G.nr : r;
+        e = e < 0 ? e + G.ne : e;
+        a = a < 0 ? a + G.na : a;
+    }
+    return (r * G.ne + e) * G.na + a;
+}
+
 // Forward fill + diff + masking over the sorted list (raytracer.py:126, 140-173), one lane.
-template <int MODE, typename T, class V>
+template <int MODE, typename T, typename F, bool INV, class V>
 __device__ void exact_walk(const GridDev& G, const TraceOut<T>& o, int64_t ray, const int* s,
                            const V& v) {
     const int K = G.K, r_lim = 2 * G.nbr, e_lim = 2 * G.nbr + 2 * G.nbe;
@@ -1357,10 +1279,9 @@ __device__ void exact_walk(const GridDev& G, const TraceOut<T>& o, int64_t ray, 
             }
             if (k + 1 < K) cur = v.get(k + 1);
             const double tn = k + 1 < K ? cur.t : kInf;
-            const double len = tn - t;
-            if (!(len > 0.0) || !__builtin_isfinite(len)) continue;
-            if (cr < 0 || cr >= G.nr || ce < 0 || ce >= G.ne || ca < 0 || ca >= G.na) continue;
-            const int vx = (cr * G.ne + ce) * G.na + ca;
+            const double len = seg_length<F>(tn, t);
+            if (!seg_keep<INV>(G, len, cr, ce, ca)) continue;
+            const int vx = seg_voxel<INV>(G, cr, ce, ca);
             if (MODE == MODE_FILL || (MODE == MODE_EMIT && nseg < cap)) {
                 o.vox[base + nseg] = vx;
                 o.len[base + nseg] = len;
@@ -1381,7 +1302,7 @@ __device__ void exact_walk(const GridDev& G, const TraceOut<T>& o, int64_t ray, 
 // The same walk, wave-parallel over 64-entry chunks of the sorted list (ts, ps): "last update
 // wins" scans for the three region rows, differences, and in-order compaction of the non-zero
 // in-grid segments into (seg_vox, seg_len) (LDS, K entries), then count / copy / integrate.
-template <int MODE, typename T>
+template <int MODE, typename T, typename F, bool INV>
 __device__ void exact_walk_wave(const GridDev& G, const TraceOut<T>& o, int64_t ray, const int* s,
                                 const double* ts, const uint32_t* ps, int32_t* seg_vox,
                                 double* seg_len, int lane) {
@@ -1417,14 +1338,13 @@ __device__ void exact_walk_wave(const GridDev& G, const TraceOut<T>& o, int64_t 
         cr = __builtin_amdgcn_readlane(ur, 63);
         ce = __builtin_amdgcn_readlane(ue, 63);
         ca = __builtin_amdgcn_readlane(ua, 63);
-        const double len = tn - t;
-        const bool ok = real && len > 0.0 && __builtin_isfinite(len) && ur >= 0 && ur < G.nr &&
-                        ue >= 0 && ue < G.ne && ua >= 0 && ua < G.na;
+        const double len = seg_length<F>(tn, t);
+        const bool ok = real && seg_keep<INV>(G, len, ur, ue, ua);
         const uint64_t m = __ballot(ok);
         if (MODE != MODE_COUNT && ok) {
             const int pos = nseg + __popcll(m & lanemask_lt(lane));
             seg_len[pos] = len;
-            seg_vox[pos] = (ur * G.ne + ue) * G.na + ua;
+            seg_vox[pos] = seg_voxel<INV>(G, ur, ue, ua);
         }
         nseg += __popcll(m);
     }
@@ -1456,25 +1376,39 @@ __device__ void exact_walk_wave(const GridDev& G, const TraceOut<T>& o, int64_t 
 
 // Large K (the wave list does not fit kExactLdsMax): lane 0 sorts the ray's list serially in the
 // wave's slice of workspace.
-template <int MODE, typename T>
+// ALL: every ray of R (the reference-mode trace, sphrt_trace_reference), not the deferred list.
+template <bool ALL, typename T>
+__device__ __forceinline__ int64_t exact_count(const RaysDev& R, const TraceOut<T>& o) {
+    return ALL ? R.n : (int64_t)*o.n_deferred;
+}
+template <bool ALL, typename T>
+__device__ __forceinline__ int64_t exact_ray(const TraceOut<T>& o, int64_t q) {
+    return ALL ? q : o.deferred[q];
+}
+template <typename F>
+__device__ __forceinline__ RayGeoT<F> exact_geo(const double* x, const double* d) {
+    return make_ray<F>((F)x[0], (F)x[1], (F)x[2], (F)d[0], (F)d[1], (F)d[2]);
+}
+
+template <int MODE, typename T, typename F = double, bool INV = false, bool ALL = false>
 __global__ __launch_bounds__(64) void exact_kernel(GridDev G, RaysDev R, TraceOut<T> o,
                                                    Cand* scratch) {
     const int lane = threadIdx.x;
     const CandList v{scratch + (int64_t)blockIdx.x * G.K};
-    const int64_t count = (int64_t)*o.n_deferred;
+    const int64_t count = exact_count<ALL>(R, o);
     for (int64_t q = blockIdx.x; q < count; q += gridDim.x) {
-        const int64_t ray = o.deferred[q];
+        const int64_t ray = exact_ray<ALL>(o, q);
         double x[3], d[3];
         int s[3];
         load_ray(R, ray, x, d, s);
-        const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
+        const RayGeoT<F> g = exact_geo<F>(x, d);
         exact_candidates(G, g, lane, [&](int c, double t, int reg) {
             v.set(c, Cand{t, ((uint32_t)c << 16) | (uint32_t)(reg + 2), 0u});
         });
         __syncthreads();
         if (lane == 0) {
             introsort(v, G.K);
-            exact_walk<MODE, T>(G, o, ray, s, v);
+            exact_walk<MODE, T, F, INV>(G, o, ray, s, v);
         }
         __syncthreads();
     }
@@ -1499,7 +1433,7 @@ __host__ __device__ constexpr size_t exact_wave_lds(int K) {
     return (size_t)K * kExactWaveEntryBytes + 3 * kExactStack * sizeof(int);
 }
 
-template <int MODE, typename T>
+template <int MODE, typename T, typename F = double, bool INV = false, bool ALL = false>
 __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
     extern __shared__ __attribute__((aligned(16))) unsigned char xw_lds[];
     const int K = G.K;
@@ -1518,14 +1452,14 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
     const SoaList v{tk, pk};
     const int lane = threadIdx.x;
     const uint64_t below = lanemask_lt(lane);
-    const int64_t count = (int64_t)*o.n_deferred;
+    const int64_t count = exact_count<ALL>(R, o);
     for (int64_t q = blockIdx.x; q < count; q += gridDim.x) {
-        const int64_t ray = o.deferred[q];
+        const int64_t ray = exact_ray<ALL>(o, q);
         double x[3], d[3];
         int s[3];
         load_ray(R, ray, x, d, s);
         TRACE_T(x0);
-        const RayGeo g = make_ray(x[0], x[1], x[2], d[0], d[1], d[2]);
+        const RayGeoT<F> g = exact_geo<F>(x, d);
         exact_candidates(G, g, lane, [&](int c, double t, int reg) {
             tk[c] = t;
             pk[c] = ((uint32_t)c << 16) | (uint32_t)(reg + 2);
@@ -1537,7 +1471,7 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
         if (__ballot(nan) != 0) {
             if (lane == 0) {
                 introsort(v, K);
-                exact_walk<MODE, T>(G, o, ray, s, v);
+                exact_walk<MODE, T, F, INV>(G, o, ray, s, v);
             }
             wave_sync();
             continue;
@@ -1641,7 +1575,7 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
         TRACE_T(x3);
         TRACE_ADD(11, x2, x3);
         // (the pre-sort list and the left-stop list are free now: compacted segments go there)
-        exact_walk_wave<MODE, T>(G, o, ray, s, ts, ps, lpos, tk, lane);
+        exact_walk_wave<MODE, T, F, INV>(G, o, ray, s, ts, ps, lpos, tk, lane);
         wave_sync();
         TRACE_T(x4);
         TRACE_ADD(12, x3, x4);
@@ -1734,31 +1668,11 @@ static size_t exact_scratch_bytes(const GridDev& G) {   // lists of large-K grid
     return exact_in_lds(G) ? 0 : (size_t)kExactSerialBlocks * G.K * sizeof(Cand);
 }
 static size_t hits_bytes(int64_t n) { return (((size_t)n * sizeof(HitRay) + 255) / 256) * 256; }
-static size_t walk_bytes(int64_t n) { return (((size_t)n * sizeof(int32_t) + 255) / 256) * 256; }
 static size_t workspace_bytes(const GridDev& G, int64_t n) {
     return kWsHead + (((size_t)n * sizeof(int64_t) + 255) / 256) * 256 + hits_bytes(n) +
-           walk_bytes(n) + exact_scratch_bytes(G);
+           exact_scratch_bytes(G);
 }
 
-// The walk's boundary tables (sphrt_plan_pack_tables' block: doubles, then the cone flags) in
-// 8-byte words, staged in LDS per workgroup; grids whose tables exceed kWalkTabMax keep the list
-// trace.
-constexpr size_t kWalkTabMax = 32 * 1024;
-static int walk_tab_words(const GridDev& G) {
-    const size_t bytes = ((size_t)G.nbr + 2 * (size_t)G.nbe + 3 * (size_t)G.nba) * 8 + G.nbe;
-    return (int)((bytes + 7) / 8);
-}
-
-// The walk is opt-in (SPHRT_WALK=1, read at every launch): measured on MI355X it is slower than
-// the list trace on every BASELINE config (count pass, us, list / walk: C2 174 / 430, C4 511 /
-// 610, C5 766 / 896, C3 4475 / 5027) — one ray per lane serialises every solve of
-// a ray behind FP64 latency, and lanes advancing different families diverge, where the list
-// trace solves 64 boundaries per instruction.  It stays as a tested alternative (bitwise the
-// list trace's CSR: test_walk_equals_list_trace*, tests/test_walk_host.py).
-static bool walk_enabled() {
-    const char* e = getenv("SPHRT_WALK");
-    return e && e[0] == '1';
-}
 // The half-plane wedge (trace_one) is on unless SPHRT_TRACE_WEDGE=0 (A/B tests: the CSR is the
 // same bit for bit either way).
 static bool wedge_enabled() {
@@ -1792,11 +1706,6 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     o.n_hits = (unsigned*)(ws + 64);
     o.deferred = (int64_t*)(ws + kWsHead);
     o.hits = (HitRay*)(ws + kWsHead + (((size_t)R.n * sizeof(int64_t) + 255) / 256) * 256);
-    o.n_walk = (unsigned*)(ws + 128);
-    o.walk_rays = (int32_t*)((unsigned char*)o.hits + hits_bytes(R.n));
-    // the walk integrates one channel per ray (a register accumulator)
-    o.walk = walk_enabled() && (MODE != MODE_INTEGRATE || o.n_chan == 1 || o.ray_chan_div > 0) &&
-             (size_t)walk_tab_words(G) * 8 <= kWalkTabMax;
     o.wedge = wedge_enabled();
     Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
     if constexpr (MODE == MODE_BOUND) steps = kScreen;
@@ -1811,14 +1720,6 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     }
     if constexpr (MODE == MODE_BOUND) return 0;
     if (!(steps & kTrace)) return 0;
-    if (MODE != MODE_BOUND && o.walk) {
-        // the walk first: its out-of-order rays join the list trace's hit list
-        // (sized for every ray: the walk list's length is on the device; blocks past it exit)
-        const int tab_words = walk_tab_words(G);
-        hipLaunchKernelGGL((walk_kernel<MODE, T>), dim3((unsigned)((R.n + 255) / 256)), dim3(256),
-                           (size_t)tab_words * 8, st, G, R, o, tab_words);
-        if (int e = check_launch("walk_kernel")) return e;
-    }
     // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
     const int64_t grid = SPHRT_TRACE_GRID * kWavesPerBlock / waves;
     hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,
@@ -1968,16 +1869,87 @@ extern "C" int sphrt_trace_integrate_f64(const sphrt_plan* plan, const sphrt_ray
                                    out_chan_stride, workspace, workspace_size, stream);
 }
 
-extern "C" int sphrt_solve(const sphrt_plan* plan, const sphrt_rays* rays, int family, double* t,
-                           int32_t* region, int8_t* neg, void* stream) {
+template <typename F>
+static int solve(const sphrt_plan* plan, const sphrt_rays* rays, int family, F* t,
+                 int32_t* region, int8_t* neg, void* stream) {
     GridDev G;
     RaysDev R;
     if (int e = resolve(plan, rays, G, R, stream)) return e;
     DeviceGuard guard(plan->device);
     if (family < 0 || family > 2) return fail("family must be 0 (r), 1 (e) or 2 (a)");
     if (R.n == 0) return 0;
+    if (!t || !region || !neg) return fail("null solve output");
     const int64_t grid = (R.n + 255) / 256;
-    hipLaunchKernelGGL(solve_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, G, R,
-                       family, t, region, neg);
+    hipLaunchKernelGGL(solve_kernel<F>, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, G,
+                       R, family, t, region, neg);
     return check_launch("solve_kernel");
+}
+extern "C" int sphrt_solve(const sphrt_plan* plan, const sphrt_rays* rays, int family, double* t,
+                           int32_t* region, int8_t* neg, void* stream) {
+    return solve<double>(plan, rays, family, t, region, neg, stream);
+}
+extern "C" int sphrt_solve_f32(const sphrt_plan* plan, const sphrt_rays* rays, int family,
+                               float* t, int32_t* region, int8_t* neg, void* stream) {
+    return solve<float>(plan, rays, family, t, region, neg, stream);
+}
+
+// ---- reference-mode trace (Operator(..., ftype=float32) and / or invalid=True) ---------------
+// Every ray takes the exact path — all K candidates in the reference's concatenation order, the
+// emulated libstdc++ introsort, the forward fill and diff over the whole list — with the solves
+// and the length differences in the trace's precision and, for invalid=True, no masking.  These
+// options are outside every fast path (whose pruning — the outer-sphere span, the start-voxel
+// rules, the wedge — relies on float64 distances and on the masks); they cost one exact-path pass
+// per ray (count, then fill).
+template <int MODE, typename F, bool INV>
+static int launch_reference(const GridDev& G, const RaysDev& R, TraceOut<double> o,
+                            void* workspace, size_t workspace_size, hipStream_t st) {
+    if (G.nr < 1 || G.ne < 1 || G.na < 1) return fail("tracing needs at least one voxel per axis");
+    if (R.n == 0) return 0;
+    if (!workspace || workspace_size < workspace_bytes(G, R.n))
+        return fail("trace workspace too small: %zu < %zu bytes", workspace_size,
+                    workspace_bytes(G, R.n));
+    unsigned char* ws = (unsigned char*)workspace;
+    o.n_deferred = (unsigned long long*)ws;
+    if (exact_in_lds(G)) {
+        const int64_t blocks = R.n < 4 * kExactBlocks ? R.n : 4 * kExactBlocks;
+        hipLaunchKernelGGL((exact_wave_kernel<MODE, double, F, INV, true>), dim3((unsigned)blocks),
+                           dim3(64), exact_wave_lds(G.K), st, G, R, o);
+    } else {
+        Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
+        hipLaunchKernelGGL((exact_kernel<MODE, double, F, INV, true>), dim3(kExactSerialBlocks),
+                           dim3(64), 0, st, G, R, o, scratch);
+    }
+    return check_launch("exact_kernel (reference mode)");
+}
+
+extern "C" int sphrt_trace_reference(const sphrt_plan* plan, const sphrt_rays* rays, int flags,
+                                     int32_t* counts, const int64_t* row_ptr, int32_t* vox,
+                                     double* len, void* workspace, size_t workspace_size,
+                                     void* stream) {
+    GridDev G;
+    RaysDev R;
+    if (int e = resolve(plan, rays, G, R, stream)) return e;
+    DeviceGuard guard(plan->device);
+    if (flags & ~(SPHRT_TRACE_F32 | SPHRT_TRACE_INVALID)) return fail("unknown trace flags %d", flags);
+    hipStream_t st = (hipStream_t)stream;
+    TraceOut<double> o{};
+    const bool f32 = (flags & SPHRT_TRACE_F32) != 0, inv = (flags & SPHRT_TRACE_INVALID) != 0;
+    if (!row_ptr) {
+        if (!counts) return fail("null counts");
+        o.counts = counts;
+        if (f32)
+            return inv ? launch_reference<MODE_COUNT, float, true>(G, R, o, workspace, workspace_size, st)
+                       : launch_reference<MODE_COUNT, float, false>(G, R, o, workspace, workspace_size, st);
+        return inv ? launch_reference<MODE_COUNT, double, true>(G, R, o, workspace, workspace_size, st)
+                   : launch_reference<MODE_COUNT, double, false>(G, R, o, workspace, workspace_size, st);
+    }
+    if (!vox || !len) return fail("null fill output");
+    o.row_ptr = row_ptr;
+    o.vox = vox;
+    o.len = len;
+    if (f32)
+        return inv ? launch_reference<MODE_FILL, float, true>(G, R, o, workspace, workspace_size, st)
+                   : launch_reference<MODE_FILL, float, false>(G, R, o, workspace, workspace_size, st);
+    return inv ? launch_reference<MODE_FILL, double, true>(G, R, o, workspace, workspace_size, st)
+               : launch_reference<MODE_FILL, double, false>(G, R, o, workspace, workspace_size, st);
 }

@@ -147,23 +147,28 @@ class _Plan:
     the plan is created by attach() after the upload, over the caller's device copy (no
     hipMalloc, and no hipFree with its device-wide sync when the plan is destroyed)."""
 
-    def __init__(self, grid, device, boundaries=None, staging=None):
+    def __init__(self, grid, device, boundaries=None, staging=None, ftype=tr.float64):
         lib = _lib.load()
         rb, eb, ab = boundaries if boundaries is not None else (grid.r_b, grid.e_b, grid.a_b)
-        rb, eb, ab = (tr.asarray(b, dtype=tr.float64).contiguous() for b in (rb, eb, ab))
-        # trigonometric tables with torch CPU — the values the reference solvers use
+        # the boundaries in the trace's dtype (r_torch / e_torch / a_torch: tr.asarray(b, ftype))
+        rb, eb, ab = (tr.asarray(b, dtype=ftype).contiguous() for b in (rb, eb, ab))
+        # trigonometric tables with torch CPU in that dtype — the values the reference solvers
+        # use (float32: torch's float32 cos / sin, not rounded float64 values); every table is
+        # handed over as float64 (exact for float32 values)
         cos_e = tr.cos(eb)
         cos2_e = tr.cos(eb) ** 2
         cos_a, sin_a = tr.cos(ab), tr.sin(ab)
-        self._keep = [t.contiguous() for t in (rb, eb, ab, cos_e, cos2_e, cos_a, sin_a)]
+        a_wrap = bool(-ab[0] == ab[-1] == tr.pi)
+        self._keep = [t.to(tr.float64).contiguous() for t in (rb, eb, ab, cos_e, cos2_e, cos_a,
+                                                               sin_a)]
         rb, eb, ab, cos_e, cos2_e, cos_a, sin_a = self._keep
         desc = _lib.GridDesc()
         desc.nr, desc.ne, desc.na = len(rb) - 1, len(eb) - 1, len(ab) - 1
         desc.r_b, desc.e_b, desc.a_b = rb.data_ptr(), eb.data_ptr(), ab.data_ptr()
         desc.cos_e, desc.cos2_e = cos_e.data_ptr(), cos2_e.data_ptr()
         desc.cos_a, desc.sin_a = cos_a.data_ptr(), sin_a.data_ptr()
-        desc.a_wrap = int(bool(-ab[0] == ab[-1] == tr.pi))
-        res = tr.finfo(tr.float64).resolution
+        desc.a_wrap = int(a_wrap)
+        res = tr.finfo(ftype).resolution
         desc.close_tol = res ** (1 / 3)
         desc.plane_par_tol = res
         self.shape = (desc.nr, desc.ne, desc.na)
@@ -384,24 +389,29 @@ class _RayBatch:
 
 # ----- API-parity solvers (raytracer.py:248-552) ----------------------------------------------
 
+def _check_ftype(ftype):
+    if ftype not in (tr.float64, tr.float32):
+        raise NotImplementedError(f'sph_raytracer_amd traces in float64 or float32, not {ftype}')
+
+
 def _solve(family, bounds, xs, rays, ftype, itype, device):
-    if ftype != tr.float64:
-        raise NotImplementedError('sph_raytracer_amd traces in float64 only')
+    _check_ftype(ftype)
     dev = _lib.require_gpu(device)
     with tr.cuda.device(dev):
         bounds = tr.asarray(bounds, dtype=tr.float64)
         unit = tr.tensor([0.0, 1.0], dtype=tr.float64)
         grid_b = tuple(bounds if i == family else unit for i in range(3))
-        plan = _Plan(None, dev, boundaries=grid_b)
+        plan = _Plan(None, dev, boundaries=grid_b, ftype=ftype)
         batch = _RayBatch(None, xs, rays, dev)
         nb = len(bounds)
         width = nb if family == 2 else 2 * nb
-        t = tr.empty(batch.shape + (width,), dtype=tr.float64, device=dev)
+        t = tr.empty(batch.shape + (width,), dtype=ftype, device=dev)
         reg = tr.empty(batch.shape + (width,), dtype=tr.int32, device=dev)
         neg = tr.empty(batch.shape + (width,), dtype=tr.int8, device=dev)
-        _lib.check(_lib.load().sphrt_solve(plan.handle, batch.desc, family, _lib.ptr(t),
-                                           _lib.ptr(reg), _lib.ptr(neg), _lib.stream_of(dev)),
-                   'sphrt_solve')
+        lib = _lib.load()
+        fn = lib.sphrt_solve if ftype == tr.float64 else lib.sphrt_solve_f32
+        _lib.check(fn(plan.handle, batch.desc, family, _lib.ptr(t), _lib.ptr(reg), _lib.ptr(neg),
+                      _lib.stream_of(dev)), 'sphrt_solve')
         inds = tr.arange(nb, dtype=itype)
         inds = (inds if family == 2 else tr.cat((inds, inds))).repeat(*batch.shape, 1)
         return t.to(device), reg.to(itype).to(device), inds.to(device), neg.to(device)
@@ -724,10 +734,14 @@ class Operator:
 
     Args:
         grid (SphericalGrid), geom (ViewGeom or collection), dynamic (bool or None: infer from
-        geom), ftype (float64 only), itype (index dtype of the ``regs`` view), device (where
-        results live; compute always runs on the current ROCm GPU), pdevice (accepted for
-        compatibility), debug / debug_los (print one ray's segments), invalid (unsupported),
-        _compute (False: skip the trace, for plotting-only operators).
+        geom), ftype (float64, or float32: the crossings solved and differenced in float32 as
+        the reference does), itype (index dtype of the ``regs`` view), device (where results
+        live; compute always runs on the current ROCm GPU), pdevice (accepted for
+        compatibility), debug / debug_los (print one ray's segments), invalid (keep the
+        unmasked segments, inf / NaN lengths and out-of-grid regions included: the reference's
+        forward is then non-finite), _compute (False: skip the trace, for plotting-only
+        operators).  float32 and invalid traces take the reference-mode trace
+        (sphrt_trace_reference: every ray through the exact path); float64 takes the fast one.
     """
 
     def __init__(self, grid, geom, dynamic=False, ftype=FTYPE, itype=ITYPE, device=DEVICE,
@@ -740,11 +754,8 @@ class Operator:
         self.ftype = ftype
         self.itype = itype
         self.device = device
-        if ftype != tr.float64:
-            raise NotImplementedError('sph_raytracer_amd traces in float64 (the reference default); '
-                                      'ftype=float32 is not supported')
-        if invalid:
-            raise NotImplementedError('invalid=True (keep invalid segments) is not supported')
+        _check_ftype(ftype)
+        self.invalid = bool(invalid)
         self._csr = None
         self._fast = {}     # (shape, dtype, device) -> bound forward launch (steady-state calls)
         self._fastc = None  # the same bindings inside the CPython entry (csrc/fastpath.cpp)
@@ -766,7 +777,14 @@ class Operator:
         with tr.cuda.device(dev):
             self._trace_on(dev)
 
+    def _reference_mode(self):
+        """The trace options only the reference-mode trace takes (sphrt_trace_reference):
+        float32 solves (ftype=float32) and / or unmasked segments (invalid=True)."""
+        return self.ftype != tr.float64 or self.invalid
+
     def _trace_on(self, dev):
+        if self._reference_mode():
+            return self._trace_reference(dev)
         lib = _lib.load()
         # plan tables, cone-ray spec and start bins: one host-to-device copy
         stg = _Staging()
@@ -798,6 +816,50 @@ class Operator:
         n = batch.n
         stream = _lib.stream_of(dev)
         row_ptr, vox, seg_len, total = _trace_csr(lib, self._plan, batch, dev, stream)
+        self._index(lib, dev, batch, row_ptr, vox, seg_len, total, ray_id)
+
+    def _trace_reference(self, dev):
+        """Trace in reference mode: every ray through the exact path with the reference's own
+        rules for this ftype / invalid (raytracer.py:48-173), count then fill; start voxels by
+        find_starts in the trace's dtype (raytracer.py:133-137), on the host as the reference."""
+        lib = _lib.load()
+        stream = _lib.stream_of(dev)
+        self._plan = _Plan(self.grid, dev, ftype=self.ftype)
+        rays = _geom_rays(self.geom, dev)
+        xs_u = tr.asarray(self.geom.ray_starts, dtype=tr.float64).detach().to('cpu').contiguous()
+        st = tr.zeros(xs_u.shape[:-1] + (4,), dtype=tr.int32)
+        st[..., :3] = find_starts(self.grid, xs_u, ftype=self.ftype).moveaxis(0, -1).to(tr.int32)
+        staged = (xs_u.to(dev), st.to(dev))
+        batch = _RayBatch(self.grid, xs_u, rays, dev, staged=staged)
+        self._ray_shape = batch.shape
+        n = batch.n
+        flags = (_lib.TRACE_F32 if self.ftype == tr.float32 else 0) | \
+            (_lib.TRACE_INVALID if self.invalid else 0)
+        counts = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
+        row_ptr = tr.empty(n + 1, dtype=tr.int64, device=dev)
+        tws = _workspace(lib, self._plan, n, dev)
+        h, d = self._plan.handle, batch.desc
+        _lib.check(lib.sphrt_trace_reference(h, d, flags, _lib.ptr(counts), None, None, None,
+                                             _lib.ptr(tws), tws.numel(), stream),
+                   'sphrt_trace_reference(count)')
+        ws = tr.empty(lib.sphrt_scan_workspace_bytes(n), dtype=tr.uint8, device=dev)
+        _lib.check(lib.sphrt_scan_counts(_lib.ptr(counts), n, _lib.ptr(row_ptr), _lib.ptr(ws),
+                                         stream), 'sphrt_scan_counts')
+        total = int(row_ptr[n].item())
+        vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+        seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
+        if n > 0:
+            _lib.check(lib.sphrt_trace_reference(h, d, flags, None, _lib.ptr(row_ptr),
+                                                 _lib.ptr(vox), _lib.ptr(seg_len), _lib.ptr(tws),
+                                                 tws.numel(), stream),
+                       'sphrt_trace_reference(fill)')
+        del tws, counts, ws
+        self._index(lib, dev, batch, row_ptr, vox, seg_len, total, None)
+
+    def _index(self, lib, dev, batch, row_ptr, vox, seg_len, total, ray_id):
+        """The apply kernels' row index and granule tables over a traced CSR."""
+        n = batch.n
+        stream = _lib.stream_of(dev)
         batch.rays = None        # device ray directions: trace input only (24 B per ray)
         # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
         nblocks = lib.sphrt_csr_blocks(total)
@@ -1173,13 +1235,14 @@ class Operator:
     def _padded(self):
         csr = self._csr
         row_ptr, seg_vox, seg_len = self.segments()      # geometry order
+        seg_len = seg_len.to(self.ftype)                  # (float32 traces: exact)
         counts = (row_ptr[1:] - row_ptr[:-1])
         smax = max(int(counts.max().item()) if csr['n'] else 0, 1)
         n, total = csr['n'], csr['total']
         ray = tr.repeat_interleave(tr.arange(n, device=row_ptr.device), counts)
         pos = tr.arange(total, device=row_ptr.device) - row_ptr[:-1][ray]
         vox = tr.zeros((n, smax), dtype=tr.int64, device=row_ptr.device)
-        lens = tr.zeros((n, smax), dtype=tr.float64, device=row_ptr.device)
+        lens = tr.zeros((n, smax), dtype=self.ftype, device=row_ptr.device)
         vox[ray, pos] = seg_vox.to(tr.int64)
         lens[ray, pos] = seg_len
         _, ne, na = self.grid.shape[-3:]
@@ -1194,7 +1257,10 @@ class Operator:
 
     @property
     def lens(self):
-        """(*rays, S_max) segment lengths matching ``regs`` (zero padding)."""
+        """(*rays, S_max) segment lengths matching ``regs`` (zero padding), in the trace's
+        ftype.  invalid=True: every non-zero length of the reference's list, inf and NaN
+        included, with ``regs`` holding the wrapped voxel the reference's forward reads (-1 ->
+        n - 1)."""
         return self._padded()[1].to(device=self.device)
 
     def _ray_id_long(self):

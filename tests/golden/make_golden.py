@@ -123,7 +123,7 @@ def save_grad_case(name, grid, geom, pairs, note=''):
           f'-> {os.path.getsize(path) / 1e3:.0f} kB')
 
 
-def gd_case(name='gd_circ16', n_iter=25):
+def gd_case(name='gd_circ16', n_iter=25, n=16, n_views=12, det=(20, 16)):
     """A reference gd() run: examples/static_retrieval.py's loop (FullyDenseModel, [SquareLoss(),
     NegRegularizer()], lr 0.1, the reference's default Adam: retrieval.py:84-116, loss.py:92-95,
     153-155) on a 16^3 grid seen by 12 ConeCirc views; stores the inputs, the measurement, every
@@ -131,13 +131,14 @@ def gd_case(name='gd_circ16', n_iter=25):
     when the measurement is perturbed by one ulp per value (the run's own rounding sensitivity,
     which bounds any two correct implementations' agreement)."""
     L, M, RET = R.loss, R.model, R.retrieval
-    grid = G.SphericalGrid(shape=(16, 16, 16))
-    geom = orbit(12, lambda p: G.ConeCircGeom(shape=(20, 16), pos=p, fov=(0, 45)))
+    grid = G.SphericalGrid(shape=(n, n, n))
+    geom = orbit(n_views, lambda p: G.ConeCircGeom(shape=det, pos=p, fov=(0, 45)))
     xs, rays = geom.ray_starts.clone(), geom.rays.clone()
     op = RT.Operator(grid, geom)
     truth = tr.zeros(grid.shape, dtype=tr.float64)
-    truth[:, 8:, :8] = 1
-    truth[:, :8, 8:] = 1
+    h = n // 2
+    truth[:, h:, :h] = 1
+    truth[:, :h, h:] = 1
     meas = op(truth).detach()
 
     def run(y):
@@ -159,8 +160,9 @@ def gd_case(name='gd_circ16', n_iter=25):
                ray_shape=np.array(op.lens.shape[:-1]), truth=truth.numpy(), meas=meas.numpy(),
                loss_sq=l_sq, loss_neg=l_neg, coeffs=coeffs.numpy(), y_result=yres.numpy(),
                lr=np.array(0.1), iterations=np.array(n_iter),
-               note=np.array('reference gd(): 16^3, 12 ConeCirc (20,16), SquareLoss + '
-                             'NegRegularizer, Adam lr 0.1 (default implementation), 25 iterations'))
+               note=np.array(f'reference gd(): {n}^3, {n_views} ConeCirc {det}, SquareLoss + '
+                             f'NegRegularizer, Adam lr 0.1 (default implementation), {n_iter} '
+                             'iterations'))
     path = os.path.join(HERE, f'{name}.npz')
     np.savez_compressed(path, **out)
     print(f'{name}: final SquareLoss {l_sq[-1]:.4g} (from {l_sq[0]:.4g}) -> '
@@ -198,6 +200,102 @@ def pins():
     save_grad_case('multichannel', grid, geom, pairs,
                    note='static (12,10,14), ConeRect (24,20); channels 3, 14 (preview3d), (2,2)')
     gd_case()
+
+
+def save_api_case(name, grid, geom, densities=(), ys=(), note='', **op_kw):
+    """An Operator(..., **op_kw) case (ftype=float32, invalid=True): inputs, the reference's dense
+    (regs, lens) exactly as it returns them (lens in the trace's ftype, invalid entries kept), its
+    forward on float32 and float64 densities and its adjoint T(y)."""
+    xs, rays = geom.ray_starts.clone(), geom.rays.clone()
+    op = RT.Operator(grid, geom, **op_kw)
+    out = dict(grid_arrays(grid), xs=xs.numpy(), rays=rays.numpy(),
+               ray_shape=np.array(op.lens.shape[:-1]), note=np.array(note),
+               dense_regs=op.regs.numpy().astype(np.int32), dense_lens=op.lens.numpy())
+    for i, d in enumerate(densities):
+        out[f'density{i}'] = d.to(tr.float64).numpy()
+        out[f'fwd64_{i}'] = op(d.to(tr.float64)).numpy()
+        out[f'fwd32_{i}'] = op(d.to(tr.float32)).numpy()
+    for i, y in enumerate(ys):
+        out[f'y{i}'] = y.to(tr.float64).numpy()
+        out[f'adj64_{i}'] = op.T(y.to(tr.float64)).numpy()
+        try:   # (the reference's T raises for a float32 y on float64 lengths: index_put_ dtypes)
+            out[f'adj32_{i}'] = op.T(y.to(tr.float32)).numpy()
+        except RuntimeError as exc:
+            out[f'adj32_{i}_error'] = np.array(str(exc))
+    path = os.path.join(HERE, f'{name}.npz')
+    np.savez_compressed(path, **out)
+    lens = op.lens
+    print(f'{name}: rays={int(np.prod(lens.shape[:-1]))} K={lens.shape[-1]} lens {lens.dtype} '
+          f'finite non-zero {int((lens.isfinite() & (lens != 0)).sum())} nan '
+          f'{int(lens.isnan().sum())} inf {int(lens.isinf().sum())} -> '
+          f'{os.path.getsize(path) / 1e3:.0f} kB')
+
+
+def api_surface():
+    """Fixtures for the Operator options the GPU build once refused: ftype=float32 traces
+    (raytracer.py:48-173 and the solvers in float32, isclose threshold 0.01), invalid=True (the
+    un-masked lengths, raytracer.py:155-173), and ParallelGeom through ViewGeom (SURVEY App. C.2:
+    the reference's own Operator raises on ParallelGeom's broadcast rays)."""
+    g = tr.Generator().manual_seed(41)
+    f32 = tr.float32
+    # float32 solvers on random rays (as solvers.npz, ftype=float32)
+    n = 3000
+    xs = (tr.rand(n, 3, generator=g, dtype=tr.float64) - 0.5) * 6
+    xs[: n // 4] = (tr.rand(n // 4, 3, generator=g, dtype=tr.float64) - 0.5) * 1.2
+    rays = tr.randn(n, 3, generator=g, dtype=tr.float64)
+    rays /= tr.linalg.norm(rays, axis=-1)[..., None]
+    r_b = tr.linspace(0, 1, 11, dtype=tr.float64)
+    e_b = tr.linspace(0, tr.pi, 11, dtype=tr.float64)
+    a_b = tr.linspace(-tr.pi, tr.pi, 11, dtype=tr.float64)
+    out = dict(xs=xs.numpy(), rays=rays.numpy(), r_b=r_b.numpy(), e_b=e_b.numpy(),
+               a_b=a_b.numpy())
+    for key, fn, b in (('r', RT.r_torch, r_b), ('e', RT.e_torch, e_b), ('a', RT.a_torch, a_b)):
+        t, reg, _, neg = fn(b, xs.clone(), rays.clone(), ftype=f32)
+        out[f'{key}_t'] = t.numpy()
+        out[f'{key}_reg'] = reg.numpy().astype(np.int32)
+        out[f'{key}_neg'] = neg.numpy().astype(np.int8)
+    np.savez_compressed(os.path.join(HERE, 'solvers_f32.npz'), **out)
+    print('solvers_f32: done')
+    # float32 traces: a ConeRect view, a ConeCirc pair (ring 0 through the origin), inside starts
+    grid = G.SphericalGrid(shape=(16, 14, 18))
+    geom = G.ConeRectGeom((30, 40), pos=(5, 0.3, 1), fov=(45, 45))
+    save_api_case('f32_rect', grid, geom, densities=[tr.rand(grid.shape, generator=g)],
+                  ys=[tr.rand(geom.shape, generator=g, dtype=tr.float64)],
+                  note='ftype=float32: 16x14x18, ConeRect (30,40)', ftype=f32)
+    geom = orbit(2, lambda p: G.ConeCircGeom(shape=(24, 20), pos=p, fov=(0, 45)))
+    save_api_case('f32_circ', grid, geom, densities=[tr.rand(grid.shape, generator=g)],
+                  ys=[tr.rand(geom.shape, generator=g, dtype=tr.float64)],
+                  note='ftype=float32: 16x14x18, 2 ConeCirc (24,20)', ftype=f32)
+    grid = G.SphericalGrid(shape=(12, 10, 14))
+    n = 2000
+    xs = (tr.rand(n, 3, generator=g, dtype=tr.float64) - 0.5) * 1.6
+    rays = tr.randn(n, 3, generator=g, dtype=tr.float64)
+    save_api_case('f32_inside', grid, G.ViewGeom(xs, rays),
+                  densities=[tr.rand(grid.shape, generator=g)],
+                  ys=[tr.rand((n,), generator=g, dtype=tr.float64)],
+                  note='ftype=float32: random starts in/around the unit grid', ftype=f32)
+    # invalid=True: nothing masked (float64)
+    grid = G.SphericalGrid(shape=(16, 14, 18))
+    geom = G.ConeRectGeom((20, 24), pos=(5, 0.3, 1), fov=(45, 45))
+    save_api_case('invalid_rect', grid, geom, densities=[tr.rand(grid.shape, generator=g)],
+                  ys=[tr.rand(geom.shape, generator=g, dtype=tr.float64)],
+                  note='invalid=True: 16x14x18, ConeRect (20,24)', invalid=True)
+    grid = G.SphericalGrid(shape=(12, 10, 14))
+    n = 1000
+    xs = (tr.rand(n, 3, generator=g, dtype=tr.float64) - 0.5) * 1.6
+    rays = tr.randn(n, 3, generator=g, dtype=tr.float64)
+    save_api_case('invalid_inside', grid, G.ViewGeom(xs, rays),
+                  densities=[tr.rand(grid.shape, generator=g)],
+                  ys=[tr.rand((n,), generator=g, dtype=tr.float64)],
+                  note='invalid=True: random starts in/around the unit grid', invalid=True)
+    # ParallelGeom (geometry.py:607-655) through ViewGeom with the broadcast rays materialised
+    grid = G.SphericalGrid(shape=(20, 18, 24))
+    pg = G.ParallelGeom((30, 40), pos=(5, 0.5, 1), size=(2.2, 2.2))
+    vg = G.ViewGeom(pg.ray_starts, pg.rays.expand(pg.ray_starts.shape).clone())
+    save_case('parallel_geom', grid, vg, densities=[tr.rand(grid.shape, generator=g)],
+              ys=[tr.rand(vg.shape, generator=g, dtype=tr.float64)],
+              note='ParallelGeom (30,40) at (5,0.5,1), size 2.2: ViewGeom(ray_starts, rays '
+                   'expanded) (SURVEY App. C.2)')
 
 
 def main():
@@ -282,4 +380,14 @@ def main():
 if __name__ == '__main__':
     # `make_golden.py`: the trace fixtures; `make_golden.py pins`: dynamic_grad,
     # dynamic_single_grad, multichannel, gd_circ16
-    pins() if sys.argv[1:] == ['pins'] else main()
+    # `make_golden.py api`: solvers_f32, f32_*, invalid_*, parallel_geom;
+    # `make_golden.py gd32`: gd_circ32 (32^3, 32 ConeCirc views, 20 iterations)
+    arg = sys.argv[1:]
+    if arg == ['pins']:
+        pins()
+    elif arg == ['api']:
+        api_surface()
+    elif arg == ['gd32']:
+        gd_case('gd_circ32', n_iter=20, n=32, n_views=32, det=(50, 40))
+    else:
+        main()

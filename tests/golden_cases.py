@@ -11,7 +11,9 @@ import torch as tr
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 CASES = ['c1_single_vantage', 'c2_orbit3', 'circ_orbit', 'inside_starts', 'partial_grid',
-         'log_grid', 'dynamic_obs'] + [f'optest_{i}' for i in range(5)]
+         'log_grid', 'dynamic_obs', 'parallel_geom'] + [f'optest_{i}' for i in range(5)]
+F32_CASES = ['f32_rect', 'f32_circ', 'f32_inside']        # Operator(..., ftype=float32)
+INVALID_CASES = ['invalid_rect', 'invalid_inside']        # Operator(..., invalid=True)
 
 TINY = 1e-12           # segments shorter than TINY*scale are tie/ulp artefacts
 LEN_RTOL = 1e-12       # lengths, float64
@@ -67,9 +69,10 @@ def canonical(ptr, vox, seg, tiny):
     return ptr_m, vox[idx], seg_m
 
 
-def compare_segments(ref, got, scale, what=''):
-    """ref/got: (ptr, vox, len).  Returns None if equal under the contract, else a message."""
-    tiny = TINY * scale
+def compare_segments(ref, got, scale, what='', tiny=TINY, len_rtol=LEN_RTOL, len_atol=LEN_ATOL):
+    """ref/got: (ptr, vox, len).  Returns None if equal under the contract, else a message.
+    (float32 traces: tiny / len_rtol / len_atol at float32's resolution.)"""
+    tiny = tiny * scale
     pr, vr, lr = canonical(*ref, tiny)
     pg, vg, lg = canonical(*got, tiny)
     if len(pr) != len(pg):
@@ -84,11 +87,28 @@ def compare_segments(ref, got, scale, what=''):
                 f'ref {list(zip(vr[pr[i]:pr[i+1]].tolist(), lr[pr[i]:pr[i+1]].round(12).tolist()))} '
                 f'got {list(zip(vg[pg[i]:pg[i+1]].tolist(), lg[pg[i]:pg[i+1]].round(12).tolist()))}')
     err = np.abs(lr - lg)
-    tol = LEN_RTOL * np.abs(lr) + LEN_ATOL * scale
+    tol = len_rtol * np.abs(lr) + len_atol * scale
     if np.any(err > tol):
         k = int(np.argmax(err - tol))
         return f'{what}: length mismatch {lr[k]!r} vs {lg[k]!r} (|d|={err[k]:.3g})'
     return None
+
+
+def dense_to_segments(regs, lens, grid_shape, invalid=False):
+    """The reference's dense (3, *rays, K) regs and (*rays, K) lens -> per-ray segment lists in
+    order: (ptr, vox, len).  Default: the positive lengths (zero-length entries carry nothing).
+    invalid=True traces: every non-zero length (inf and NaN included) with its voxel wrapped as
+    the reference's forward indexes it (density[-1] is the last slice)."""
+    nr, ne, na = (int(v) for v in grid_shape)
+    K = lens.shape[-1]
+    regs = np.asarray(regs).reshape(3, -1, K).astype(np.int64)
+    lens = np.asarray(lens, np.float64).reshape(-1, K)
+    keep = (lens != 0) if invalid else (lens > 0)
+    ptr = np.zeros(lens.shape[0] + 1, np.int64)
+    ptr[1:] = np.cumsum(keep.sum(1))
+    r, e, a = (regs[i][keep] for i in range(3))
+    r, e, a = np.where(r < 0, r + nr, r), np.where(e < 0, e + ne, e), np.where(a < 0, a + na, a)
+    return ptr, ((r * ne + e) * na + a).astype(np.int64), lens[keep]
 
 
 def rel_close(got, ref, rtol, floor=1e-30):

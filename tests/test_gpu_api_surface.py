@@ -1,0 +1,158 @@
+"""GPU parity for the Operator options traced in reference mode and for ParallelGeom, against
+fixtures the reference itself produced (tests/golden/make_golden.py api):
+
+  - ftype=torch.float32 (raytracer.py:48-246 in float32; isclose threshold 0.01): the per-family
+    solvers (regions exact, distances within 2 float32 ulp: torch's CPU float32 sqrt is not always
+    the correctly rounded one), the trace (voxel sequences exact under the canonical form, lengths
+    at float32 resolution), forwards (float32 1e-5, float64 1e-10 on the float32 lengths) and
+    adjoints;
+  - invalid=True (raytracer.py:155: nothing masked): every non-zero entry of the reference's
+    dense trace per ray, in order — voxels (wrapped as the reference's forward indexes them),
+    finite lengths within 1e-12, and the inf / NaN entries at the same places — and the
+    reference's forward and adjoint, which are non-finite exactly where the reference's are;
+  - ParallelGeom (geometry.py:607-655: one direction broadcast over a plane of starts) through
+    Operator directly, which the reference's own Operator refuses, against the
+    reference's ViewGeom(pg.ray_starts, pg.rays.expand(...).clone()) fixture.
+"""
+import numpy as np
+import pytest
+import torch as tr
+
+import golden_cases as gc
+
+pytestmark = pytest.mark.gpu
+F32_TINY = 1e-6          # float32 resolution: length / tiny-segment scale of a float32 trace
+F32_LEN_RTOL = 4e-7      # 2-3 ulp of float32
+
+
+def _op(case, gpu, **kw):
+    from sph_raytracer_amd import Operator
+    return Operator(gc.make_grid(case), gc.FixtureGeom(case), device=gpu, **kw)
+
+
+@pytest.mark.parametrize('family', ['r', 'e', 'a'])
+def test_solvers_f32(family, gpu):
+    from sph_raytracer_amd.raytracer import a_torch, e_torch, r_torch
+    case = gc.load('solvers_f32')
+    fn = {'r': r_torch, 'e': e_torch, 'a': a_torch}[family]
+    b = tr.from_numpy(case[f'{family}_b'])
+    t, reg, _, neg = fn(b, tr.from_numpy(case['xs']), tr.from_numpy(case['rays']),
+                        ftype=tr.float32, device=gpu)
+    assert t.dtype == tr.float32
+    t, reg, neg = t.cpu().numpy(), reg.cpu().numpy(), neg.cpu().numpy()
+    t_ref = case[f'{family}_t']
+    assert np.array_equal(np.isfinite(t), np.isfinite(t_ref)), family
+    fin = np.isfinite(t_ref)
+    ulp = np.abs(t[fin].view(np.int32).astype(np.int64) - t_ref[fin].view(np.int32).astype(np.int64))
+    assert ulp.max() <= 2, f'{family}: {int((ulp > 0).sum())} distances differ, max {ulp.max()} ulp'
+    assert np.array_equal(t[~fin], t_ref[~fin])
+    # regions follow the distances: exact except where a distance moved by an ulp across a region
+    # test (none in this fixture's rays)
+    assert np.array_equal(reg, case[f'{family}_reg']), family
+    assert np.array_equal(neg, case[f'{family}_neg']), family
+
+
+@pytest.mark.parametrize('name', gc.F32_CASES)
+def test_f32_trace(name, gpu):
+    case = gc.load(name)
+    op = _op(case, gpu, ftype=tr.float32)
+    ptr, vox, seg = (t.cpu().numpy() for t in op.segments())
+    # float32 lengths: exactly float32 values
+    assert np.array_equal(seg.astype(np.float32).astype(np.float64), seg)
+    shape = tuple(int(v) for v in case['shape'])[-3:]
+    ref = gc.dense_to_segments(case['dense_regs'], case['dense_lens'], shape)
+    msg = gc.compare_segments(ref, (ptr, vox, seg), gc.scale_of(case), name, tiny=F32_TINY,
+                              len_rtol=F32_LEN_RTOL, len_atol=F32_TINY)
+    assert msg is None, msg
+    assert op.lens.dtype == tr.float32
+
+
+@pytest.mark.parametrize('name', gc.F32_CASES)
+def test_f32_forward_adjoint(name, gpu):
+    case = gc.load(name)
+    op = _op(case, gpu, ftype=tr.float32)
+    d64 = tr.from_numpy(case['density0']).to(gpu)
+    got = op(d64.float())
+    assert got.dtype == tr.float32
+    err = gc.rel_close(got.cpu().numpy(), case['fwd32_0'], gc.F32_RTOL)
+    assert err <= gc.F32_RTOL, f'{name} f32 forward rel err {err:.3g}'
+    # float64 density on float32 lengths (the reference promotes): the lengths' rounding bounds it
+    err = gc.rel_close(op(d64).cpu().numpy(), case['fwd64_0'], 1e-6)
+    assert err <= 1e-6, f'{name} f64 forward rel err {err:.3g}'
+    y = tr.from_numpy(case['y0']).to(gpu)
+    for yy, key, tol in ((y, 'adj64_0', 1e-6), (y.float(), 'adj32_0', 1e-5)):
+        got = op.T(yy).cpu().numpy()
+        ref = case[key]
+        err = float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-300))
+        assert err <= tol, f'{name} {key} rel err {err:.3g}'
+
+
+def _same_nonfinite(got, ref):
+    return np.array_equal(np.isnan(got), np.isnan(ref)) and \
+        np.array_equal(np.isposinf(got), np.isposinf(ref)) and \
+        np.array_equal(np.isneginf(got), np.isneginf(ref))
+
+
+@pytest.mark.parametrize('name', gc.INVALID_CASES)
+def test_invalid_trace(name, gpu):
+    case = gc.load(name)
+    op = _op(case, gpu, invalid=True)
+    ptr, vox, seg = (t.cpu().numpy() for t in op.segments())
+    shape = tuple(int(v) for v in case['shape'])[-3:]
+    rp, rv, rl = gc.dense_to_segments(case['dense_regs'], case['dense_lens'], shape, invalid=True)
+    assert np.array_equal(ptr, rp), f'{name}: segment counts differ'
+    assert np.array_equal(vox, rv), f'{name}: voxels differ'
+    assert _same_nonfinite(seg, rl), f'{name}: inf / NaN lengths at other places'
+    fin = np.isfinite(rl)
+    err = np.abs(seg[fin] - rl[fin])
+    tol = gc.LEN_RTOL * np.abs(rl[fin]) + gc.LEN_ATOL * gc.scale_of(case)
+    assert np.all(err <= tol), f'{name}: finite lengths differ by {err.max():.3g}'
+    assert int(fin.sum()) > 0 and int((~fin).sum()) > 0
+
+
+@pytest.mark.parametrize('name', gc.INVALID_CASES)
+def test_invalid_forward_adjoint(name, gpu):
+    """The reference's forward with invalid=True is non-finite for every ray (each ray's list
+    holds an inf - inf = NaN length); ours is non-finite in the same places, and so is T."""
+    case = gc.load(name)
+    op = _op(case, gpu, invalid=True)
+    d64 = tr.from_numpy(case['density0']).to(gpu)
+    for dt, key in ((tr.float64, 'fwd64_0'), (tr.float32, 'fwd32_0')):
+        got = op(d64.to(dt)).cpu().numpy()
+        ref = case[key]
+        assert _same_nonfinite(got, ref), f'{name} {key}: non-finite pattern differs'
+        fin = np.isfinite(ref)
+        if fin.any():
+            assert gc.rel_close(got[fin], ref[fin], 1e-5) <= 1e-5
+    got = op.T(tr.from_numpy(case['y0']).to(gpu)).cpu().numpy()
+    ref = case['adj64_0']
+    assert _same_nonfinite(got, ref), f'{name} T: non-finite pattern differs'
+    fin = np.isfinite(ref)
+    if fin.any():
+        err = float(np.abs(got[fin] - ref[fin]).max() / max(np.abs(ref[fin]).max(), 1e-300))
+        assert err <= 1e-10
+
+
+def test_parallel_geom_operator(gpu):
+    """ParallelGeom straight into Operator (its (1, 1, 3) rays broadcast over the starts, as
+    trace_indices broadcasts them, raytracer.py:77-80) equals the reference's trace and forward
+    of the same rays materialised per start."""
+    from sph_raytracer_amd import Operator, ParallelGeom, SphericalGrid
+    case = gc.load('parallel_geom')
+    pg = ParallelGeom((30, 40), pos=(5, 0.5, 1), size=(2.2, 2.2))
+    assert tuple(pg.rays.shape) == (1, 1, 3)
+    assert tr.equal(pg.ray_starts, tr.from_numpy(case['xs']))
+    assert tr.equal(pg.rays.expand(pg.ray_starts.shape), tr.from_numpy(case['rays']))
+    op = Operator(SphericalGrid(shape=(20, 18, 24)), pg, device=gpu)
+    ptr, vox, seg = (t.cpu().numpy() for t in op.segments())
+    msg = gc.compare_segments((case['seg_ptr'], case['seg_vox'], case['seg_len']),
+                              (ptr, vox, seg), gc.scale_of(case), 'parallel_geom')
+    assert msg is None, msg
+    d = tr.from_numpy(case['density0']).to(gpu)
+    got = op(d)
+    assert tuple(got.shape) == (30, 40)
+    err = gc.rel_close(got.cpu().numpy(), case['fwd64_0'], gc.F64_RTOL)
+    assert err <= gc.F64_RTOL, f'parallel_geom forward rel err {err:.3g}'
+    got = op.T(tr.from_numpy(case['y0']).to(gpu)).cpu().numpy()
+    ref = case['adj64_0']
+    assert float(np.abs(got - ref).max() / np.abs(ref).max()) <= 1e-10

@@ -191,22 +191,3 @@ def test_onepass_trace_equals_twopass(name, gpu, monkeypatch):
     got = _csr(_op(case, gpu))
     for a, b in zip(ref, got):
         assert tr.equal(a, b), name + ' (fallback)'
-
-
-@pytest.mark.parametrize('name', gc.CASES)
-def test_walk_equals_list_trace(name, gpu, monkeypatch):
-    """The lane walk (csrc/walk.hpp: rays from outside the grid, one per lane, their crossings
-    merged from per-family runs) builds the CSR of the list trace (every hit ray sorted by one
-    wave) bit for bit, on every fixture; so does the fused no-store forward."""
-    from sph_raytracer_amd.raytracer import line_integrals
-    case = gc.load(name)
-    monkeypatch.setenv('SPHRT_WALK', '0')
-    ref = _csr(_op(case, gpu))
-    d = tr.from_numpy(case['density0']).to(gpu)
-    fref = line_integrals(gc.make_grid(case), gc.FixtureGeom(case), d)
-    monkeypatch.setenv('SPHRT_WALK', '1')
-    got = _csr(_op(case, gpu))
-    for a, b in zip(ref, got):
-        assert tr.equal(a, b), name
-    fgot = line_integrals(gc.make_grid(case), gc.FixtureGeom(case), d)
-    assert float((fgot - fref).abs().max()) <= 1e-12 * max(float(fref.abs().max()), 1e-300)

@@ -77,20 +77,23 @@ def test_multichannel_vs_reference(gpu):
     _grad_check(case, op, gpu, 'multichannel')
 
 
-@pytest.mark.parametrize('optim_kw', [{}, {'fused': True}])
-def test_gd_vs_reference(optim_kw, gpu):
+@pytest.mark.parametrize('case_name,n,n_views,det,optim_kw', [
+    ('gd_circ16', 16, 12, (20, 16), {}), ('gd_circ16', 16, 12, (20, 16), {'fused': True}),
+    ('gd_circ32', 32, 32, (50, 40), {})])
+def test_gd_vs_reference(case_name, n, n_views, det, optim_kw, gpu):
     """Row f2: gd() with the reference's arguments (FullyDenseModel, [SquareLoss(),
-    NegRegularizer()], lr 0.1, 25 iterations) against the reference's own run on the same
+    NegRegularizer()], lr 0.1; 16^3 x 12 views x 25 iterations, and 32^3 x 32 views (50, 40) x 20
+    iterations, closer to C5) against the reference's own run on the same
     measurement: every iteration's loss values and the final coefficients and reconstruction.
     The default optimiser is the reference's (torch's default Adam); fused=True, the caller's
     choice, stays inside the same tolerance.  Both take the autograd-free loop (_gd_direct)."""
     from sph_raytracer_amd import ConeCircGeom, Operator, SphericalGrid, retrieval
     from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
     from sph_raytracer_amd.model import FullyDenseModel
-    case = gc.load('gd_circ16')
-    grid = SphericalGrid(shape=(16, 16, 16))
-    th = tr.linspace(0, 2 * tr.pi, 12)
-    geom = sum(ConeCircGeom(shape=(20, 16), pos=(5 * tr.cos(t), 5 * tr.sin(t), 1), fov=(0, 45))
+    case = gc.load(case_name)
+    grid = SphericalGrid(shape=(n, n, n))
+    th = tr.linspace(0, 2 * tr.pi, n_views)
+    geom = sum(ConeCircGeom(shape=det, pos=(5 * tr.cos(t), 5 * tr.sin(t), 1), fov=(0, 45))
                for t in th)
     assert tr.equal(geom.rays, tr.from_numpy(case['rays']))
     op = Operator(grid, geom, device=gpu)
@@ -112,7 +115,7 @@ def test_gd_vs_reference(optim_kw, gpu):
         retrieval._gd_direct = direct
     assert calls == [1]
     l_sq, l_neg = np.array(losses[sq]), np.array(losses[neg])
-    assert len(l_sq) == len(case['loss_sq']) == 25
+    assert len(l_sq) == len(case['loss_sq']) == int(case['iterations'])
     err = np.abs(l_sq - case['loss_sq']) / case['loss_sq']
     assert err.max() <= 1e-9, f'SquareLoss history rel err {err.max():.3g} at {err.argmax()}'
     err = np.abs(l_neg - case['loss_neg'])

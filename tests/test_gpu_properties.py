@@ -835,54 +835,6 @@ def test_onepass_tables_equal_twopass(grid_shape, staged, gpu, monkeypatch):
         assert tr.equal(t0[b * s0:b * s0 + k], t1[b * s1:b * s1 + k])
 
 
-@pytest.mark.parametrize('case', ['orbit', 'orbit_staged', 'random_rays', 'dynamic'])
-def test_hash_tables_equal_radix(case, gpu, monkeypatch):
-    """Granule tables of blocks <= 2048 segments built from the hash-deduplicated sort
-    (apply.hip hash_table, SPHRT_TABLE_SORT=hash) equal the sort of every segment (the default)
-    bitwise: block records, loc, tables, stride, fallback count — orbits above 2^19 voxels
-    (natural and brick-staged columns), random lines (blocks of 1025-2046 distinct granules: the
-    8-key sort of the distinct granules, and blocks over kMaxGran: the fallback) and a
-    time-paired dynamic grid (32-bit tables)."""
-    from sph_raytracer_amd import Operator, SphericalGrid, ViewGeom
-    if case == 'random_rays':
-        grid = SphericalGrid(shape=(96, 80, 90))
-        rng = np.random.default_rng(7)
-        xs = rng.normal(size=(60000, 3))
-        xs = 1.5 * xs / np.linalg.norm(xs, axis=1, keepdims=True)
-        d = rng.normal(size=(60000, 3)) * 0.3 - xs
-        d /= np.linalg.norm(d, axis=1, keepdims=True)
-        geom = ViewGeom(tr.from_numpy(xs), tr.from_numpy(d))
-    elif case == 'dynamic':
-        grid, geom = _orbit(8, (24, 32), grid_shape=(48, 48, 48))
-        grid = SphericalGrid(shape=(8, 48, 48, 48))
-    else:
-        grid, geom = _orbit(6, (40, 64), grid_shape=(96, 80, 90))
-    monkeypatch.setenv('SPHRT_BRICK', '4,2,4' if case == 'orbit_staged' else 'off')
-    res = []
-    for mode in ('radix', 'hash'):
-        monkeypatch.setenv('SPHRT_TABLE_SORT', mode)
-        op = Operator(grid, geom, device=gpu)
-        c = op._csr
-        blocks, loc, tab, d_ = c['blocks'], c['loc'], c['tab'], c['desc']
-        if case == 'dynamic':
-            op(tr.rand(grid.shape, device=gpu))
-            p = c[('paired', 8, 24 * 32)]
-            _, blocks, loc, tab, _ = p['keep']
-            d_ = p['desc']
-        res.append((blocks.cpu(), loc[:c['total']].cpu(), d_.tab_stride, d_.n_fallback,
-                    tab[:c['nblocks'] * d_.tab_stride].cpu(), d_.tab_bytes))
-    (b0, l0, s0, f0, t0, w0), (b1, l1, s1, f1, t1, w1) = res
-    assert s0 == s1 and f0 == f1 and w0 == w1
-    assert tr.equal(b0, b1) and tr.equal(l0, l1)
-    n_tab = b0.reshape(-1, 6)[:, 5]
-    for b in range(len(n_tab)):
-        k = int(n_tab[b])
-        if k > 0:
-            assert tr.equal(t0[b * s0:b * s0 + k], t1[b * s1:b * s1 + k])
-    if case == 'random_rays':
-        assert int((n_tab > 1024).sum()) > 0
-
-
 def _expected_runs(csr, n_blocks_fields):
     """Host restatement of block_runs_kernel: per block, the runs of consecutive rays of its rows
     and of its share of the empty list (None for more than MAX_RUNS)."""
@@ -1227,24 +1179,3 @@ def test_gd_direct_declines_what_it_cannot_run(gpu, monkeypatch):
                                  num_iterations=8, loss_fns=fns, progress_bar=False)
     assert len(calls) == 2 and c1.device == dev1
     assert tr.equal(c1.cpu(), ca.cpu())
-
-
-@pytest.mark.parametrize('kind, n_views, det, grid_shape', [
-    ('rect', 50, (50, 100), (50, 50, 50)),          # C2
-    ('circ', 64, (100, 50), (64, 64, 64)),          # C5 geometry (ring 0 through the origin)
-    ('rect', 12, (128, 256), (128, 128, 128)),      # C3 grid
-    ('circ', 9, (40, 30), (40, 70, 33)),
-])
-def test_walk_equals_list_trace_full_size(kind, n_views, det, grid_shape, gpu, monkeypatch):
-    """At full size the lane walk's CSR equals the list trace's bit for bit (the walk sends
-    tie-ambiguous rays to the exact kernel and rays whose run order fails to the list trace)."""
-    from sph_raytracer_amd import Operator
-    grid, geom = _orbit(n_views, det, kind=kind, grid_shape=grid_shape)
-    monkeypatch.setenv('SPHRT_WALK', '0')
-    ref = Operator(grid, geom, device=gpu)._csr
-    monkeypatch.setenv('SPHRT_WALK', '1')
-    got = Operator(grid, geom, device=gpu)._csr
-    assert ref['total'] == got['total']
-    for k in ('row_ptr', 'vox', 'len'):
-        assert tr.equal(ref[k][:ref['total'] if k != 'row_ptr' else None],
-                        got[k][:got['total'] if k != 'row_ptr' else None]), k
