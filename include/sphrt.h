@@ -132,10 +132,15 @@ int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64
  * plan, as for sphrt_solve_f32; lengths are float32 values stored as doubles);
  * SPHRT_TRACE_INVALID — no masking (raytracer.py:155 `if not invalid`): every non-zero length is
  * kept, inf and NaN included, with its voxel wrapped the way the reference's forward indexes it
- * (region -1 reads the last shell / cone / wedge).  row_ptr == NULL: count pass (`counts`, int32
- * per ray); else fill pass into (vox, len) at row_ptr.  Workspace: sphrt_trace_workspace_bytes. */
+ * (region -1 reads the last shell / cone / wedge); SPHRT_TRACE_FRESH_RAYS — the caller's rays are
+ * not of the trace's dtype, so tr.asarray(rays, ftype) hands each solver a fresh copy
+ * (raytracer.py:276,360,500): r_torch and e_torch normalise theirs once, a_torch uses them
+ * unnormalised (without the flag the in-place normalisations of raytracer.py:281,365 chain: e_torch
+ * and a_torch see the twice-normalised rays).  row_ptr == NULL: count pass (`counts`, int32 per
+ * ray); else fill pass into (vox, len) at row_ptr.  Workspace: sphrt_trace_workspace_bytes. */
 #define SPHRT_TRACE_F32 1
 #define SPHRT_TRACE_INVALID 2
+#define SPHRT_TRACE_FRESH_RAYS 4
 int sphrt_trace_reference(const sphrt_plan *plan, const sphrt_rays *rays, int flags,
                           int32_t *counts, const int64_t *row_ptr, int32_t *vox, double *len,
                           void *workspace, size_t workspace_size, void *stream);

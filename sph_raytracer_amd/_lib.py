@@ -113,7 +113,7 @@ _SIGNATURES = [
                                           c_i64, c_vp, c_i64, c_vp, ctypes.c_size_t, c_vp]),
 ]
 EXPORTED = [s[0] for s in _SIGNATURES]
-TRACE_F32, TRACE_INVALID = 1, 2        # sphrt_trace_reference flags (sphrt.h)
+TRACE_F32, TRACE_INVALID, TRACE_FRESH_RAYS = 1, 2, 4   # sphrt_trace_reference flags (sphrt.h)
 
 _lib = None
 

@@ -27,6 +27,7 @@ struct RaysDev {
     const double* xs;
     const double* rays;
     const int32_t* start;
+    int fresh;    // reference-mode trace: each solver normalises its own copy (exact_list)
 };
 
 int fail(const char* fmt, ...);   // records the message, returns -1
@@ -88,6 +89,7 @@ inline int resolve(const sphrt_plan* plan, const sphrt_rays* rays, GridDev& G, R
     R.xs = rays->xs;
     R.rays = rays->rays;
     R.start = rays->start;
+    R.fresh = 0;
     return 0;
 }
 

@@ -1193,33 +1193,55 @@ __global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int fa
 // Candidates in the reference's concatenation order (raytracer.py:92, 117-122), solved by the
 // lanes in parallel.  Returns through `put(c, t, region)`.
 // F: the solves' precision (double; float for ftype=torch.float32 traces), the distances handed
-// to `put` as doubles (exact for float).
+// to `put` as doubles (exact for float).  gr / ge / ga: the ray as r_torch / e_torch / a_torch see
+// it (the same RayGeo unless the rays are fresh copies per solver, exact_list).
 template <typename F, class Put>
-__device__ __forceinline__ void exact_candidates(const GridDev& G, const RayGeoT<F>& g, int lane,
-                                                 Put put) {
+__device__ __forceinline__ void exact_candidates(const GridDev& G, const RayGeoT<F>& gr,
+                                                 const RayGeoT<F>& ge, const RayGeoT<F>& ga,
+                                                 int lane, Put put) {
     const int nbr = G.nbr, nbe = G.nbe, nba = G.nba;
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe;
     for (int j = lane; j < nbr; j += 64) {
         F ti, to;
         int ri, ro, ni, no;
-        sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
+        sphere_solve(G, gr, j, ti, ri, to, ro, ni, no);
         put(j, (double)ti, ri);
         put(nbr + j, (double)to, ro);
     }
     for (int j = lane; j < nbe; j += 64) {
         F ta, tb;
         int ra, rb, na_, nb_;
-        cone_solve(G, g, j, ta, ra, tb, rb, na_, nb_);
+        cone_solve(G, ge, j, ta, ra, tb, rb, na_, nb_);
         put(r_lim + j, (double)ta, ra);
         put(r_lim + nbe + j, (double)tb, rb);
     }
     for (int j = lane; j < nba; j += 64) {
         F t;
         int r, ng;
-        plane_solve(G, g, j, t, r, ng);
+        plane_solve(G, ga, j, t, r, ng);
         put(e_lim + j, (double)t, r);
     }
     if (lane == 0) put(G.K - 1, 0.0, 0);
+}
+// The candidate list of one ray.  trace_indices hands the same `rays` tensor to the three solvers
+// and each converts it with tr.asarray(rays, ftype) (raytracer.py:276,360,500): when that is the
+// caller's tensor (its dtype is ftype) r_torch and e_torch normalise it in place in turn
+// (raytracer.py:281,365) and a_torch sees it normalised twice (make_ray); when the dtype differs
+// (R.fresh: sphrt_trace_reference's SPHRT_TRACE_FRESH_RAYS, e.g. float64 rays in a float32 trace)
+// every solver gets a fresh copy: r_torch and e_torch normalise theirs once, a_torch not at all.
+template <bool ALL, typename F, class Put>
+__device__ __forceinline__ void exact_list(const GridDev& G, const RaysDev& R,
+                                           const RayGeoT<F>& g, const double* x, const double* d,
+                                           int lane, Put put) {
+    if (ALL && R.fresh) {
+        const RayGeoT<F> ge = make_ray_family<F>((F)x[0], (F)x[1], (F)x[2], (F)d[0], (F)d[1],
+                                                 (F)d[2], 1);
+        const RayGeoT<F> ga = make_ray_family<F>((F)x[0], (F)x[1], (F)x[2], (F)d[0], (F)d[1],
+                                                 (F)d[2], 2);
+        exact_candidates(G, g, ge, ga, lane, put);
+    } else {
+        exact_candidates(G, g, g, g, lane, put);
+    }
 }
 
 // A sorted entry's segment under the trace's options: its length (tn - t in F: float32 traces
@@ -1402,7 +1424,7 @@ __global__ __launch_bounds__(64) void exact_kernel(GridDev G, RaysDev R, TraceOu
         int s[3];
         load_ray(R, ray, x, d, s);
         const RayGeoT<F> g = exact_geo<F>(x, d);
-        exact_candidates(G, g, lane, [&](int c, double t, int reg) {
+        exact_list<ALL>(G, R, g, x, d, lane, [&](int c, double t, int reg) {
             v.set(c, Cand{t, ((uint32_t)c << 16) | (uint32_t)(reg + 2), 0u});
         });
         __syncthreads();
@@ -1460,7 +1482,7 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
         load_ray(R, ray, x, d, s);
         TRACE_T(x0);
         const RayGeoT<F> g = exact_geo<F>(x, d);
-        exact_candidates(G, g, lane, [&](int c, double t, int reg) {
+        exact_list<ALL>(G, R, g, x, d, lane, [&](int c, double t, int reg) {
             tk[c] = t;
             pk[c] = ((uint32_t)c << 16) | (uint32_t)(reg + 2);
         });
@@ -1930,7 +1952,9 @@ extern "C" int sphrt_trace_reference(const sphrt_plan* plan, const sphrt_rays* r
     RaysDev R;
     if (int e = resolve(plan, rays, G, R, stream)) return e;
     DeviceGuard guard(plan->device);
-    if (flags & ~(SPHRT_TRACE_F32 | SPHRT_TRACE_INVALID)) return fail("unknown trace flags %d", flags);
+    if (flags & ~(SPHRT_TRACE_F32 | SPHRT_TRACE_INVALID | SPHRT_TRACE_FRESH_RAYS))
+        return fail("unknown trace flags %d", flags);
+    R.fresh = (flags & SPHRT_TRACE_FRESH_RAYS) != 0;
     hipStream_t st = (hipStream_t)stream;
     TraceOut<double> o{};
     const bool f32 = (flags & SPHRT_TRACE_F32) != 0, inv = (flags & SPHRT_TRACE_INVALID) != 0;

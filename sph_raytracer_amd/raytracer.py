@@ -24,7 +24,7 @@ import os
 import torch as tr
 
 from . import _lib
-from .geometry import ViewGeomCollection
+from .geometry import ViewGeom, ViewGeomCollection
 
 DEVICE = 'cpu'
 PDEVICE = 'cpu'
@@ -777,10 +777,25 @@ class Operator:
         with tr.cuda.device(dev):
             self._trace_on(dev)
 
+    def _fresh_rays(self):
+        """True when trace_indices' solvers each get a fresh copy of the rays: tr.asarray(rays,
+        ftype) copies when the geometry's rays are not of the trace's dtype
+        (raytracer.py:276,360,500), and then r_torch and e_torch normalise their own copy once and
+        a_torch takes the rays unnormalised; otherwise the in-place normalisations chain
+        (raytracer.py:281,365).  Every geometry class here holds float64 rays, as the
+        reference's do (geometry.py:25,285-286)."""
+        if isinstance(self.geom, (ViewGeom, ViewGeomCollection)):
+            dt = tr.float64
+        else:
+            rays = self.geom.rays
+            dt = rays.dtype if isinstance(rays, tr.Tensor) else tr.asarray(rays).dtype
+        return dt != self.ftype
+
     def _reference_mode(self):
         """The trace options only the reference-mode trace takes (sphrt_trace_reference):
-        float32 solves (ftype=float32) and / or unmasked segments (invalid=True)."""
-        return self.ftype != tr.float64 or self.invalid
+        float32 solves (ftype=float32), unmasked segments (invalid=True), fresh ray copies per
+        solver (_fresh_rays)."""
+        return self.ftype != tr.float64 or self.invalid or self._fresh_rays()
 
     def _trace_on(self, dev):
         if self._reference_mode():
@@ -834,7 +849,8 @@ class Operator:
         self._ray_shape = batch.shape
         n = batch.n
         flags = (_lib.TRACE_F32 if self.ftype == tr.float32 else 0) | \
-            (_lib.TRACE_INVALID if self.invalid else 0)
+            (_lib.TRACE_INVALID if self.invalid else 0) | \
+            (_lib.TRACE_FRESH_RAYS if self._fresh_rays() else 0)
         counts = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
         row_ptr = tr.empty(n + 1, dtype=tr.int64, device=dev)
         tws = _workspace(lib, self._plan, n, dev)

@@ -45,6 +45,16 @@ def make_grid(case):
     return SphericalGrid(**kw)
 
 
+def ref_mode_starts(case, f32):
+    """(3, *rays) start voxels of a reference-mode fixture (no stored starts): find_starts in the
+    trace's dtype (raytracer.py:111), pinned by the inside_starts fixture."""
+    from sph_raytracer_amd.raytracer import find_starts
+    xs, rays = tr.from_numpy(case['xs']), tr.from_numpy(case['rays'])
+    shape = tuple(np.broadcast_shapes(xs.shape, rays.shape))
+    return find_starts(make_grid(case), xs.broadcast_to(shape),
+                       ftype=tr.float32 if f32 else tr.float64).numpy()
+
+
 def scale_of(case):
     return max(float(np.abs(case['r_b']).max()), float(np.abs(case['xs']).max()))
 

@@ -314,7 +314,9 @@ def test_library_builds_and_exports_header():
     assert sorted(_lib.EXPORTED) == declared, 'ctypes bindings out of sync with the header'
     hdr = open(os.path.join(ROOT, 'include', 'sphrt.h')).read()
     for name, val in (('SPHRT_ROW_HEAD', _lib.ROW_HEAD), ('SPHRT_BLOCK_FIELDS', _lib.BLOCK_FIELDS),
-                      ('SPHRT_LOC_HEAD', _lib.LOC_HEAD)):
+                      ('SPHRT_LOC_HEAD', _lib.LOC_HEAD), ('SPHRT_TRACE_F32', _lib.TRACE_F32),
+                      ('SPHRT_TRACE_INVALID', _lib.TRACE_INVALID),
+                      ('SPHRT_TRACE_FRESH_RAYS', _lib.TRACE_FRESH_RAYS)):
         m = re.search(rf'#define {name} (0x[0-9a-fA-F]+|\d+)', hdr)
         assert m and int(m.group(1).rstrip('u'), 0) == val, name
     lib = _lib.load()

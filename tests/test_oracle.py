@@ -169,3 +169,52 @@ def test_known_answers_a():
         assert check(t, t_exp)
         if reg_exp is not None:
             assert check(reg, reg_exp)
+
+
+# ---- reference-mode options: ftype=float32 and invalid=True (make_golden.py api fixtures) -----
+
+def test_solvers_f32_vs_reference(sqrt_mode):
+    """The float32 solvers (raytracer.py:248-552 with ftype=float32) bit for bit with MKL vsSqrt.
+    With IEEE sqrt (the GPU's) ~3 % of sphere / cone distances differ: torch's float32 sqrt is
+    not correctly rounded on ~0.6 % of its inputs, and t = tc -+ sqrt(R^2 - d^2) resp.
+    (-b +- sqrt(delta)) / 2a amplify that ulp near grazing incidence (up to ~64 / ~200 ulp of t,
+    < 1e-4 absolute here); regions and crossing signs are unaffected."""
+    z = gc.load('solvers_f32')
+    g = oracle.Grid.from_boundaries(z['r_b'], z['e_b'], z['a_b'], ftype='float32')
+    for fam, key in enumerate('rea'):
+        t, reg, neg = oracle.solve(g, fam, z['xs'], z['rays'])
+        assert t.dtype == np.float32
+        rt = z[f'{key}_t']
+        assert np.array_equal(np.isfinite(t), np.isfinite(rt)), key
+        assert np.array_equal(reg, z[f'{key}_reg']), key
+        assert np.array_equal(neg, z[f'{key}_neg']), key
+        fin = np.isfinite(rt)
+        if sqrt_mode:
+            assert np.array_equal(t, rt), f'{key}: not bit-exact with MKL sqrt'
+        else:
+            assert np.abs(t[fin].astype(np.float64) - rt[fin]).max() <= 1e-4, key
+            assert np.array_equal(t[~fin], rt[~fin])
+
+
+@pytest.mark.parametrize('name', gc.F32_CASES + gc.INVALID_CASES)
+def test_reference_mode_trace_vs_reference(name, sqrt_mode):
+    """Operator(..., ftype=float32) / Operator(..., invalid=True) traces: the reference's dense
+    (regs, lens), entry for entry with MKL sqrt (float32: the solvers each normalise their own
+    float32 copy of the float64 rays, raytracer.py:276,360,500); with IEEE sqrt the same regions
+    and lengths within float32 resolution (float64: 1e-12)."""
+    case = gc.load(name)
+    f32 = name in gc.F32_CASES
+    g = oracle.Grid.from_boundaries(case['r_b'], case['e_b'], case['a_b'],
+                                    ftype='float32' if f32 else 'float64')
+    regs, lens = oracle.trace_dense(g, case['xs'], case['rays'], gc.ref_mode_starts(case, f32),
+                                    invalid=not f32)
+    rr, rl = case['dense_regs'], case['dense_lens']
+    regs, lens = regs.reshape(rr.shape), lens.reshape(rl.shape)
+    assert np.array_equal(regs, rr), name
+    if sqrt_mode:
+        assert np.array_equal(lens, rl, equal_nan=True), f'{name}: not bit-exact with MKL sqrt'
+    else:
+        fin = np.isfinite(rl)
+        assert np.array_equal(np.isfinite(lens), fin)
+        tol = (1e-6 if f32 else 1e-12) * gc.scale_of(case)
+        assert np.abs(lens[fin] - rl[fin]).max() <= tol
