@@ -199,7 +199,9 @@ int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const doubl
  * segment.
  * Per-segment arrays (vox, len, len32, loc) are read in aligned 8- or 16-entry chunks: allocate
  * them to round_up(n_segments, 16) entries (the entries past n_segments are never used).  `len32` is
- * the float32 copy of `len` used by the float32 forward (sphrt_f64_to_f32). */
+ * the float32 copy of `len` used by the float32 forward: sphrt_csr_local_count / _build write it
+ * (len32[i] = (float)len[i], every segment) when both len and len32 are set, else the caller makes
+ * it (sphrt_f64_to_f32). */
 #define SPHRT_ROW_HEAD 0x80000000u
 #define SPHRT_BLOCK_FIELDS 6   /* int64 per entry of blocks */
 #define SPHRT_LOC_HEAD 0x8000u

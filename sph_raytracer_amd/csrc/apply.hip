@@ -480,6 +480,30 @@ __global__ __launch_bounds__(256) void stage_pack_kernel(const T* __restrict__ s
 // than segments) and the segments read LDS.  n_tab = -1 marks a workgroup left on the
 // per-segment gather (more than kLocalMax segments or kMaxGran granules).
 
+// The float32 lengths (sphrt_csr.len32) written by the table launch that decides the tables
+// (count / build), one block's segments per workgroup: the float32 forward's stream without a
+// pass of its own over the float64 lengths (C3: f64_to_f32_kernel 0.25 ms).  The common block
+// (<= 8 * kThreads segments) issues its eight loads before any store.
+__device__ __forceinline__ void copy_len32(const double* __restrict__ len, float* __restrict__ len32,
+                                           int64_t s0, int64_t n) {
+    const int tid = threadIdx.x;
+    if (n <= 8 * kThreads) {
+        double v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int p = i * kThreads + tid;
+            v[i] = p < n ? len[s0 + p] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int p = i * kThreads + tid;
+            if (p < n) len32[s0 + p] = (float)v[i];
+        }
+        return;
+    }
+    for (int64_t p = tid; p < n; p += kThreads) len32[s0 + p] = (float)len[s0 + p];
+}
+
 // The tables from a bitmap of the volume's granules in LDS, when the
 // bitmap is small (n_cols/4 bits; 128^3 voxels = 64 KiB): set one bit per segment, prefix-popcount
 // the words, and a granule's rank is the number of set bits below it.  O(segments + words) per
@@ -488,7 +512,7 @@ template <int TM, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int n_words, StageMap sm,
-    unsigned long long* stats) {
+    unsigned long long* stats, const double* __restrict__ len, float* __restrict__ len32) {
     extern __shared__ __attribute__((aligned(16))) unsigned char bm_lds[];
     uint32_t* bm = reinterpret_cast<uint32_t*>(bm_lds);     // n_words bitmap words
     int32_t* pre = reinterpret_cast<int32_t*>(bm + n_words);  // set bits before each word
@@ -498,6 +522,7 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
     if (TM == kTabFill && m[5] < 0) return;
     const int tid = threadIdx.x;
     const int64_t n = s1 - s0;
+    if (TM != kTabFill && len32) copy_len32(len, len32, s0, n);
     if (n > kLocalMax) {
         if (TM != kTabFill && tid == 0) {
             m[5] = -1;
@@ -654,7 +679,7 @@ template <int TM, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
-    unsigned long long* stats) {
+    unsigned long long* stats, const double* __restrict__ len, float* __restrict__ len32) {
     __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, 8>()];
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
@@ -662,6 +687,8 @@ __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_k
     const int64_t s0 = m[2], s1 = m[3];
     if (TM == kTabFill && m[5] < 0) return;
     const int64_t n = s1 - s0;
+    // every block's lengths, whichever launch then builds its table (or none)
+    if (TM != kTabFill && len32) copy_len32(len, len32, s0, n);
     if (n > kLocalMax) {
         if (TM != kTabFill && threadIdx.x == 0) {
             m[5] = -1;
@@ -1481,6 +1508,12 @@ extern "C" int sphrt_diag_fwd_stamps(unsigned long long* host, int64_t n) {
 }
 #endif
 
+// The float32 lengths a count / build launch writes: len32 when the caller set it with len
+// (sphrt.h: the table launch then fills the float32 copy), else none.
+static float* len32_out(const sphrt_csr* c) {
+    return c->len && c->len32 ? const_cast<float*>(c->len32) : nullptr;
+}
+
 // bitmap words for a volume of n_cols voxels, or 0 when the bitmap costs more than sorting the
 // workgroup's segments (every workgroup clears and scans the whole bitmap: <= 4096 words, i.e.
 // volumes up to 2^19 voxels; larger ones take the radix sort)
@@ -1498,9 +1531,10 @@ static int granule_key_bits(int64_t n_cols) {
 template <int TM, typename TabT>
 static int launch_tables(unsigned nb, hipStream_t st, int64_t* blocks, const int32_t* vox,
                          uint16_t* loc, TabT* tab, int64_t stride, int kb, const StageMap& sm,
-                         unsigned long long* stats) {
+                         unsigned long long* stats, const double* len = nullptr,
+                         float* len32 = nullptr) {
     hipLaunchKernelGGL((local_table_radix_kernel<TM, TabT>), dim3(nb), dim3(kThreads), 0, st,
-                       blocks, vox, loc, tab, stride, kb, sm, stats);
+                       blocks, vox, loc, tab, stride, kb, sm, stats, len, len32);
     hipLaunchKernelGGL((local_table_big_kernel<TM, TabT>), dim3((nb + kBigScan - 1) / kBigScan),
                        dim3(kThreads), 0, st, blocks, (int64_t)nb, vox, loc, tab, stride, kb, sm,
                        stats);
@@ -1522,12 +1556,12 @@ extern "C" int sphrt_csr_local_count(const sphrt_csr* c, int64_t* blocks, int64_
     if (const int words = table_bitmap_words(cols)) {
         hipLaunchKernelGGL((local_table_bitmap_kernel<kTabCount, int32_t>), dim3((unsigned)c->n_blocks),
                            dim3(kThreads), (size_t)words * 8, st, blocks, c->vox, nullptr, nullptr,
-                           0, words, sm, (unsigned long long*)stats);
+                           0, words, sm, (unsigned long long*)stats, c->len, len32_out(c));
         return check_launch("local_table_bitmap_kernel<count>");
     }
     return launch_tables<kTabCount, int32_t>((unsigned)c->n_blocks, st, blocks,
                                              c->vox, nullptr, nullptr, 0, granule_key_bits(cols),
-                                             sm, (unsigned long long*)stats);
+                                             sm, (unsigned long long*)stats, c->len, len32_out(c));
 }
 
 extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, uint16_t* loc,
@@ -1548,11 +1582,11 @@ extern "C" int sphrt_csr_local_fill(const sphrt_csr* c, const int64_t* blocks, u
         if (u16)
             hipLaunchKernelGGL((local_table_bitmap_kernel<kTabFill, uint16_t>), dim3((unsigned)c->n_blocks),
                                dim3(kThreads), (size_t)words * 8, st, (int64_t*)blocks, c->vox, loc,
-                               (uint16_t*)tab, tab_stride, words, sm, nullptr);
+                               (uint16_t*)tab, tab_stride, words, sm, nullptr, nullptr, nullptr);
         else
             hipLaunchKernelGGL((local_table_bitmap_kernel<kTabFill, int32_t>), dim3((unsigned)c->n_blocks),
                                dim3(kThreads), (size_t)words * 8, st, (int64_t*)blocks, c->vox, loc,
-                               (int32_t*)tab, tab_stride, words, sm, nullptr);
+                               (int32_t*)tab, tab_stride, words, sm, nullptr, nullptr, nullptr);
         return check_launch("local_table_bitmap_kernel<fill>");
     }
     const int kb = granule_key_bits(cols);
@@ -1585,18 +1619,22 @@ extern "C" int sphrt_csr_local_build(const sphrt_csr* c, int64_t* blocks, uint16
         const size_t lds = (size_t)words * 8;
         if (u16)
             hipLaunchKernelGGL((local_table_bitmap_kernel<kTabBuild, uint16_t>), g, b, lds, st,
-                               blocks, c->vox, loc, (uint16_t*)tab_wide, kTabWide, words, sm, s);
+                               blocks, c->vox, loc, (uint16_t*)tab_wide, kTabWide, words, sm, s,
+                               c->len, len32_out(c));
         else
             hipLaunchKernelGGL((local_table_bitmap_kernel<kTabBuild, int32_t>), g, b, lds, st,
-                               blocks, c->vox, loc, (int32_t*)tab_wide, kTabWide, words, sm, s);
+                               blocks, c->vox, loc, (int32_t*)tab_wide, kTabWide, words, sm, s,
+                               c->len, len32_out(c));
         return check_launch("local_table_bitmap_kernel<build>");
     }
     const int kb = granule_key_bits(cols);
     if (u16)
         return launch_tables<kTabBuild, uint16_t>(g.x, st, blocks, c->vox, loc,
-                                                  (uint16_t*)tab_wide, kTabWide, kb, sm, s);
+                                                  (uint16_t*)tab_wide, kTabWide, kb, sm, s, c->len,
+                                                  len32_out(c));
     return launch_tables<kTabBuild, int32_t>(g.x, st, blocks, c->vox, loc,
-                                             (int32_t*)tab_wide, kTabWide, kb, sm, s);
+                                             (int32_t*)tab_wide, kTabWide, kb, sm, s, c->len,
+                                             len32_out(c));
 }
 
 extern "C" int sphrt_csr_local_pack(const sphrt_csr* c, const int64_t* blocks,

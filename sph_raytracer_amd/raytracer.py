@@ -891,13 +891,15 @@ class Operator:
         c = _lib.CSR()
         c.n_rays, c.n_segments, c.n_blocks = n, total, nblocks
         c.row_ptr, c.vox, c.len = row_ptr.data_ptr(), vox.data_ptr(), seg_len.data_ptr()
-        c.row_ray, c.blocks, c.len32 = row_ray.data_ptr(), blocks.data_ptr(), None
+        # the float32 lengths come with the granule tables (sphrt_csr_local_build writes len32)
+        len32 = tr.empty(seg_len.shape, dtype=tr.float32, device=dev)
+        c.row_ray, c.blocks, c.len32 = row_ray.data_ptr(), blocks.data_ptr(), len32.data_ptr()
         c.empty_ray = empty_ray.data_ptr()
         c.n_cols = math.prod(self.grid.shape[-3:])
         shape3 = tuple(int(v) for v in self.grid.shape[-3:])
         _set_stage(c, shape3, _stage_brick(nblocks))
         loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
-        self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, row_ray=row_ray,
+        self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, len32=len32, row_ray=row_ray,
                          empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, runs=runs,
                          nblocks=nblocks, n=n, total=total, desc=c, ray_id=ray_id)
         self._batch = batch
@@ -964,18 +966,10 @@ class Operator:
 
     def _lengths(self, dtype):
         """Segment lengths as streamed by the forward kernel: the float64 trace, or (float32
-        path) a float32 copy made once — half the bytes, <=6e-8 relative rounding."""
+        path) its float32 copy — half the bytes, <=6e-8 relative rounding — written by the
+        granule-table launch (no pass of its own: C3 f64_to_f32_kernel 0.25 ms)."""
         csr = self._csr
-        if dtype == tr.float64:
-            return csr['len']
-        if 'len32' not in csr:
-            l32 = tr.empty(csr['len'].shape, dtype=tr.float32, device=self._cdev)
-            _lib.check(_lib.load().sphrt_f64_to_f32(_lib.ptr(csr['len']), _lib.ptr(l32),
-                                                     csr['len'].numel(), _lib.stream_of(self._cdev)),
-                       'sphrt_f64_to_f32')
-            csr['len32'] = l32
-            csr['desc'].len32 = l32.data_ptr()
-        return csr['len32']
+        return csr['len'] if dtype == tr.float64 else csr['len32']
 
     def _launch_args(self, d, n_chan, div):
         """(csr desc, n_chan, chan_stride, div) of the launch for density d: a view <-> time
@@ -1102,9 +1096,7 @@ class Operator:
                                        _lib.ptr(vox_list), _lib.ptr(empty_vox), _lib.ptr(blocks),
                                        nblocks, None, _lib.ptr(iws), stream),
                    'sphrt_csr_index(T)')
-        t_len32 = tr.empty(t_len.shape, dtype=tr.float32, device=dev)
-        _lib.check(lib.sphrt_f64_to_f32(_lib.ptr(t_len), _lib.ptr(t_len32), t_len.numel(), stream),
-                   'sphrt_f64_to_f32')
+        t_len32 = tr.empty(t_len.shape, dtype=tr.float32, device=dev)   # (filled with the tables)
         c = _lib.CSR()
         c.n_rays, c.n_segments, c.n_blocks = n_vox, total, nblocks
         c.row_ptr, c.vox, c.len, c.len32 = (col_ptr.data_ptr(), t_ray.data_ptr(),
@@ -1145,7 +1137,9 @@ class Operator:
         c.vox, c.blocks, c.n_cols = vox_p.data_ptr(), blocks_p.data_ptr(), T * vol
         c.order |= 2        # disjoint slices per view: one contiguous block range per XCD (sphrt.h)
         c.loc, c.tab, c.tab_stride, c.n_fallback = None, None, 0, 0
+        l32, c.len32 = c.len32, None                # (the trace's float32 lengths: made already)
         loc, tab, runs = _local_tables(lib, c, blocks_p, nblocks, total, dev, stream)
+        c.len32 = l32
         csr[key] = dict(desc=c, keep=(vox_p, blocks_p, loc, tab, runs), n_t=T)
         return csr[key]
 
