@@ -257,7 +257,9 @@ __device__ __forceinline__ void plane_solve(const GridDev& G, const RayGeoT<F>& 
     int ng = cz < z ? 1 : 0;
     int r = j - ng;
     if (G.a_wrap) {
-        r %= G.na;
+        // regions % na (raytracer.py:529, Python's modulo) for r = j - ng in [-1, na]: two
+        // selects instead of an integer division by a runtime divisor
+        if (r == G.na) r = 0;
         if (r < 0) r += G.na;
     } else if (r == G.na) {
         r = -1;

@@ -54,6 +54,22 @@ __device__ unsigned long long g_trace_cycles[16];   // 8..12: exact_wave_kernel
 #endif
 constexpr size_t kLdsBytes = 160 * 1024;        // LDS per CU; one workgroup may take all of it
 
+// Ablation builds only (-DSPHRT_TRACE_ABL=k, tools/pmc_trace.py --ablate): trace_one stops after
+// phase k (1 solve + list, 2 sort, 3 tie check, 4 fill) with a zero segment count — wrong results
+// by design; the PMC difference between consecutive k is the phase's instruction count.
+#ifdef SPHRT_TRACE_ABL
+#define TRACE_ABL(k)                                                                          \
+    do {                                                                                      \
+        if (SPHRT_TRACE_ABL == (k)) {                                                         \
+            if ((MODE == MODE_COUNT || MODE == MODE_EMIT) && lane == 0) o.counts[ray] = 0;    \
+            wave_sync();                                                                      \
+            return;                                                                           \
+        }                                                                                     \
+    } while (0)
+#else
+#define TRACE_ABL(k) do {} while (0)
+#endif
+
 #ifndef SPHRT_SORT_INLINE
 #define SPHRT_SORT_INLINE
 #endif
@@ -106,6 +122,12 @@ __device__ __forceinline__ int scan_last(int v, int /*lane*/) {
 // xlane<X>(x): the value x holds in lane (lane ^ X), X a compile-time constant: DPP quad
 // permutes and row (half-)mirrors inside 16 lanes, row shifts for xor 4 / 8, a swizzle for
 // xor 16 / 31 inside 32 lanes, the gfx950 32-lane swap for xor 32.
+// xor 4 / 8 through ds_swizzle (the LDS crossbar, no VALU issue) instead of two row shifts and a
+// select (three VALU instructions per dword).  Trace kernel, same box, round 4: C3 3126 -> 3113,
+// C5 525 -> 520, C2 124.6 -> 122.4 us (profiles/r04_trace_ab.txt); 0 restores the row shifts.
+#ifndef SPHRT_XLANE_SWZ
+#define SPHRT_XLANE_SWZ 1
+#endif
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
@@ -117,10 +139,10 @@ __device__ __forceinline__ uint32_t xlane(uint32_t x, int lane) {
     else if constexpr (X == 3) return dpp_mov<0x1B>(x);            // quad_perm [3,2,1,0]
     else if constexpr (X == 7) return dpp_mov<0x141>(x);           // row_half_mirror
     else if constexpr (X == 15) return dpp_mov<0x140>(x);          // row_mirror
-    else if constexpr (X == 4 || X == 8) {                         // row_shl / row_shr by X
+    else if constexpr ((X == 4 || X == 8) && !SPHRT_XLANE_SWZ) {  // row_shl / row_shr by X
         const uint32_t up = dpp_mov<0x100 + X>(x), dn = dpp_mov<0x110 + X>(x);
         return (lane & X) ? dn : up;
-    } else if constexpr (X == 16 || X == 31) {
+    } else if constexpr (X == 4 || X == 8 || X == 16 || X == 31) {
         return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (X << 10) | 0x1F);
     } else if constexpr (X == 32) {
         const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
@@ -481,9 +503,15 @@ struct FillState {
     int r0, e0, a0;        // rows before the first entry
     int r_lim, e_lim, start_c;
 };
-template <int M, bool STORE>
+// STORE: kFillNone (count only), kFillLds (the segments compacted into seg_len / seg_vox in LDS,
+// for the no-store forward and the LDS-list path), kFillGlobal (straight from the registers into
+// the CSR: seg_len / seg_vox are the output arrays, the ray's segments start at gbase; stored only
+// when head + count <= gcap — an emit slot that fits; no LDS round trip, no copy loop).
+enum { kFillNone = 0, kFillLds = 1, kFillGlobal = 2 };
+template <int M, int STORE>
 __device__ SPHRT_SORT_INLINE int fill_regs(const GridDev& G, const uint64_t* keys, const uint32_t* pays, int F,
-                         int lane, const FillState& fs, double* seg_len, int32_t* seg_vox) {
+                         int lane, const FillState& fs, double* seg_len, int32_t* seg_vox,
+                         int64_t gbase = 0, int64_t gcap = 0, int head = 0) {
     uint64_t kb[M];
     int ur[M], ue[M], ua[M];
 #pragma unroll
@@ -541,7 +569,7 @@ __device__ SPHRT_SORT_INLINE int fill_regs(const GridDev& G, const uint64_t* key
     }
     const int incl = wave_scan(cnt, 0, [](int x, int y) { return x + y; });
     const int total = __builtin_amdgcn_readlane(incl, 63);
-    if (STORE) {
+    if (STORE == kFillLds) {
         wave_sync();
         int pos = incl - cnt;
 #pragma unroll
@@ -553,6 +581,16 @@ __device__ SPHRT_SORT_INLINE int fill_regs(const GridDev& G, const uint64_t* key
             }
         }
         wave_sync();
+    } else if (STORE == kFillGlobal && head + total <= gcap) {
+        int64_t pos = gbase + (incl - cnt);
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+            if (ok[i]) {
+                seg_len[pos] = len[i];
+                seg_vox[pos] = vox[i];
+                ++pos;
+            }
+        }
     }
     return total;
 }
@@ -830,6 +868,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     wave_sync();
 
     // ---- 2. sort by (distance, candidate) ------------------------------------------------
+    TRACE_ABL(1);
     TRACE_T(ts1);
     TRACE_ADD(0, ts0, ts1);
     int sflags = 2;          // bit 0: repair the order; bit 1: look for ambiguous ties
@@ -850,6 +889,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     }
     if (sflags & 1) fix_near_ties(keys, pays, F, lane);
 
+    TRACE_ABL(2);
     TRACE_T(ts2);
     TRACE_ADD(1, ts1, ts2);
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe, start_c = G.K - 1;
@@ -864,6 +904,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     }
 
     // ---- 3. forward fill, lengths, compaction ----------------------------------------------
+    TRACE_ABL(3);
     TRACE_T(ts3);
     TRACE_ADD(2, ts2, ts3);
     // every distance behind the start is integrated in the start voxel (raytracer.py:126,140)
@@ -872,13 +913,19 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     int32_t* seg_vox = reinterpret_cast<int32_t*>(pays);
     int cr = sr, cE = e_in, cA = a_in;  // state before the first sorted entry
     int nseg = 0;
-    constexpr bool kStore = MODE != MODE_COUNT;
+    // FILL / EMIT: lists in registers store their segments straight into the CSR slot
+    constexpr bool kDirect = MODE == MODE_FILL || MODE == MODE_EMIT;
+    constexpr int kStore = MODE == MODE_COUNT ? kFillNone : kDirect ? kFillGlobal : kFillLds;
     const FillState fs{sr, se, sa, sr, e_in, a_in, r_lim, e_lim, start_c};
     if (!pair_fmt) {                    // F <= 512: the list in registers, lane-major
-        nseg = F <= 64 ? fill_regs<1, kStore>(G, keys, pays, F, lane, fs, seg_len, seg_vox)
-             : F <= 128 ? fill_regs<2, kStore>(G, keys, pays, F, lane, fs, seg_len, seg_vox)
-             : F <= 256 ? fill_regs<4, kStore>(G, keys, pays, F, lane, fs, seg_len, seg_vox)
-                        : fill_regs<8, kStore>(G, keys, pays, F, lane, fs, seg_len, seg_vox);
+        double* sl = kDirect ? o.len : seg_len;
+        int32_t* sv = kDirect ? o.vox : seg_vox;
+        const int64_t gcap = MODE == MODE_EMIT ? slot1 - slot0 : (int64_t)INT_MAX;
+        const int64_t gb = slot0 + head;
+        nseg = F <= 64 ? fill_regs<1, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head)
+             : F <= 128 ? fill_regs<2, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head)
+             : F <= 256 ? fill_regs<4, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head)
+                        : fill_regs<8, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head);
     }
     for (int c0 = 0; pair_fmt && c0 < F; c0 += 64) {
         const int e = c0 + lane;
@@ -930,6 +977,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     }
 
     // ---- 4. emit ---------------------------------------------------------------------------
+    TRACE_ABL(4);
     TRACE_T(ts4);
     TRACE_ADD(3, ts3, ts4);
     if (MODE == MODE_COUNT) {
@@ -946,7 +994,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
             o.vox[r0] = (sr * G.ne + se) * G.na + sa;
             o.len[r0] = -tneg;
         }
-        for (int q = lane; q < nseg; q += 64) {
+        for (int q = lane; pair_fmt && q < nseg; q += 64) {    // (register lists stored already)
             o.vox[r0 + head + q] = seg_vox[q];
             o.len[r0 + head + q] = seg_len[q];
         }
