@@ -278,6 +278,22 @@ int sphrt_csr_local_build(const sphrt_csr *csr, int64_t *blocks, uint16_t *loc, 
                           int64_t *stats, void *stream);
 int sphrt_csr_local_pack(const sphrt_csr *csr, const int64_t *blocks, const void *tab_wide,
                          void *tab, int64_t tab_stride, void *stream);
+/* The one-pass trace without its compaction pass (radix-sorted tables: volumes over 2^19 columns,
+ * one-pass build).  After sphrt_trace_emit the segments sit in staging slots (svox / slen at
+ * slot[row], the scanned bounds); sphrt_csr_index_staged indexes the CSR from row_ptr alone (no
+ * head bits: vox is not written yet) and lists the trace row of every non-empty row (nz_row, one
+ * int32 per non-empty row: allocate n_rays); sphrt_csr_local_build_staged then moves every block's
+ * segments from the staging into csr->vox (with the row-head bits), csr->len and csr->len32 and
+ * builds the tables from them — the same CSR, loc and tables as sphrt_trace_compact +
+ * sphrt_csr_index + sphrt_csr_local_build (csr->vox/len/len32 are written through the const
+ * pointers).  The staging may be freed after it. */
+int sphrt_csr_index_staged(const int64_t *row_ptr, int64_t n_rays, int32_t *row_ray,
+                           int32_t *empty_ray, int64_t *blocks, int64_t n_blocks,
+                           const int32_t *ray_ids, int32_t *nz_row, void *workspace, void *stream);
+int sphrt_csr_local_build_staged(const sphrt_csr *csr, int64_t *blocks, uint16_t *loc,
+                                 void *tab_wide, int64_t *stats, const int64_t *slot,
+                                 const int32_t *nz_row, const int32_t *svox, const double *slen,
+                                 void *stream);
 /* Row runs (optional).  Block b's rows map to rays in runs of consecutive rays, and its share of
  * the empty rays (empty_ray[empty_lo .. empty_hi)) to ranges of consecutive rays; when both fit
  * in SPHRT_MAX_RUNS entries for every block, the table-mode forward takes them from one 128-byte

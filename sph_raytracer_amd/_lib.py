@@ -83,11 +83,15 @@ _SIGNATURES = [
     ('sphrt_csr_blocks', c_i64, [c_i64]),
     ('sphrt_csr_index_workspace_bytes', ctypes.c_size_t, [c_i64]),
     ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    ('sphrt_csr_index_staged', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                                       c_vp]),
     ('sphrt_csr_runs', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp]),
     ('sphrt_csr_local_count', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp]),
     ('sphrt_csr_local_fill', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp]),
     ('sphrt_csr_local_build', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_vp, c_vp]),
     ('sphrt_csr_local_pack', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_i64, c_vp]),
+    ('sphrt_csr_local_build_staged', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp, c_vp, c_vp,
+                                             c_vp, c_vp, c_vp, c_vp]),
     ('sphrt_csr_time_columns', c_int, [ctypes.POINTER(CSR), c_i64, c_i64, c_vp, c_vp]),
     ('sphrt_forward_f32', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,
                                   c_vp]),

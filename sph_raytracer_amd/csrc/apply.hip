@@ -90,18 +90,22 @@ __global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* row_ptr, 
     const int64_t a = row_ptr[r];
     const bool ne = row_ptr[r + 1] > a;
     nonempty[r] = ne ? 1 : 0;
-    if (ne) vox[a] = (int32_t)((uint32_t)vox[a] | kHead);
+    if (ne && vox) vox[a] = (int32_t)((uint32_t)vox[a] | kHead);
 }
 
 __global__ __launch_bounds__(256) void row_list_kernel(const int64_t* row_ptr,
                                                        const int64_t* row_pre, int64_t n,
                                                        const int32_t* ray_ids, int32_t* row_ray,
-                                                       int32_t* empty_ray) {
+                                                       int32_t* empty_ray, int32_t* nz_row) {
     const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (r >= n) return;
     const int32_t id = ray_ids ? ray_ids[r] : (int32_t)r;   // the ray (output index) of row r
-    if (row_ptr[r + 1] > row_ptr[r]) row_ray[row_pre[r]] = id;
-    else empty_ray[r - row_pre[r]] = id;
+    if (row_ptr[r + 1] > row_ptr[r]) {
+        row_ray[row_pre[r]] = id;
+        if (nz_row) nz_row[row_pre[r]] = (int32_t)r;          // (staged index: the row itself)
+    } else {
+        empty_ray[r - row_pre[r]] = id;
+    }
 }
 
 __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
@@ -596,12 +600,15 @@ struct RadixTable {
 };
 
 // One block's table from a sort of its n <= ITEMS * kThreads segments (block-uniform call).
+// xin: the block's voxels already in registers (xin[i]: segment ITEMS * t + i, the staged
+// gather), else loaded from vox.
 template <int ITEMS, int TM, typename TabT>
 __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restrict__ vox,
                                             uint16_t* __restrict__ loc, TabT* __restrict__ tab_b,
                                             int64_t s0, int n, int key_bits, const StageMap& sm,
                                             unsigned char* ts_raw, uint32_t* last_key,
-                                            ScanShared& sh, unsigned long long* stats) {
+                                            ScanShared& sh, unsigned long long* stats,
+                                            const uint32_t* xin = nullptr) {
     using RT = RadixTable<ITEMS, TM>;
     auto& ts = *reinterpret_cast<typename RT::Storage*>(ts_raw);
     const int tid = threadIdx.x;
@@ -613,7 +620,7 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
         key[i] = 0xffffffffu;                     // padding sorts last
         val[i] = 0;
         if (p < n) {
-            const uint32_t x = (uint32_t)vox[s0 + p];
+            const uint32_t x = xin ? xin[i] : (uint32_t)vox[s0 + p];
             const uint32_t v = stage_col(x & ~kHead, sm);
             key[i] = v >> 2;
             val[i] = (uint16_t)((p << 3) | ((x >> 31) << 2) | (v & 3u));
@@ -675,20 +682,105 @@ template <int TM, typename TabT, int ITEMS>
 constexpr size_t table_lds() {
     return sizeof(typename RadixTable<ITEMS, TM>::Storage);
 }
+// A one-pass trace's segments still in their staging slots (sphrt_trace_emit): the table build
+// that reads them moves them into the CSR itself (sphrt_csr_local_build_staged) — no separate
+// compaction pass (C3 compact_kernel 0.68 ms) and no second read of the voxels.
+struct Staged {
+    const int64_t* row_ptr;   // CSR row starts (the trace's rows)
+    const int64_t* slot;      // staging slot starts (the scanned bounds)
+    const int32_t* nz_row;    // the trace row of each non-empty row (sphrt_csr_index_staged)
+    int64_t n_rays;           // rows (empty ones included)
+    const int32_t* svox;      // staging voxels and lengths
+    const double* slen;
+    int32_t* vox;             // the CSR: voxels (with the row-head bits), lengths, float32 lengths
+    double* len;
+    float* len32;
+};
+constexpr int kStagedRows = (int)kSegPerBlock + 1;   // a block's rows start in its window
+constexpr size_t kStagedLds = (size_t)kStagedRows * (sizeof(int32_t) + sizeof(int64_t)) + 16;
+
+// Block b's gather: its rows (non-empty rows [k0, k1), each starting in the block's window) as
+// (start - s0, slot - start) in LDS, then segment p of the block reads staging slot
+// s0 + p + delta(row of p).  Blocks of <= 8 * kThreads segments: thread t gathers segments
+// 8t .. 8t + 7 (one binary search, then a forward walk); larger ones search per segment.
+// Writes vox (head bit on each row's first segment), len and len32, and hands the common block's
+// voxels to the table build in registers (xs[i]: segment 8t + i; nothing is read back).
+__device__ __forceinline__ void staged_gather(const Staged& S, const int64_t* blocks, int64_t nb,
+                                              int64_t b, int64_t s0, int64_t n,
+                                              unsigned char* lds, uint32_t (&xs)[8]) {
+    const int tid = threadIdx.x;
+    const int64_t k0 = blocks[kBlockFields * b + 4];
+    // (the last block's rows end at the non-empty row count: rays minus the empty list's end)
+    const int64_t k1 = b + 1 < nb ? blocks[kBlockFields * (b + 1) + 4]
+                                  : S.n_rays - blocks[kBlockFields * (nb - 1) + 1];
+    const int nrow = (int)(k1 - k0);
+    int32_t* rs = reinterpret_cast<int32_t*>(lds);
+    int64_t* rd = reinterpret_cast<int64_t*>(lds + (((size_t)(nrow + 1) * 4 + 7) & ~(size_t)7));
+    for (int t = tid; t < nrow; t += kThreads) {
+        const int64_t r = S.nz_row[k0 + t];
+        const int64_t a = S.row_ptr[r];
+        rs[t] = (int32_t)(a - s0);
+        rd[t] = S.slot[r] - a;
+    }
+    if (tid == 0) rs[nrow] = (int32_t)n;          // sentinel: the end of the last row
+    __syncthreads();
+    auto row_of = [&](int p) {                    // last row t with rs[t] <= p
+        int lo = 0, hi = nrow - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (rs[mid] <= p) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    auto move = [&](int p, int row) {
+        const int64_t src = s0 + p + rd[row];
+        const uint32_t v = (uint32_t)S.svox[src];
+        const double l = S.slen[src];
+        const uint32_t x = p == rs[row] ? (v | kHead) : v;
+        S.vox[s0 + p] = (int32_t)x;
+        S.len[s0 + p] = l;
+        S.len32[s0 + p] = (float)l;
+        return x;
+    };
+    if (n <= 8 * kThreads) {
+        const int p0 = tid * 8;
+        int row = p0 < n ? row_of(p0) : 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int p = p0 + i;
+            xs[i] = 0u;
+            if (p < n) {
+                while (rs[row + 1] <= p) ++row;
+                xs[i] = move(p, row);
+            }
+        }
+    } else {
+        for (int p = tid; p < n; p += kThreads) move(p, row_of(p));
+    }
+    __syncthreads();                              // (the LDS is reused by the table build)
+}
+
 template <int TM, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
-    unsigned long long* stats, const double* __restrict__ len, float* __restrict__ len32) {
-    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, 8>()];
+    unsigned long long* stats, const double* __restrict__ len, float* __restrict__ len32,
+    Staged S = Staged{}, int64_t n_blocks = 0) {
+    constexpr size_t kSortLds = table_lds<TM, TabT, 8>();
+    __shared__ __attribute__((aligned(16)))
+    unsigned char ts_raw[kSortLds > kStagedLds ? kSortLds : kStagedLds];
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
     int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
     const int64_t s0 = m[2], s1 = m[3];
     if (TM == kTabFill && m[5] < 0) return;
     const int64_t n = s1 - s0;
-    // every block's lengths, whichever launch then builds its table (or none)
-    if (TM != kTabFill && len32) copy_len32(len, len32, s0, n);
+    // every block's segments / lengths, whichever launch then builds its table (or none)
+    uint32_t xs[8];
+    const bool staged = TM == kTabBuild && S.svox;
+    if (staged) staged_gather(S, blocks, n_blocks, blockIdx.x, s0, n, ts_raw, xs);
+    else if (TM != kTabFill && len32) copy_len32(len, len32, s0, n);
     if (n > kLocalMax) {
         if (TM != kTabFill && threadIdx.x == 0) {
             m[5] = -1;
@@ -699,7 +791,7 @@ __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_k
     if (n > 8 * kThreads) return;                 // local_table_big_kernel's
     TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
     radix_table<8, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key, sh,
-                             stats);
+                             stats, staged ? xs : nullptr);
 }
 
 // The blocks of 2049..kLocalMax segments: workgroup g looks at blocks [kBigScan g, kBigScan g +
@@ -1461,10 +1553,9 @@ extern "C" size_t sphrt_csr_index_workspace_bytes(int64_t n_rays) {
     return a + b + sphrt_scan_workspace_bytes(n_rays);
 }
 
-extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* vox,
-                               int32_t* row_ray, int32_t* empty_ray, int64_t* blocks,
-                               int64_t n_blocks, const int32_t* ray_ids,
-                               void* workspace, void* stream) {
+static int csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* vox, int32_t* row_ray,
+                     int32_t* empty_ray, int64_t* blocks, int64_t n_blocks,
+                     const int32_t* ray_ids, int32_t* nz_row, void* workspace, void* stream) {
     if (n_rays < 0 || n_blocks < 1) return fail("bad CSR index sizes");
     if (n_rays == 0) return 0;
     StreamGuard guard(stream);
@@ -1478,11 +1569,29 @@ extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* 
     if (int e = check_launch("mark_rows")) return e;
     if (int e = sphrt_scan_counts(flags, n_rays, pre, scan_ws, stream)) return e;
     hipLaunchKernelGGL(row_list_kernel, dim3(g), dim3(256), 0, st, row_ptr, pre, n_rays, ray_ids,
-                       row_ray, empty_ray);
+                       row_ray, empty_ray, nz_row);
     if (int e = check_launch("row_list")) return e;
     hipLaunchKernelGGL(block_meta_kernel, dim3((unsigned)((n_blocks + 255) / 256)), dim3(256), 0,
                        st, row_ptr, pre, n_rays, n_blocks, blocks);
     return check_launch("block_meta");
+}
+
+extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* vox,
+                               int32_t* row_ray, int32_t* empty_ray, int64_t* blocks,
+                               int64_t n_blocks, const int32_t* ray_ids,
+                               void* workspace, void* stream) {
+    if (!vox && n_rays > 0) return fail("null vox");
+    return csr_index(row_ptr, n_rays, vox, row_ray, empty_ray, blocks, n_blocks, ray_ids, nullptr,
+                     workspace, stream);
+}
+
+extern "C" int sphrt_csr_index_staged(const int64_t* row_ptr, int64_t n_rays, int32_t* row_ray,
+                                      int32_t* empty_ray, int64_t* blocks, int64_t n_blocks,
+                                      const int32_t* ray_ids, int32_t* nz_row, void* workspace,
+                                      void* stream) {
+    if (!nz_row && n_rays > 0) return fail("null nz_row");
+    return csr_index(row_ptr, n_rays, nullptr, row_ray, empty_ray, blocks, n_blocks, ray_ids,
+                     nz_row, workspace, stream);
 }
 
 extern "C" int sphrt_csr_runs(const sphrt_csr* c, int32_t* runs, int64_t* stats, void* stream) {
@@ -1532,9 +1641,9 @@ template <int TM, typename TabT>
 static int launch_tables(unsigned nb, hipStream_t st, int64_t* blocks, const int32_t* vox,
                          uint16_t* loc, TabT* tab, int64_t stride, int kb, const StageMap& sm,
                          unsigned long long* stats, const double* len = nullptr,
-                         float* len32 = nullptr) {
+                         float* len32 = nullptr, const Staged& S = Staged{}) {
     hipLaunchKernelGGL((local_table_radix_kernel<TM, TabT>), dim3(nb), dim3(kThreads), 0, st,
-                       blocks, vox, loc, tab, stride, kb, sm, stats, len, len32);
+                       blocks, vox, loc, tab, stride, kb, sm, stats, len, len32, S, (int64_t)nb);
     hipLaunchKernelGGL((local_table_big_kernel<TM, TabT>), dim3((nb + kBigScan - 1) / kBigScan),
                        dim3(kThreads), 0, st, blocks, (int64_t)nb, vox, loc, tab, stride, kb, sm,
                        stats);
@@ -1635,6 +1744,39 @@ extern "C" int sphrt_csr_local_build(const sphrt_csr* c, int64_t* blocks, uint16
     return launch_tables<kTabBuild, int32_t>(g.x, st, blocks, c->vox, loc,
                                              (int32_t*)tab_wide, kTabWide, kb, sm, s, c->len,
                                              len32_out(c));
+}
+
+extern "C" int sphrt_csr_local_build_staged(const sphrt_csr* c, int64_t* blocks, uint16_t* loc,
+                                            void* tab_wide, int64_t* stats, const int64_t* slot,
+                                            const int32_t* nz_row, const int32_t* svox,
+                                            const double* slen,
+                                            void* stream) {
+    if (!c || !c->row_ptr || !c->vox || !c->len || !c->len32 || !blocks || !loc || !tab_wide ||
+        !stats || !slot || !nz_row || !svox || !slen)
+        return fail("incomplete staged CSR for the granule tables");
+    if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
+    StageMap sm;
+    if (!stage_map(c, sm)) return fail("inconsistent brick staging fields");
+    const int64_t cols = table_cols(c);
+    if (table_bitmap_words(cols))
+        return fail("staged table build is for radix-sorted tables (volumes over 2^19 columns)");
+    const bool u16 = c->tab_bytes == 2;
+    if (u16 && (cols + 3) / 4 > 65536) return fail("16-bit granule tables need <= 2^18 columns");
+    StreamGuard guard(stream);
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(stats, 0, 2 * sizeof(int64_t), st) != hipSuccess)
+        return fail("hipMemsetAsync failed");
+    if (c->n_segments == 0) return 0;
+    const Staged S{c->row_ptr, slot, nz_row, c->n_rays, svox, slen, const_cast<int32_t*>(c->vox),
+                   const_cast<double*>(c->len), const_cast<float*>(c->len32)};
+    const int kb = granule_key_bits(cols);
+    unsigned long long* s = (unsigned long long*)stats;
+    const unsigned nb = (unsigned)c->n_blocks;
+    if (u16)
+        return launch_tables<kTabBuild, uint16_t>(nb, st, blocks, c->vox, loc, (uint16_t*)tab_wide,
+                                                  kTabWide, kb, sm, s, nullptr, nullptr, S);
+    return launch_tables<kTabBuild, int32_t>(nb, st, blocks, c->vox, loc, (int32_t*)tab_wide,
+                                             kTabWide, kb, sm, s, nullptr, nullptr, S);
 }
 
 extern "C" int sphrt_csr_local_pack(const sphrt_csr* c, const int64_t* blocks,

@@ -475,7 +475,25 @@ def _seg_alloc(total):
     return max((total + 15) // 16 * 16, 16)
 
 
-def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
+def _tables_one_pass(desc, nblocks, dev):
+    """Whether _local_tables builds in one pass (wide tables fit comfortably in free memory and
+    SPHRT_TABLES is not 'twopass'); decides desc.tab_bytes (16-bit entries when every granule
+    index fits: <= 2^18 columns, half the table bytes the forward streams)."""
+    cols = desc.stage_cols if desc.stage_shape[0] > 0 else desc.n_cols
+    desc.tab_bytes = 2 if (cols + 3) // 4 <= 65536 else 4
+    wide_bytes = nblocks * _lib.TAB_WIDE * desc.tab_bytes
+    return (os.environ.get('SPHRT_TABLES', 'onepass') != 'twopass' and
+            wide_bytes <= 0.3 * tr.cuda.mem_get_info(dev)[0])
+
+
+def _radix_tables(desc):
+    """Tables from a radix sort per block (volumes over 2^19 columns; smaller ones take the
+    bitmap kernel, apply.hip table_bitmap_words)."""
+    cols = desc.stage_cols if desc.stage_shape[0] > 0 else desc.n_cols
+    return ((cols + 3) // 4 + 31) // 32 > 4096
+
+
+def _local_tables(lib, desc, blocks, nblocks, total, dev, stream, staged=None):
     """Per-workgroup granule tables and run records of a CSR; sets desc.loc/.tab/.tab_stride/
     .n_fallback/.runs and returns (loc, tab, runs).  One host sync (the largest table decides
     the stride; the run-record overflow count decides desc.runs).  One pass
@@ -499,15 +517,17 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream):
     else:
         stats[2:].fill_(1)
     loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
-    # 16-bit entries when every granule index fits (<= 2^18 columns): half the table bytes the
-    # forward streams
-    cols = desc.stage_cols if desc.stage_shape[0] > 0 else desc.n_cols
-    desc.tab_bytes = 2 if (cols + 3) // 4 <= 65536 else 4
+    one_pass = staged is not None or _tables_one_pass(desc, nblocks, dev)
     tdt = tr.int16 if desc.tab_bytes == 2 else tr.int32
-    wide_bytes = nblocks * _lib.TAB_WIDE * desc.tab_bytes
-    one_pass = (os.environ.get('SPHRT_TABLES', 'onepass') != 'twopass' and
-                wide_bytes <= 0.3 * tr.cuda.mem_get_info(dev)[0])
-    if one_pass:
+    if staged is not None:      # (the caller checked one_pass and the radix kernel)
+        (bound_ptr, svox, slen), nz_row = staged
+        wide = tr.empty(nblocks * _lib.TAB_WIDE, dtype=tdt, device=dev)
+        _lib.check(lib.sphrt_csr_local_build_staged(desc, _lib.ptr(blocks), _lib.ptr(loc),
+                                                    _lib.ptr(wide), _lib.ptr(stats),
+                                                    _lib.ptr(bound_ptr), _lib.ptr(nz_row),
+                                                    _lib.ptr(svox), _lib.ptr(slen), stream),
+                   'sphrt_csr_local_build_staged')
+    elif one_pass:
         wide = tr.empty(nblocks * _lib.TAB_WIDE, dtype=tdt, device=dev)
         _lib.check(lib.sphrt_csr_local_build(desc, _lib.ptr(blocks), _lib.ptr(loc), _lib.ptr(wide),
                                              _lib.ptr(stats), stream), 'sphrt_csr_local_build')
@@ -624,15 +644,18 @@ def _workspace(lib, plan, n, dev):
 _bound_hook = None   # tests only: callable(bounds) run on the one-pass trace's bounds
 
 
-def _trace_csr(lib, plan, batch, dev, stream):
-    """Trace every ray of `batch` into the segment CSR -> (row_ptr, vox, len, total).
+def _trace_csr(lib, plan, batch, dev, stream, keep_staging=False):
+    """Trace every ray of `batch` into the segment CSR -> (row_ptr, vox, len, total, staging).
 
     One pass (sphrt_trace_bound / _emit / _compact, include/sphrt.h): a geometric upper bound of
     every ray's segment count sizes a staging CSR, every ray is traced once into its slot, and
     the rows are compacted — two host syncs (the bound total; the segment total).  The two-pass
     trace (count, then fill: every ray traced twice, one sync) serves when the staging would
     not fit comfortably in free device memory, when a bound failed (then only the fill pass
-    runs: the counts are exact), and on request (SPHRT_TRACE=twopass)."""
+    runs: the counts are exact), and on request (SPHRT_TRACE=twopass).  keep_staging: a
+    successful one-pass trace returns its staging (bound_ptr, svox, slen) uncompacted, with vox
+    and len None — the caller compacts it (_compact_staging) or lets the table build move the
+    segments (sphrt_csr_local_build_staged); staging is None otherwise."""
     n = batch.n
     counts = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
     row_ptr = tr.empty(n + 1, dtype=tr.int64, device=dev)
@@ -669,23 +692,31 @@ def _trace_csr(lib, plan, batch, dev, stream):
             total, n_over = tr.stack((row_ptr[n], over[0])).tolist()   # host sync 2
             if n_over == 0:
                 del tws, counts, over
-                # voxels and lengths in one pass (one row search per segment for both): peak =
-                # staging + 12 B per segment.  (Two passes, freeing the voxel staging in between,
-                # peaked 4 B per staging slot lower and cost C3 2 x 457 us.)
-                vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
-                seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
-                _lib.check(lib.sphrt_trace_compact(n, _lib.ptr(bound_ptr), _lib.ptr(svox),
-                                                   _lib.ptr(slen), _lib.ptr(row_ptr),
-                                                   _lib.ptr(vox), _lib.ptr(seg_len), stream),
-                           'sphrt_trace_compact')
-                del svox, slen
-                return row_ptr, vox, seg_len, total
+                staging = (bound_ptr, svox, slen)
+                if keep_staging:
+                    return row_ptr, None, None, total, staging
+                return (row_ptr,) + _compact_staging(lib, n, row_ptr, total, staging, dev,
+                                                     stream) + (total, None)
             del svox, slen
-            return (row_ptr,) + fill(total) + (total,)
+            return (row_ptr,) + fill(total) + (total, None)
     _lib.check(lib.sphrt_trace_count(h, d, _lib.ptr(counts), *tw, stream), 'sphrt_trace_count')
     scan(counts, row_ptr)
     total = int(row_ptr[n].item())        # the one host sync of the two-pass trace
-    return (row_ptr,) + fill(total) + (total,)
+    return (row_ptr,) + fill(total) + (total, None)
+
+
+def _compact_staging(lib, n, row_ptr, total, staging, dev, stream):
+    """A one-pass trace's staging -> the tight CSR (vox, len) (sphrt_trace_compact: voxels and
+    lengths in one pass, one row search per segment for both; peak = staging + 12 B per segment.
+    Two passes, freeing the voxel staging in between, peaked 4 B per staging slot lower and cost
+    C3 2 x 457 us)."""
+    bound_ptr, svox, slen = staging
+    vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+    seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
+    _lib.check(lib.sphrt_trace_compact(n, _lib.ptr(bound_ptr), _lib.ptr(svox), _lib.ptr(slen),
+                                       _lib.ptr(row_ptr), _lib.ptr(vox), _lib.ptr(seg_len), stream),
+               'sphrt_trace_compact')
+    return vox, seg_len
 
 
 def line_integrals(grid, geom, density):
@@ -830,8 +861,9 @@ class Operator:
         self._ray_shape = batch.shape
         n = batch.n
         stream = _lib.stream_of(dev)
-        row_ptr, vox, seg_len, total = _trace_csr(lib, self._plan, batch, dev, stream)
-        self._index(lib, dev, batch, row_ptr, vox, seg_len, total, ray_id)
+        row_ptr, vox, seg_len, total, staging = _trace_csr(lib, self._plan, batch, dev, stream,
+                                                           keep_staging=True)
+        self._index(lib, dev, batch, row_ptr, vox, seg_len, total, ray_id, staging)
 
     def _trace_reference(self, dev):
         """Trace in reference mode: every ray through the exact path with the reference's own
@@ -872,33 +904,55 @@ class Operator:
         del tws, counts, ws
         self._index(lib, dev, batch, row_ptr, vox, seg_len, total, None)
 
-    def _index(self, lib, dev, batch, row_ptr, vox, seg_len, total, ray_id):
-        """The apply kernels' row index and granule tables over a traced CSR."""
+    def _index(self, lib, dev, batch, row_ptr, vox, seg_len, total, ray_id, staging=None):
+        """The apply kernels' row index and granule tables over a traced CSR.  With a one-pass
+        trace's staging (vox / seg_len None), grids whose tables are radix-sorted in one pass
+        let the table build move the segments out of the staging (sphrt_csr_local_build_staged:
+        no compaction pass, C3 compact_kernel 0.68 ms); others compact it first."""
         n = batch.n
         stream = _lib.stream_of(dev)
         batch.rays = None        # device ray directions: trace input only (24 B per ray)
-        # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
         nblocks = lib.sphrt_csr_blocks(total)
+        c = _lib.CSR()
+        c.n_rays, c.n_segments, c.n_blocks = n, total, nblocks
+        c.n_cols = math.prod(self.grid.shape[-3:])
+        shape3 = tuple(int(v) for v in self.grid.shape[-3:])
+        _set_stage(c, shape3, _stage_brick(nblocks))
+        staged = (staging is not None and os.environ.get('SPHRT_TABLE_STAGED', '1') != '0' and
+                  _tables_one_pass(c, nblocks, dev) and _radix_tables(c))
+        if staging is not None and not staged:
+            vox, seg_len = _compact_staging(lib, n, row_ptr, total, staging, dev, stream)
+            staging = None
+        elif staged:
+            vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
+            seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
+        # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
         row_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
         empty_ray = tr.empty(n + 1, dtype=tr.int32, device=dev)
         blocks = tr.empty(_lib.BLOCK_FIELDS * nblocks, dtype=tr.int64, device=dev)
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n), dtype=tr.uint8, device=dev)
-        _lib.check(lib.sphrt_csr_index(_lib.ptr(row_ptr), n, _lib.ptr(vox), _lib.ptr(row_ray),
-                                       _lib.ptr(empty_ray), _lib.ptr(blocks), nblocks,
-                                       _lib.ptr(ray_id), _lib.ptr(iws), stream),
-                   'sphrt_csr_index')
+        nz_row = None
+        if staged:      # (head bits and the segments come with the tables)
+            nz_row = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
+            _lib.check(lib.sphrt_csr_index_staged(_lib.ptr(row_ptr), n, _lib.ptr(row_ray),
+                                                  _lib.ptr(empty_ray), _lib.ptr(blocks), nblocks,
+                                                  _lib.ptr(ray_id), _lib.ptr(nz_row),
+                                                  _lib.ptr(iws), stream),
+                       'sphrt_csr_index_staged')
+        else:
+            _lib.check(lib.sphrt_csr_index(_lib.ptr(row_ptr), n, _lib.ptr(vox), _lib.ptr(row_ray),
+                                           _lib.ptr(empty_ray), _lib.ptr(blocks), nblocks,
+                                           _lib.ptr(ray_id), _lib.ptr(iws), stream),
+                       'sphrt_csr_index')
         del iws
-        c = _lib.CSR()
-        c.n_rays, c.n_segments, c.n_blocks = n, total, nblocks
         c.row_ptr, c.vox, c.len = row_ptr.data_ptr(), vox.data_ptr(), seg_len.data_ptr()
         # the float32 lengths come with the granule tables (sphrt_csr_local_build writes len32)
         len32 = tr.empty(seg_len.shape, dtype=tr.float32, device=dev)
         c.row_ray, c.blocks, c.len32 = row_ray.data_ptr(), blocks.data_ptr(), len32.data_ptr()
         c.empty_ray = empty_ray.data_ptr()
-        c.n_cols = math.prod(self.grid.shape[-3:])
-        shape3 = tuple(int(v) for v in self.grid.shape[-3:])
-        _set_stage(c, shape3, _stage_brick(nblocks))
-        loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
+        loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream,
+                                       staged=(staging, nz_row) if staged else None)
+        del staging, nz_row
         self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, len32=len32, row_ray=row_ray,
                          empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, runs=runs,
                          nblocks=nblocks, n=n, total=total, desc=c, ray_id=ray_id)

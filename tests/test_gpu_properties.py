@@ -1179,3 +1179,40 @@ def test_gd_direct_declines_what_it_cannot_run(gpu, monkeypatch):
                                  num_iterations=8, loss_fns=fns, progress_bar=False)
     assert len(calls) == 2 and c1.device == dev1
     assert tr.equal(c1.cpu(), ca.cpu())
+
+
+@pytest.mark.parametrize('case', ['c3_views', 'long_rows'])
+def test_staged_table_build_equals_compaction(case, gpu, monkeypatch):
+    """The one-pass trace's staging moved into the CSR by the table build
+    (sphrt_csr_local_build_staged) equals compacting it first (sphrt_trace_compact +
+    sphrt_csr_index + sphrt_csr_local_build, SPHRT_TABLE_STAGED=0) bit for bit: row pointers,
+    voxels with their head bits, float64 / float32 lengths, blocks, slots and tables; and the
+    forwards agree.  long_rows: a radix-table volume (> 2^19 columns) whose rays of ~5000
+    segments make blocks over 2048 segments (the big-block kernel) and over 4096 (no table)."""
+    from sph_raytracer_amd import ConeRectGeom, Operator, SphericalGrid
+    if case == 'c3_views':
+        grid, geom = _orbit(6, (32, 64), grid_shape=(128, 128, 128))
+    else:
+        grid = SphericalGrid(shape=(2500, 16, 16))
+        geom = ConeRectGeom((6, 8), pos=(3, 0.01, 0.02), fov=(3, 3))
+
+    def build(flag):
+        monkeypatch.setenv('SPHRT_TABLE_STAGED', flag)
+        op = Operator(grid, geom, device=gpu)
+        c = op._csr
+        n_seg = c['total']
+        arrs = {k: c[k][:n_seg].cpu() for k in ('vox', 'len', 'len32', 'loc')}
+        arrs.update(row_ptr=c['row_ptr'].cpu(), blocks=c['blocks'].cpu(), tab=c['tab'].cpu())
+        return op, arrs
+
+    op1, a1 = build('1')
+    op0, a0 = build('0')
+    for k in a0:
+        assert tr.equal(a1[k], a0[k]), k
+    if case == 'long_rows':
+        blocks = a1['blocks'].numpy().reshape(-1, 6)
+        n = blocks[:, 3] - blocks[:, 2]
+        assert (n > 2048).any() and (n > 4096).any()
+    x = tr.rand(grid.shape, dtype=tr.float32, device=gpu)
+    assert tr.equal(op1(x), op0(x))
+    assert tr.equal(op1(x.double()), op0(x.double()))
