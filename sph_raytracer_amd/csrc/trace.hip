@@ -286,6 +286,53 @@ __device__ SPHRT_SORT_INLINE int sort_regs(uint64_t* keys, uint32_t* pays, int F
 // shell run and the padding between, the list is bitonic and one merge stage (log2(64 M)
 // half-cleaner layers) sorts it.  C3 (F ~153, ~88 shell entries): 28 + 8 layers on 2 + 4
 // registers instead of 36 on 4.
+// Merge path (SPHRT_MERGE_PATH): the shell run A (ascending composite keys: keys[Sn-1] ..
+// keys[0], then keys[cap-1], keys[cap-2], ...) and the sorted other entries B (keys[Sn ..
+// Sn+O)) merged by rank — lane L finds how many of A precede output L*M (a binary search along
+// its diagonal), then takes its M outputs in turn — instead of log2(64 M) half-cleaner layers
+// over M registers.  The same sorted sequence whenever A is strictly ascending (merge_sort
+// checks that first and keeps the bitonic merge otherwise: equal shell distances, repeated
+// radii).
+#ifndef SPHRT_MERGE_PATH
+#define SPHRT_MERGE_PATH 0
+#endif
+__device__ __forceinline__ uint64_t shell_run(const uint64_t* keys, int Sn, int cap, int i) {
+    return i < Sn ? keys[Sn - 1 - i] : keys[cap - 1 - (i - Sn)];
+}
+template <int M>
+__device__ __forceinline__ void merge_path(const uint64_t* keys, int F, int Sn, int S, int cap,
+                                           int lane, uint64_t (&k)[M]) {
+    const int O = F - S;
+    const uint64_t* B = keys + Sn;
+    const int p0 = lane * M;
+    int lo = max(0, p0 - O), hi = min(p0, S);
+    while (lo < hi) {                      // first A entry not among the first p0 outputs
+        const int mid = (lo + hi) >> 1;
+        if (shell_run(keys, Sn, cap, mid) < B[p0 - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    int ai = lo, bj = p0 - lo;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        k[i] = ~0ull;
+        if (p0 + i < F) {
+            const uint64_t a = ai < S ? shell_run(keys, Sn, cap, ai) : ~0ull;
+            const uint64_t b = bj < O ? B[bj] : ~0ull;
+            const bool ta = ai < S && (bj >= O || a < b);
+            k[i] = ta ? a : b;
+            ai += ta ? 1 : 0;
+            bj += ta ? 0 : 1;
+        }
+    }
+}
+__device__ __forceinline__ bool shell_run_ascending(const uint64_t* keys, int Sn, int S, int cap,
+                                                    int lane) {
+    bool ok = true;
+    for (int i = lane + 1; i < S; i += 64)
+        ok &= shell_run(keys, Sn, cap, i - 1) < shell_run(keys, Sn, cap, i);
+    return __ballot(!ok) == 0;
+}
+
 template <int M, int M2>
 __device__ SPHRT_SORT_INLINE int merge_sort(uint64_t* keys, uint32_t* pays, int F, int Sn, int Sf, int cap,
                            int lane, uint64_t cmask) {
@@ -308,6 +355,10 @@ __device__ SPHRT_SORT_INLINE int merge_sort(uint64_t* keys, uint32_t* pays, int 
     }
     constexpr int P = 64 * M;
     uint64_t k[M];
+    if (SPHRT_MERGE_PATH && shell_run_ascending(keys, Sn, S, cap, lane)) {
+        merge_path<M>(keys, F, Sn, S, cap, lane, k);
+        return finish_sort<M>(k, keys, pays, F, lane, cmask);
+    }
 #pragma unroll
     for (int i = 0; i < M; ++i) {
         const int e = lane * M + i;
@@ -1065,14 +1116,17 @@ __device__ __forceinline__ double polar(double px, double py, double pz) {
 // double root) and +2 / +4 absorb rounding.  A bound that fails anyway only costs time: the ray
 // is counted in n_over and the caller falls back to the two-pass trace.  Starts inside a voxel
 // get K: the exact (tie) path may split the behind-start stretch at every crossing behind it.
-__device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok) {
+// rb / eb / ab: the grid's boundaries (LDS copies in the screen kernel: the binary searches are
+// chains of dependent loads).
+__device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok, const double* rb,
+                             const double* eb, const double* ab) {
     if (start_ok) return G.K;
     const double R = G.r_outer;
     const double t1c = __builtin_sqrt(R * R - g.dd * g.dd);
     const double ta = fmax(g.tc - t1c, 0.0), tb = g.tc + t1c;
     if (!(tb >= ta)) return 2;                       // (NaN: a miss; behind the start: nothing)
     const double eps = 1e-9;
-    const int n_s = G.nbr - first_ge(G.r_b, G.nbr, g.dd * (1.0 - 1e-12));
+    const int n_s = G.nbr - first_ge(rb, G.nbr, g.dd * (1.0 - 1e-12));
     const double ax = g.x0 + ta * g.w0, ay = g.x1 + ta * g.w1, az = g.x2 + ta * g.w2;
     const double bx = g.x0 + tb * g.w0, by = g.x1 + tb * g.w1, bz = g.x2 + tb * g.w2;
     int b_a = G.nba;
@@ -1088,12 +1142,12 @@ __device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok) {
             // only the shifted windows that can overlap [a_b[0], a_b[nba - 1]] (the others
             // count nothing; one window of margin either side for rounding): three instead of
             // five for the usual [-pi, pi] grid
-            const double a_lo = G.a_b()[0], a_hi = G.a_b()[G.nba - 1];
+            const double a_lo = ab[0], a_hi = ab[G.nba - 1];
             const int k0 = max(-2, (int)__builtin_ceil((a_lo - hi) / two_pi) - 1);
             const int k1 = min(2, (int)__builtin_floor((a_hi - lo) / two_pi) + 1);
             int c = 0;
             for (int k = k0; k <= k1; ++k)
-                c += count_in(G.a_b(), G.nba, lo + k * two_pi, hi + k * two_pi);
+                c += count_in(ab, G.nba, lo + k * two_pi, hi + k * two_pi);
             if (__builtin_isfinite(lo) && __builtin_isfinite(hi)) b_a = min(c + 2, G.nba);
         }
     }
@@ -1106,10 +1160,10 @@ __device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok) {
         int c;
         if (ts > ta && ts < tb) {
             const double th_s = polar(g.x0 + ts * g.w0, g.x1 + ts * g.w1, g.x2 + ts * g.w2);
-            c = count_in(G.e_b(), G.nbe, fmin(th_a, th_s) - m, fmax(th_a, th_s) + m) +
-                count_in(G.e_b(), G.nbe, fmin(th_s, th_b) - m, fmax(th_s, th_b) + m);
+            c = count_in(eb, G.nbe, fmin(th_a, th_s) - m, fmax(th_a, th_s) + m) +
+                count_in(eb, G.nbe, fmin(th_s, th_b) - m, fmax(th_s, th_b) + m);
         } else {
-            c = count_in(G.e_b(), G.nbe, fmin(th_a, th_b) - m, fmax(th_a, th_b) + m);
+            c = count_in(eb, G.nbe, fmin(th_a, th_b) - m, fmax(th_a, th_b) + m);
         }
         if (__builtin_isfinite(th_a) && __builtin_isfinite(th_b)) b_e = min(c + 4, 2 * G.nbe);
     }
@@ -1120,8 +1174,25 @@ __device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok) {
 // in a voxel — otherwise every r-row value stays the (invalid) start region (t1c is NaN for every
 // shell when it is NaN for the outermost: monotone in R; tangents excluded).  Misses get their
 // zero outputs here; hits are appended (wave-aggregated) to the hit list the trace kernel drains.
+// The bound screen stages the grid's boundaries in LDS when they fit (screen_lds_bytes): the
+// bound's binary searches then wait on LDS instead of global memory.
+constexpr int kScreenLdsMax = 4096;   // boundaries (32 KB)
+__host__ __device__ __forceinline__ bool screen_lds(const GridDev& G) {
+    return G.nbr + G.nbe + G.nba <= kScreenLdsMax;
+}
 template <int MODE, typename T>
 __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
+    extern __shared__ double bnd_lds[];
+    const double *rb = G.r_b, *eb = G.e_b(), *ab = G.a_b();
+    if (MODE == MODE_BOUND && screen_lds(G)) {
+        for (int i = threadIdx.x; i < G.nbr; i += 256) bnd_lds[i] = rb[i];
+        for (int i = threadIdx.x; i < G.nbe; i += 256) bnd_lds[G.nbr + i] = eb[i];
+        for (int i = threadIdx.x; i < G.nba; i += 256) bnd_lds[G.nbr + G.nbe + i] = ab[i];
+        __syncthreads();
+        rb = bnd_lds;
+        eb = bnd_lds + G.nbr;
+        ab = bnd_lds + G.nbr + G.nbe;
+    }
     const int lane = threadIdx.x & 63;
     const int64_t ray = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const bool active = ray < R.n;
@@ -1134,7 +1205,7 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
     const bool hit = active && !(!start_r_ok && __builtin_isnan(t1c_outer));
     if (MODE == MODE_BOUND && active)
         o.counts[ray] = hit ? segment_bound(G, g, start_r_ok && s[1] >= 0 && s[1] < G.ne &&
-                                                      s[2] >= 0 && s[2] < G.na)
+                                                      s[2] >= 0 && s[2] < G.na, rb, eb, ab)
                             : 0;
     if (active && !hit) {
         if (MODE == MODE_COUNT) o.counts[ray] = 0;
@@ -1782,8 +1853,10 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     if constexpr (MODE == MODE_EMIT) steps = kTrace;
     if (steps & kScreen) {
         if (hipMemsetAsync(ws, 0, kWsHead, st) != hipSuccess) return fail("memset failed");
+        const size_t slds = MODE == MODE_BOUND && screen_lds(G)
+                                ? (size_t)(G.nbr + G.nbe + G.nba) * sizeof(double) : 0;
         hipLaunchKernelGGL((screen_kernel<MODE, T>), dim3((unsigned)((R.n + 255) / 256)), dim3(256),
-                           0, st, G, R, o);
+                           slds, st, G, R, o);
         if (int e = check_launch("screen_kernel")) return e;
     } else if (hipMemsetAsync(o.n_deferred, 0, sizeof(unsigned long long), st) != hipSuccess) {
         return fail("memset failed");
