@@ -1202,7 +1202,19 @@ def test_staged_table_build_equals_compaction(case, gpu, monkeypatch):
         c = op._csr
         n_seg = c['total']
         arrs = {k: c[k][:n_seg].cpu() for k in ('vox', 'len', 'len32', 'loc')}
-        arrs.update(row_ptr=c['row_ptr'].cpu(), blocks=c['blocks'].cpu(), tab=c['tab'].cpu())
+        arrs.update(row_ptr=c['row_ptr'].cpu(), blocks=c['blocks'].cpu())
+        # the tables' used entries (each block's first n_tab at its stride; the rest is padding)
+        stride, tab = c['desc'].tab_stride, c['tab'].cpu()
+        n_tab = arrs['blocks'].view(-1, 6)[:, 5].tolist()
+        arrs['tab'] = tr.cat([tab[b * stride:b * stride + k] for b, k in enumerate(n_tab)
+                              if k > 0] or [tab[:0]])
+        # slots exist only in blocks with a table (the others gather per segment)
+        bl = arrs['blocks'].view(-1, 6)
+        keep = tr.zeros(n_seg, dtype=tr.bool)
+        for b, k in enumerate(n_tab):
+            if k >= 0:
+                keep[int(bl[b, 2]):int(bl[b, 3])] = True
+        arrs['loc'] = arrs['loc'][keep]
         return op, arrs
 
     op1, a1 = build('1')
