@@ -278,8 +278,7 @@ int sphrt_csr_local_build(const sphrt_csr *csr, int64_t *blocks, uint16_t *loc, 
                           int64_t *stats, void *stream);
 int sphrt_csr_local_pack(const sphrt_csr *csr, const int64_t *blocks, const void *tab_wide,
                          void *tab, int64_t tab_stride, void *stream);
-/* The one-pass trace without its compaction pass (radix-sorted tables: volumes over 2^19 columns,
- * one-pass build).  After sphrt_trace_emit the segments sit in staging slots (svox / slen at
+/* The one-pass trace without its compaction pass (one-pass table build).  After sphrt_trace_emit the segments sit in staging slots (svox / slen at
  * slot[row], the scanned bounds); sphrt_csr_index_staged indexes the CSR from row_ptr alone (no
  * head bits: vox is not written yet) and lists the trace row of every non-empty row (nz_row, one
  * int32 per non-empty row: allocate n_rays); sphrt_csr_local_build_staged then moves every block's

@@ -508,6 +508,103 @@ __device__ __forceinline__ void copy_len32(const double* __restrict__ len, float
     for (int64_t p = tid; p < n; p += kThreads) len32[s0 + p] = (float)len[s0 + p];
 }
 
+// A one-pass trace's segments still in their staging slots (sphrt_trace_emit): the table build
+// that reads them moves them into the CSR itself (sphrt_csr_local_build_staged) — no separate
+// compaction pass (C3 compact_kernel 0.68 ms) and no second read of the voxels.
+struct Staged {
+    const int64_t* row_ptr;   // CSR row starts (the trace's rows)
+    const int64_t* slot;      // staging slot starts (the scanned bounds)
+    const int32_t* nz_row;    // the trace row of each non-empty row (sphrt_csr_index_staged)
+    int64_t n_rays;           // rows (empty ones included)
+    const int32_t* svox;      // staging voxels and lengths
+    const double* slen;
+    int32_t* vox;             // the CSR: voxels (with the row-head bits), lengths, float32 lengths
+    double* len;
+    float* len32;
+};
+constexpr int kStagedRows = (int)kSegPerBlock + 1;   // a block's rows start in its window
+constexpr size_t kStagedLds = (size_t)kStagedRows * (sizeof(int32_t) + sizeof(int64_t)) + 16;
+
+// Block b's gather: its rows (non-empty rows [k0, k1), each starting in the block's window) as
+// (start - s0, slot - start) in LDS when they fit in lds_cap bytes (else read from nz_row /
+// row_ptr / slot in global memory: rare), then segment p of the block reads staging slot
+// s0 + p + delta(row of p) (a binary search over the rows).  Thread t takes segments t,
+// t + kThreads, ... (striped: every load and store instruction covers consecutive segments;
+// thread t taking 8t .. 8t + 7 with one search and a walk measured C3 2.59 ms for gather +
+// tables against 1.22 + 0.68 ms for tables + compaction: stride-8 accesses).  Writes vox (head
+// bit on each row's first segment), len and len32, and hands the block's voxels to the table
+// build in registers when it has at most ITEMS * kThreads segments (xs[i]: segment
+// i * kThreads + t; nothing is read back).
+template <int ITEMS>
+__device__ __forceinline__ void staged_gather(const Staged& S, const int64_t* blocks, int64_t nb,
+                                              int64_t b, int64_t s0, int64_t n,
+                                              unsigned char* lds, size_t lds_cap,
+                                              uint32_t (&xs)[ITEMS]) {
+    const int tid = threadIdx.x;
+    const int64_t k0 = blocks[kBlockFields * b + 4];
+    // (the last block's rows end at the non-empty row count: rays minus the empty list's end)
+    const int64_t k1 = b + 1 < nb ? blocks[kBlockFields * (b + 1) + 4]
+                                  : S.n_rays - blocks[kBlockFields * (nb - 1) + 1];
+    const int nrow = (int)(k1 - k0);
+    const size_t rs_bytes = ((size_t)(nrow + 1) * 4 + 7) & ~(size_t)7;
+    const bool in_lds = rs_bytes + (size_t)nrow * 8 <= lds_cap;     // (block-uniform)
+    int32_t* rs = reinterpret_cast<int32_t*>(lds);
+    int64_t* rd = reinterpret_cast<int64_t*>(lds + rs_bytes);
+    if (in_lds) {
+        for (int t = tid; t < nrow; t += kThreads) {
+            const int64_t r = S.nz_row[k0 + t];
+            const int64_t a = S.row_ptr[r];
+            rs[t] = (int32_t)(a - s0);
+            rd[t] = S.slot[r] - a;
+        }
+        if (tid == 0) rs[nrow] = (int32_t)n;      // sentinel: the end of the last row
+    }
+    __syncthreads();
+    auto start_of = [&](int t) -> int32_t {
+        return in_lds ? rs[t] : (int32_t)(S.row_ptr[S.nz_row[k0 + t]] - s0);
+    };
+    auto row_of = [&](int p) {                    // last row t with start(t) <= p
+        int lo = 0, hi = nrow - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (start_of(mid) <= p) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    auto move = [&](int p, int row) {
+        int32_t st;
+        int64_t dl;
+        if (in_lds) {
+            st = rs[row];
+            dl = rd[row];
+        } else {
+            const int64_t r = S.nz_row[k0 + row];
+            const int64_t a = S.row_ptr[r];
+            st = (int32_t)(a - s0);
+            dl = S.slot[r] - a;
+        }
+        const int64_t src = s0 + p + dl;
+        const uint32_t v = (uint32_t)S.svox[src];
+        const double l = S.slen[src];
+        const uint32_t x = p == st ? (v | kHead) : v;
+        S.vox[s0 + p] = (int32_t)x;
+        S.len[s0 + p] = l;
+        S.len32[s0 + p] = (float)l;
+        return x;
+    };
+    if (n <= ITEMS * kThreads) {
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            const int p = i * kThreads + tid;
+            xs[i] = p < n ? move(p, row_of(p)) : 0u;
+        }
+    } else {
+        for (int p = tid; p < n; p += kThreads) move(p, row_of(p));
+    }
+    __syncthreads();                              // (the LDS is reused by the table build)
+}
+
 // The tables from a bitmap of the volume's granules in LDS, when the
 // bitmap is small (n_cols/4 bits; 128^3 voxels = 64 KiB): set one bit per segment, prefix-popcount
 // the words, and a granule's rank is the number of set bits below it.  O(segments + words) per
@@ -516,7 +613,8 @@ template <int TM, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int n_words, StageMap sm,
-    unsigned long long* stats, const double* __restrict__ len, float* __restrict__ len32) {
+    unsigned long long* stats, const double* __restrict__ len, float* __restrict__ len32,
+    Staged S = Staged{}, int64_t n_blocks = 0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char bm_lds[];
     uint32_t* bm = reinterpret_cast<uint32_t*>(bm_lds);     // n_words bitmap words
     int32_t* pre = reinterpret_cast<int32_t*>(bm + n_words);  // set bits before each word
@@ -526,7 +624,18 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
     if (TM == kTabFill && m[5] < 0) return;
     const int tid = threadIdx.x;
     const int64_t n = s1 - s0;
-    if (TM != kTabFill && len32) copy_len32(len, len32, s0, n);
+    // staged: every block's segments moved out of the staging (rows in the bitmap's LDS when
+    // they fit), its table blocks' voxels kept in registers (kLocalMax = 16 * kThreads)
+    constexpr int kXs = kLocalMax / kThreads;
+    static_assert(kXs * kThreads == kLocalMax, "a table block's voxels fit the registers");
+    uint32_t xs[kXs];
+    const bool staged = TM == kTabBuild && S.svox;
+    if (staged) staged_gather<kXs>(S, blocks, n_blocks, blockIdx.x, s0, n, bm_lds,
+                                   (size_t)n_words * 8, xs);
+    else if (TM != kTabFill && len32) copy_len32(len, len32, s0, n);
+    auto vox_at = [&](int k, int i) {            // segment i = k * kThreads + tid
+        return staged ? xs[k] : (uint32_t)vox[s0 + i];
+    };
     if (n > kLocalMax) {
         if (TM != kTabFill && tid == 0) {
             m[5] = -1;
@@ -536,9 +645,13 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
     }
     for (int w = tid; w < n_words; w += kThreads) bm[w] = 0u;
     __syncthreads();
-    for (int i = tid; i < n; i += kThreads) {
-        const uint32_t g = stage_col((uint32_t)vox[s0 + i] & ~kHead, sm) >> 2;
-        atomicOr(&bm[g >> 5], 1u << (g & 31));
+#pragma unroll
+    for (int k = 0; k < kXs; ++k) {
+        const int i = k * kThreads + tid;
+        if (i < n) {
+            const uint32_t g = stage_col(vox_at(k, i) & ~kHead, sm) >> 2;
+            atomicOr(&bm[g >> 5], 1u << (g & 31));
+        }
     }
     __syncthreads();
     // thread t owns words [t*per, (t+1)*per)
@@ -571,11 +684,15 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
         }
     }
     __syncthreads();
-    for (int i = tid; i < n; i += kThreads) {
-        const uint32_t x = (uint32_t)vox[s0 + i];
-        const uint32_t v = stage_col(x & ~kHead, sm), g = v >> 2;
-        const int rank = pre[g >> 5] + __builtin_popcount(bm[g >> 5] & ((1u << (g & 31)) - 1u));
-        loc[s0 + i] = loc_code(rank, v, (x & kHead) != 0);
+#pragma unroll
+    for (int k = 0; k < kXs; ++k) {
+        const int i = k * kThreads + tid;
+        if (i < n) {
+            const uint32_t x = vox_at(k, i);
+            const uint32_t v = stage_col(x & ~kHead, sm), g = v >> 2;
+            const int rank = pre[g >> 5] + __builtin_popcount(bm[g >> 5] & ((1u << (g & 31)) - 1u));
+            loc[s0 + i] = loc_code(rank, v, (x & kHead) != 0);
+        }
     }
 }
 
@@ -683,81 +800,6 @@ template <int TM, typename TabT, int ITEMS>
 constexpr size_t table_lds() {
     return sizeof(typename RadixTable<ITEMS, TM>::Storage);
 }
-// A one-pass trace's segments still in their staging slots (sphrt_trace_emit): the table build
-// that reads them moves them into the CSR itself (sphrt_csr_local_build_staged) — no separate
-// compaction pass (C3 compact_kernel 0.68 ms) and no second read of the voxels.
-struct Staged {
-    const int64_t* row_ptr;   // CSR row starts (the trace's rows)
-    const int64_t* slot;      // staging slot starts (the scanned bounds)
-    const int32_t* nz_row;    // the trace row of each non-empty row (sphrt_csr_index_staged)
-    int64_t n_rays;           // rows (empty ones included)
-    const int32_t* svox;      // staging voxels and lengths
-    const double* slen;
-    int32_t* vox;             // the CSR: voxels (with the row-head bits), lengths, float32 lengths
-    double* len;
-    float* len32;
-};
-constexpr int kStagedRows = (int)kSegPerBlock + 1;   // a block's rows start in its window
-constexpr size_t kStagedLds = (size_t)kStagedRows * (sizeof(int32_t) + sizeof(int64_t)) + 16;
-
-// Block b's gather: its rows (non-empty rows [k0, k1), each starting in the block's window) as
-// (start - s0, slot - start) in LDS, then segment p of the block reads staging slot
-// s0 + p + delta(row of p) (a binary search over the rows in LDS).  Thread t takes segments
-// t, t + kThreads, ... (striped: every load and store instruction covers consecutive segments;
-// thread t taking 8t .. 8t + 7 with one search and a walk measured C3 2.59 ms for gather +
-// tables against 1.22 + 0.68 ms for tables + compaction: stride-8 accesses).  Writes vox (head
-// bit on each row's first segment), len and len32, and hands the common block's voxels to the
-// table build in registers (xs[i]: segment i * kThreads + t; nothing is read back).
-__device__ __forceinline__ void staged_gather(const Staged& S, const int64_t* blocks, int64_t nb,
-                                              int64_t b, int64_t s0, int64_t n,
-                                              unsigned char* lds, uint32_t (&xs)[8]) {
-    const int tid = threadIdx.x;
-    const int64_t k0 = blocks[kBlockFields * b + 4];
-    // (the last block's rows end at the non-empty row count: rays minus the empty list's end)
-    const int64_t k1 = b + 1 < nb ? blocks[kBlockFields * (b + 1) + 4]
-                                  : S.n_rays - blocks[kBlockFields * (nb - 1) + 1];
-    const int nrow = (int)(k1 - k0);
-    int32_t* rs = reinterpret_cast<int32_t*>(lds);
-    int64_t* rd = reinterpret_cast<int64_t*>(lds + (((size_t)(nrow + 1) * 4 + 7) & ~(size_t)7));
-    for (int t = tid; t < nrow; t += kThreads) {
-        const int64_t r = S.nz_row[k0 + t];
-        const int64_t a = S.row_ptr[r];
-        rs[t] = (int32_t)(a - s0);
-        rd[t] = S.slot[r] - a;
-    }
-    if (tid == 0) rs[nrow] = (int32_t)n;          // sentinel: the end of the last row
-    __syncthreads();
-    auto row_of = [&](int p) {                    // last row t with rs[t] <= p
-        int lo = 0, hi = nrow - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (rs[mid] <= p) lo = mid;
-            else hi = mid - 1;
-        }
-        return lo;
-    };
-    auto move = [&](int p, int row) {
-        const int64_t src = s0 + p + rd[row];
-        const uint32_t v = (uint32_t)S.svox[src];
-        const double l = S.slen[src];
-        const uint32_t x = p == rs[row] ? (v | kHead) : v;
-        S.vox[s0 + p] = (int32_t)x;
-        S.len[s0 + p] = l;
-        S.len32[s0 + p] = (float)l;
-        return x;
-    };
-    if (n <= 8 * kThreads) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int p = i * kThreads + tid;
-            xs[i] = p < n ? move(p, row_of(p)) : 0u;
-        }
-    } else {
-        for (int p = tid; p < n; p += kThreads) move(p, row_of(p));
-    }
-    __syncthreads();                              // (the LDS is reused by the table build)
-}
-
 template <int TM, typename TabT = int32_t>
 __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
@@ -776,7 +818,7 @@ __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_k
     // every block's segments / lengths, whichever launch then builds its table (or none)
     uint32_t xs[8];
     const bool staged = TM == kTabBuild && S.svox;
-    if (staged) staged_gather(S, blocks, n_blocks, blockIdx.x, s0, n, ts_raw, xs);
+    if (staged) staged_gather<8>(S, blocks, n_blocks, blockIdx.x, s0, n, ts_raw, sizeof(ts_raw), xs);
     else if (TM != kTabFill && len32) copy_len32(len, len32, s0, n);
     if (n > kLocalMax) {
         if (TM != kTabFill && threadIdx.x == 0) {
@@ -1758,8 +1800,6 @@ extern "C" int sphrt_csr_local_build_staged(const sphrt_csr* c, int64_t* blocks,
     StageMap sm;
     if (!stage_map(c, sm)) return fail("inconsistent brick staging fields");
     const int64_t cols = table_cols(c);
-    if (table_bitmap_words(cols))
-        return fail("staged table build is for radix-sorted tables (volumes over 2^19 columns)");
     const bool u16 = c->tab_bytes == 2;
     if (u16 && (cols + 3) / 4 > 65536) return fail("16-bit granule tables need <= 2^18 columns");
     StreamGuard guard(stream);
@@ -1769,9 +1809,21 @@ extern "C" int sphrt_csr_local_build_staged(const sphrt_csr* c, int64_t* blocks,
     if (c->n_segments == 0) return 0;
     const Staged S{c->row_ptr, slot, nz_row, c->n_rays, svox, slen, const_cast<int32_t*>(c->vox),
                    const_cast<double*>(c->len), const_cast<float*>(c->len32)};
-    const int kb = granule_key_bits(cols);
     unsigned long long* s = (unsigned long long*)stats;
     const unsigned nb = (unsigned)c->n_blocks;
+    if (const int words = table_bitmap_words(cols)) {
+        const size_t lds = (size_t)words * 8;
+        if (u16)
+            hipLaunchKernelGGL((local_table_bitmap_kernel<kTabBuild, uint16_t>), dim3(nb),
+                               dim3(kThreads), lds, st, blocks, c->vox, loc, (uint16_t*)tab_wide,
+                               kTabWide, words, sm, s, nullptr, nullptr, S, (int64_t)nb);
+        else
+            hipLaunchKernelGGL((local_table_bitmap_kernel<kTabBuild, int32_t>), dim3(nb),
+                               dim3(kThreads), lds, st, blocks, c->vox, loc, (int32_t*)tab_wide,
+                               kTabWide, words, sm, s, nullptr, nullptr, S, (int64_t)nb);
+        return check_launch("local_table_bitmap_kernel<build, staged>");
+    }
+    const int kb = granule_key_bits(cols);
     if (u16)
         return launch_tables<kTabBuild, uint16_t>(nb, st, blocks, c->vox, loc, (uint16_t*)tab_wide,
                                                   kTabWide, kb, sm, s, nullptr, nullptr, S);

@@ -486,13 +486,6 @@ def _tables_one_pass(desc, nblocks, dev):
             wide_bytes <= 0.3 * tr.cuda.mem_get_info(dev)[0])
 
 
-def _radix_tables(desc):
-    """Tables from a radix sort per block (volumes over 2^19 columns; smaller ones take the
-    bitmap kernel, apply.hip table_bitmap_words)."""
-    cols = desc.stage_cols if desc.stage_shape[0] > 0 else desc.n_cols
-    return ((cols + 3) // 4 + 31) // 32 > 4096
-
-
 def _local_tables(lib, desc, blocks, nblocks, total, dev, stream, staged=None):
     """Per-workgroup granule tables and run records of a CSR; sets desc.loc/.tab/.tab_stride/
     .n_fallback/.runs and returns (loc, tab, runs).  One host sync (the largest table decides
@@ -519,7 +512,7 @@ def _local_tables(lib, desc, blocks, nblocks, total, dev, stream, staged=None):
     loc = tr.empty(_seg_alloc(total), dtype=tr.int16, device=dev)
     one_pass = staged is not None or _tables_one_pass(desc, nblocks, dev)
     tdt = tr.int16 if desc.tab_bytes == 2 else tr.int32
-    if staged is not None:      # (the caller checked one_pass and the radix kernel)
+    if staged is not None:      # (the caller checked one_pass)
         (bound_ptr, svox, slen), nz_row = staged
         wide = tr.empty(nblocks * _lib.TAB_WIDE, dtype=tdt, device=dev)
         _lib.check(lib.sphrt_csr_local_build_staged(desc, _lib.ptr(blocks), _lib.ptr(loc),
@@ -906,9 +899,9 @@ class Operator:
 
     def _index(self, lib, dev, batch, row_ptr, vox, seg_len, total, ray_id, staging=None):
         """The apply kernels' row index and granule tables over a traced CSR.  With a one-pass
-        trace's staging (vox / seg_len None), grids whose tables are radix-sorted in one pass
-        let the table build move the segments out of the staging (sphrt_csr_local_build_staged:
-        no compaction pass, C3 compact_kernel 0.68 ms); others compact it first."""
+        trace's staging (vox / seg_len None) and one-pass tables, the table build moves the
+        segments out of the staging (sphrt_csr_local_build_staged: no compaction pass, C3
+        compact_kernel 0.68 ms); otherwise the staging is compacted first."""
         n = batch.n
         stream = _lib.stream_of(dev)
         batch.rays = None        # device ray directions: trace input only (24 B per ray)
@@ -919,7 +912,7 @@ class Operator:
         shape3 = tuple(int(v) for v in self.grid.shape[-3:])
         _set_stage(c, shape3, _stage_brick(nblocks))
         staged = (staging is not None and os.environ.get('SPHRT_TABLE_STAGED', '1') != '0' and
-                  _tables_one_pass(c, nblocks, dev) and _radix_tables(c))
+                  _tables_one_pass(c, nblocks, dev))
         if staging is not None and not staged:
             vox, seg_len = _compact_staging(lib, n, row_ptr, total, staging, dev, stream)
             staging = None

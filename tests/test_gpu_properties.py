@@ -1181,17 +1181,23 @@ def test_gd_direct_declines_what_it_cannot_run(gpu, monkeypatch):
     assert tr.equal(c1.cpu(), ca.cpu())
 
 
-@pytest.mark.parametrize('case', ['c3_views', 'long_rows'])
+@pytest.mark.parametrize('case', ['c3_views', 'long_rows', 'c2_views', 'tiny_grid'])
 def test_staged_table_build_equals_compaction(case, gpu, monkeypatch):
     """The one-pass trace's staging moved into the CSR by the table build
     (sphrt_csr_local_build_staged) equals compacting it first (sphrt_trace_compact +
     sphrt_csr_index + sphrt_csr_local_build, SPHRT_TABLE_STAGED=0) bit for bit: row pointers,
     voxels with their head bits, float64 / float32 lengths, blocks, slots and tables; and the
     forwards agree.  long_rows: a radix-table volume (> 2^19 columns) whose rays of ~5000
-    segments make blocks over 2048 segments (the big-block kernel) and over 4096 (no table)."""
+    segments make blocks over 2048 segments (the big-block kernel) and over 4096 (no table);
+    c2_views: bitmap tables, the rows in the bitmap's LDS; tiny_grid: a 4^3 grid whose bitmap LDS
+    holds no row table (the rows read from global memory)."""
     from sph_raytracer_amd import ConeRectGeom, Operator, SphericalGrid
     if case == 'c3_views':
         grid, geom = _orbit(6, (32, 64), grid_shape=(128, 128, 128))
+    elif case == 'c2_views':
+        grid, geom = _orbit(8, (50, 100), grid_shape=(50, 50, 50))
+    elif case == 'tiny_grid':
+        grid, geom = _orbit(8, (40, 60), grid_shape=(4, 4, 4))
     else:
         grid = SphericalGrid(shape=(2500, 16, 16))
         geom = ConeRectGeom((6, 8), pos=(3, 0.01, 0.02), fov=(3, 3))

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-4 records in one GPU call: forward PMC (profiles the bench's roofline traffic reads), the
+# round record (gpu suite, smoke, driver-shaped bench, bench + rocprofv3, C3/C4/C5 lines, Operator
+# kernel stats), then trace-kernel PMC at C2/C3/C5.  Stops at the first failure.
+set -e
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+STEPS=pmc bash tools/gpu_round.sh r04
+TAG=r04 bash tools/record_round.sh
+mkdir -p gpurun_out/tpmc
+for c in c2 c3 c5; do
+  timeout -k 10 120 python tools/pmc_trace.py --config $c --out gpurun_out/tpmc/r04_trace_${c}_pmc.json > gpurun_out/tpmc/pmc_$c.log 2>&1
+done
+ls gpurun_out/tpmc
