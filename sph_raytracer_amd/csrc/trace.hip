@@ -54,9 +54,10 @@ __device__ unsigned long long g_trace_cycles[16];   // 8..12: exact_wave_kernel
 #endif
 constexpr size_t kLdsBytes = 160 * 1024;        // LDS per CU; one workgroup may take all of it
 
-// Ablation builds only (-DSPHRT_TRACE_ABL=k, tools/pmc_trace.py --ablate): trace_one stops after
-// phase k (1 solve + list, 2 sort, 3 tie check, 4 fill) with a zero segment count — wrong results
-// by design; the PMC difference between consecutive k is the phase's instruction count.
+// Ablation builds only (-DSPHRT_TRACE_ABL=k, tools/abl_trace.sh): trace_one stops after phase k
+// (1 solve + list, 2 sort, 3 tie check, 4 fill; inside phase 1: 11 after the shells, 12 after
+// the cones) with a zero segment count — wrong results by design; the PMC difference between
+// consecutive stops is the phase's instruction count.
 #ifdef SPHRT_TRACE_ABL
 #define TRACE_ABL(k)                                                                          \
     do {                                                                                      \
@@ -858,6 +859,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
             push(v && keep(to) && !(to == ti && ro == ri), to, nbr + j, ro, true);
         }
         s_near = base;
+        TRACE_ABL(11);                  // (ablation: after the shells)
         const int ce0 = 2 * nbr;
         for (int j0 = nbe > 64 ? first_may_cross(nbe, lane, cone_ok) : 0; j0 < nbe; j0 += 64) {
             const int j = j0 + lane;
@@ -875,6 +877,7 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
             push(v && keep(ta), ta, ce0 + j, ra);
             push(v && keep(tb) && !(tb == ta && rb == ra), tb, ce0 + nbe + j, rb);
         }
+        TRACE_ABL(12);                  // (ablation: after the cones)
         const int ca0 = 2 * nbr + 2 * nbe;
         for (int k0 = 0; k0 < p_count; k0 += 64) {
             const bool v = k0 + lane < p_count;

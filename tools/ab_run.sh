@@ -1,4 +1,6 @@
 set -e
-bash tools/gpu_check.sh r04
-for c in c5 c2 c3; do bash tools/ab_env.sh $c staged="SPHRT_TABLE_STAGED=1" compact="SPHRT_TABLE_STAGED=0"; done
-python tools/ab_table.py gpurun_out/ab "trace_kernel|local_table|compact|screen|exact_wave" c3 c5 c2
+export TMPDIR=/tmp
+bash tools/abl_trace.sh c3 r04b
+mkdir -p gpurun_out/stamps
+SPHRT_LIB=sph_raytracer_amd/lib/variants/libsphrt_tstamps.so timeout -k 10 180 python tools/trace_phases.py c3 > gpurun_out/stamps/c3.json 2> gpurun_out/stamps/c3.err
+cat gpurun_out/stamps/c3.json

@@ -41,9 +41,13 @@ def main():
         buf = (ctypes.c_ulonglong * 16)()
         lib.sphrt_diag_trace_cycles(ctypes.cast(buf, ctypes.c_void_p), 0)
         n = max(buf[5], 1)
+        ne = max(buf[8], 1)
         rec[name] = {'rays_traced': buf[5], 'mean_F': buf[6] / n, 'wall_ms': wall * 1e3,
                      'cycles_per_ray': {k: buf[i] / n for i, k in enumerate(
-                         ['solve', 'sort', 'ties', 'fill', 'emit'])}}
+                         ['solve', 'sort', 'ties', 'fill', 'emit'])},
+                     'exact_rays': buf[8],
+                     'exact_cycles_per_ray': {k: buf[9 + i] / ne for i, k in enumerate(
+                         ['candidates', 'partition', 'leaf_ranks', 'walk'])}}
     print(json.dumps(rec, indent=1))
 
 
