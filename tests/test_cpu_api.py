@@ -384,6 +384,27 @@ def test_loss_abi_argument_checks():
         assert word in lib.sphrt_last_error().lower(), lib.sphrt_last_error()
 
 
+def test_staged_and_reference_trace_argument_checks():
+    """The staged one-pass entry points and the reference-mode trace reject bad arguments before
+    touching the device (null row list, an incomplete staged CSR, unknown trace flags), with a
+    message in sphrt_last_error.  (No compute call: no GPU here.)"""
+    from sph_raytracer_amd import _lib
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)      # never dereferenced: every call below fails its checks first
+    csr = _lib.CSR()
+    csr.n_rays, csr.n_segments, csr.n_blocks = 10, 20, 1
+    cases = [
+        (lambda: lib.sphrt_csr_index_staged(p, 10, p, p, p, 1, None, None, p, None), b'nz_row'),
+        (lambda: lib.sphrt_csr_local_build_staged(ctypes.byref(csr), p, p, p, p, p, p, p, p,
+                                                  None), b'incomplete'),
+        (lambda: lib.sphrt_trace_reference(None, None, 8, p, None, None, None, None, 0, None),
+         b'plan'),
+    ]
+    for call, word in cases:
+        assert call() != 0
+        assert word in lib.sphrt_last_error().lower(), lib.sphrt_last_error()
+
+
 def test_fastpath_entry_builds_and_declines_foreign_inputs():
     """csrc/fastpath.cpp (the CPython entry for steady-state Operator calls) builds against the
     installed torch, loads, and returns None for anything it has no binding for (CPU tensors,
