@@ -42,13 +42,19 @@ constexpr int kNone = 0x7fffffff;  // "no update" in the forward-fill scans
 constexpr int kWavesPerBlock = 4;
 
 // Diagnostic build only (-DSPHRT_TRACE_STAMPS, tools/trace_phases.py): s_memtime cycles per trace
-// phase summed over all hit rays (0 solve+push, 1 sort, 2 tie check, 3 fill/lengths, 4 emit).
+// phase summed over all hit rays (0 solve+push, 1 sort, 2 tie check, 3 fill/lengths, 4 emit);
+// exact_wave_kernel: 8 rays, 9..12 its phases, 13 / 14 the largest ray / partition phase, 15
+// depth-limit ranges; 16 / 17 partitions below the top levels and their cycles, 18 depth-limit
+// cycles.
 #ifdef SPHRT_TRACE_STAMPS
-__device__ unsigned long long g_trace_cycles[16];   // 8..12: exact_wave_kernel
+__device__ unsigned long long g_trace_cycles[24];   // 8..18: exact_wave_kernel
 #define TRACE_T(var) const uint64_t var = __builtin_amdgcn_s_memtime()
 #define TRACE_ADD(i, a, b) \
     do { if (lane == 0) atomicAdd(&g_trace_cycles[i], (unsigned long long)((b) - (a))); } while (0)
+#define TRACE_MAX(i, a, b) \
+    do { if (lane == 0) atomicMax(&g_trace_cycles[i], (unsigned long long)((b) - (a))); } while (0)
 #else
+#define TRACE_MAX(i, a, b) do {} while (0)
 #define TRACE_T(var) do {} while (0)
 #define TRACE_ADD(i, a, b) do {} while (0)
 #endif
@@ -460,6 +466,7 @@ struct TraceOut {
     unsigned* n_hits;                // workspace: screened hit-ray counter
     HitRay* hits;                    // workspace: hit rays
     unsigned long long* n_over;      // EMIT: rays whose segments exceed their bound
+    unsigned long long* n_heap;      // workspace: depth-limit ranges, rank-sorted / heap-sorted
     int wedge;                       // solve only the half-planes of a line's azimuth wedge
 };
 
@@ -1323,24 +1330,24 @@ __global__ __launch_bounds__(256) void solve_kernel(GridDev G, RaysDev R, int fa
 template <typename F, class Put>
 __device__ __forceinline__ void exact_candidates(const GridDev& G, const RayGeoT<F>& gr,
                                                  const RayGeoT<F>& ge, const RayGeoT<F>& ga,
-                                                 int lane, Put put) {
+                                                 int lane, int step, Put put) {
     const int nbr = G.nbr, nbe = G.nbe, nba = G.nba;
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe;
-    for (int j = lane; j < nbr; j += 64) {
+    for (int j = lane; j < nbr; j += step) {
         F ti, to;
         int ri, ro, ni, no;
         sphere_solve(G, gr, j, ti, ri, to, ro, ni, no);
         put(j, (double)ti, ri);
         put(nbr + j, (double)to, ro);
     }
-    for (int j = lane; j < nbe; j += 64) {
+    for (int j = lane; j < nbe; j += step) {
         F ta, tb;
         int ra, rb, na_, nb_;
         cone_solve(G, ge, j, ta, ra, tb, rb, na_, nb_);
         put(r_lim + j, (double)ta, ra);
         put(r_lim + nbe + j, (double)tb, rb);
     }
-    for (int j = lane; j < nba; j += 64) {
+    for (int j = lane; j < nba; j += step) {
         F t;
         int r, ng;
         plane_solve(G, ga, j, t, r, ng);
@@ -1357,15 +1364,15 @@ __device__ __forceinline__ void exact_candidates(const GridDev& G, const RayGeoT
 template <bool ALL, typename F, class Put>
 __device__ __forceinline__ void exact_list(const GridDev& G, const RaysDev& R,
                                            const RayGeoT<F>& g, const double* x, const double* d,
-                                           int lane, Put put) {
+                                           int lane, int step, Put put) {
     if (ALL && R.fresh) {
         const RayGeoT<F> ge = make_ray_family<F>((F)x[0], (F)x[1], (F)x[2], (F)d[0], (F)d[1],
                                                  (F)d[2], 1);
         const RayGeoT<F> ga = make_ray_family<F>((F)x[0], (F)x[1], (F)x[2], (F)d[0], (F)d[1],
                                                  (F)d[2], 2);
-        exact_candidates(G, g, ge, ga, lane, put);
+        exact_candidates(G, g, ge, ga, lane, step, put);
     } else {
-        exact_candidates(G, g, g, g, lane, put);
+        exact_candidates(G, g, g, g, lane, step, put);
     }
 }
 
@@ -1549,7 +1556,7 @@ __global__ __launch_bounds__(64) void exact_kernel(GridDev G, RaysDev R, TraceOu
         int s[3];
         load_ray(R, ray, x, d, s);
         const RayGeoT<F> g = exact_geo<F>(x, d);
-        exact_list<ALL>(G, R, g, x, d, lane, [&](int c, double t, int reg) {
+        exact_list<ALL>(G, R, g, x, d, lane, 64, [&](int c, double t, int reg) {
             v.set(c, Cand{t, ((uint32_t)c << 16) | (uint32_t)(reg + 2), 0u});
         });
         __syncthreads();
@@ -1576,12 +1583,143 @@ __global__ __launch_bounds__(64) void exact_kernel(GridDev G, RaysDev R, TraceOu
 constexpr size_t kExactWaveEntryBytes = 2 * 8 + 5 * 4;   // per candidate, see the layout below
 constexpr int kExactStack = 64;                         // partition stack (depth <= 2 log2 K)
 constexpr size_t kExactWaveLdsMax = 64 * 1024;
-__host__ __device__ constexpr size_t exact_wave_lds(int K) {
-    return (size_t)K * kExactWaveEntryBytes + 3 * kExactStack * sizeof(int);
+__host__ __device__ constexpr size_t exact_wave_lds(int K, int W) {
+    return (size_t)K * kExactWaveEntryBytes + (size_t)W * (3 * kExactStack + 3) * sizeof(int);
 }
 
-template <int MODE, typename T, typename F = double, bool INV = false, bool ALL = false>
-__global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
+// One partition of [first, last) by one wave (lane 0 runs the median-of-three), the reference's
+// __unguarded_partition_pivot; returns the cut.  lpos / rpos are indexed from `first` (ranks are
+// < last - first), so waves partitioning disjoint ranges share them.  Leaves the swaps unsynced.
+__device__ __forceinline__ int exact_partition(const SoaList& v, double* tk, uint32_t* pk,
+                                               int32_t* lpos, int32_t* rpos, int first, int last,
+                                               int lane, uint64_t below) {
+    const int mid = first + (last - first) / 2;
+    if (lane == 0) move_median_to_first(v, first, first + 1, mid, last - 1);
+    wave_sync();
+    const double piv = tk[first];
+    // stop counts
+    int n_l = 0, n_r = 0;
+    for (int c0 = first; c0 < last; c0 += 64) {
+        const int p = c0 + lane;
+        const bool in = p < last;
+        const double t = in ? tk[p] : 0.0;
+        n_l += __builtin_popcountll(__ballot(in && p > first && !(t < piv)));
+        n_r += __builtin_popcountll(__ballot(in && !(piv < t)));
+    }
+    // ranks, stop lists and k*
+    int a0 = 0, r0 = 0, ks = 0;
+    for (int c0 = first; c0 < last; c0 += 64) {
+        const int p = c0 + lane;
+        const bool in = p < last;
+        const double t = in ? tk[p] : 0.0;
+        const bool is_l = in && p > first && !(t < piv);
+        const bool is_r = in && !(piv < t);
+        const uint64_t bl = __ballot(is_l), br = __ballot(is_r);
+        const int a = a0 + __builtin_popcountll(bl & below);   // left rank
+        const int rb = r0 + __builtin_popcountll(br & below);  // right stops before p
+        if (is_l) lpos[first + a] = p;
+        if (is_r) rpos[first + n_r - 1 - rb] = p;
+        const int after = n_r - rb - (is_r ? 1 : 0);          // right stops after p
+        ks += __builtin_popcountll(__ballot(is_l && after > a));
+        a0 += __builtin_popcountll(bl);
+        r0 += __builtin_popcountll(br);
+    }
+    wave_sync();
+    int cut;
+    if (ks < n_l) cut = ks > 0 ? min(lpos[first + ks], rpos[first + ks - 1]) : lpos[first];
+    else cut = rpos[first + ks - 1];
+    for (int k = lane; k < ks; k += 64) {
+        const int i = lpos[first + k], j = rpos[first + k];
+        const double ti = tk[i], tj = tk[j];
+        const uint32_t pi = pk[i], pj = pk[j];
+        tk[i] = tj; pk[i] = pj;
+        tk[j] = ti; pk[j] = pi;
+    }
+    return cut;
+}
+
+// Whether two list entries with the same distance leave a different state in either order: both
+// set one region row (the walk's r / e / a updates; the start entry K - 1 sets all three to the
+// start voxel) to different values.
+__device__ __forceinline__ int entry_rows(uint32_t p, int K, int r_lim, int e_lim, const int* s,
+                                          int* v) {
+    const int cand = (int)(p >> 16), reg = (int)(p & 0xffffu) - 2;
+    if (cand == K - 1) {
+        v[0] = s[0]; v[1] = s[1]; v[2] = s[2];
+        return 7;
+    }
+    v[0] = v[1] = v[2] = reg;
+    if (cand < r_lim) return 1;
+    if (cand < e_lim) return reg != -2 ? 2 : 0;
+    return reg != -2 ? 4 : 0;
+}
+__device__ __forceinline__ bool entries_conflict(uint32_t pa, uint32_t pb, int K, int r_lim,
+                                                 int e_lim, const int* s) {
+    int va[3], vb[3];
+    const int m = entry_rows(pa, K, r_lim, e_lim, s, va) & entry_rows(pb, K, r_lim, e_lim, s, vb);
+    return ((m & 1) && va[0] != vb[0]) || ((m & 2) && va[1] != vb[1]) ||
+           ((m & 4) && va[2] != vb[2]);
+}
+
+// The depth limit ran out on [first, last): the reference heap-sorts it (std::__partial_sort).
+// Heapsort's order among equal distances is its own, but only the walk reads the order, and there
+// equal neighbours differ only when both set one region row to different values (the segment
+// between them is empty; for INV an infinite one is kept, NaN long).  With no such pair in the
+// range a rank sort (ascending, ties by position) gives the same segments — one wave, in
+// parallel; otherwise lane 0 runs the heapsort.  ts / ps (free until the leaf ranks) take the
+// sorted range; lpos its ranks.
+template <bool INV>
+__device__ __forceinline__ void exact_heap_range(const SoaList& v, double* tk, uint32_t* pk,
+                                                 double* ts, uint32_t* ps, int32_t* lpos,
+                                                 int first, int last, int K, int r_lim, int e_lim,
+                                                 const int* s, int lane,
+                                                 unsigned long long* n_heap) {
+    bool amb = false;
+    for (int p = first + lane; p < last; p += 64) {
+        const double t = tk[p];
+        const uint32_t pp = pk[p];
+        // ties that can matter: updates (t >= 0) with an empty segment between (finite t;
+        // INV keeps the NaN segment between two infinite ones)
+        const bool live = t >= 0.0 && (INV || t < kInf);
+        int r = first;
+        for (int j = first; j < last; ++j) {
+            const double u = tk[j];
+            r += (u < t || (u == t && j < p)) ? 1 : 0;
+            if (u == t && j != p && live) {
+                if (INV && t == kInf) amb = true;
+                else amb |= entries_conflict(pp, pk[j], K, r_lim, e_lim, s);
+            }
+        }
+        lpos[p] = r;
+    }
+    if (lane == 0 && n_heap) atomicAdd(n_heap + (__ballot(amb) != 0 ? 1 : 0), 1ull);
+    if (__ballot(amb) != 0) {
+        wave_sync();
+        if (lane == 0) heap_sort(v, first, last);
+        wave_sync();
+        return;
+    }
+    for (int p = first + lane; p < last; p += 64) {
+        const int r = lpos[p];
+        ts[r] = tk[p];
+        ps[r] = pk[p];
+    }
+    wave_sync();
+    for (int p = first + lane; p < last; p += 64) {
+        tk[p] = ts[p];
+        pk[p] = ps[p];
+    }
+    wave_sync();
+}
+
+// W waves per ray.  The candidates and the leaf ranks are spread over all 64 W lanes; the
+// partitions run breadth-first for log2(W) levels (wave w partitions range w of the level, so
+// the two halves of a partition proceed in parallel), then each wave finishes one of the W
+// ranges with its own stack: a deferred ray's latency is the partition phase's chain of ~K / 8
+// dependent partitions, which W = 4 cuts to about a quarter.  Disjoint ranges give the same
+// result in any order.  The walk runs on wave 0.
+template <int MODE, typename T, typename F = double, bool INV = false, bool ALL = false, int W = 1>
+__global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R, TraceOut<T> o) {
     extern __shared__ __attribute__((aligned(16))) unsigned char xw_lds[];
     const int K = G.K;
     double* tk = reinterpret_cast<double*>(xw_lds);   // list (distance), current order
@@ -1591,14 +1729,16 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
     int32_t* lpos = reinterpret_cast<int32_t*>(ps + K);   // left stops by rank
     int32_t* rpos = lpos + K;                              // right stops by rank
     uint32_t* leaf = reinterpret_cast<uint32_t*>(rpos + K);   // leaf range lo | hi << 16
-    // the partition stack in LDS (uniform; a private array would live in scratch memory, one
-    // global round trip per push or pop)
-    int* st_first = reinterpret_cast<int*>(leaf + K);
+    // per wave: the partition stack in LDS (uniform; a private array would live in scratch
+    // memory, one global round trip per push or pop); then the W top-level ranges
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    int* st_first = reinterpret_cast<int*>(leaf + K) + wid * 3 * kExactStack;
     int* st_last = st_first + kExactStack;
     int* st_depth = st_last + kExactStack;
+    int* top = reinterpret_cast<int*>(leaf + K) + W * 3 * kExactStack;   // (first, last, depth)
     const SoaList v{tk, pk};
-    const int lane = threadIdx.x;
     const uint64_t below = lanemask_lt(lane);
+    const int r_lim = 2 * G.nbr, e_lim = 2 * G.nbr + 2 * G.nbe;
     const int64_t count = exact_count<ALL>(R, o);
     for (int64_t q = blockIdx.x; q < count; q += gridDim.x) {
         const int64_t ray = exact_ray<ALL>(o, q);
@@ -1607,80 +1747,75 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
         load_ray(R, ray, x, d, s);
         TRACE_T(x0);
         const RayGeoT<F> g = exact_geo<F>(x, d);
-        exact_list<ALL>(G, R, g, x, d, lane, [&](int c, double t, int reg) {
+        exact_list<ALL>(G, R, g, x, d, tid, 64 * W, [&](int c, double t, int reg) {
             tk[c] = t;
             pk[c] = ((uint32_t)c << 16) | (uint32_t)(reg + 2);
         });
-        bool nan = false;
-        for (int p = lane; p < K; p += 64) leaf[p] = (uint32_t)p | ((uint32_t)(p + 1) << 16);
-        wave_sync();
-        for (int p = lane; p < K; p += 64) nan |= __builtin_isnan(tk[p]);
-        if (__ballot(nan) != 0) {
-            if (lane == 0) {
+        int nan = 0;
+        for (int p = tid; p < K; p += 64 * W) leaf[p] = (uint32_t)p | ((uint32_t)(p + 1) << 16);
+        if (tid == 0) {
+            top[0] = 0;
+            top[1] = K;
+            top[2] = 2 * (31 - __builtin_clz((unsigned)max(K, 1)));
+        }
+        __syncthreads();
+        for (int p = tid; p < K; p += 64 * W) nan |= __builtin_isnan(tk[p]) ? 1 : 0;
+        if (__syncthreads_or(nan)) {
+            if (tid == 0) {
                 introsort(v, K);
                 exact_walk<MODE, T, F, INV>(G, o, ray, s, v);
             }
-            wave_sync();
+            __syncthreads();
             continue;
         }
         TRACE_T(x1);
-        TRACE_ADD(8, 0, 1);
-        TRACE_ADD(9, x0, x1);
-        // ---- partition phase (uniform control flow) ----
+        if (wid == 0) {
+            TRACE_ADD(8, 0, 1);
+            TRACE_ADD(9, x0, x1);
+        }
+        // ---- partition phase (uniform control flow per wave) ----
+        // the top levels, breadth-first: range w of level l splits into ranges w and w + 2^l
+#pragma unroll
+        for (int n = 1; n < W; n *= 2) {
+            if (wid < n) {
+                const int f = top[3 * wid], l = top[3 * wid + 1], dep = top[3 * wid + 2];
+                int cut = l, nd = dep;
+                if (l - f > kIntroThreshold && dep > 0) {
+                    cut = exact_partition(v, tk, pk, lpos, rpos, f, l, lane, below);
+                    nd = dep - 1;
+                }
+                if (lane == 0) {
+                    top[3 * wid + 1] = cut;
+                    top[3 * wid + 2] = nd;
+                    top[3 * (wid + n)] = cut;
+                    top[3 * (wid + n) + 1] = l;
+                    top[3 * (wid + n) + 2] = nd;
+                }
+            }
+            __syncthreads();
+        }
+        // then each wave its range, depth first
         int sp = 0;
-        int first = 0, last = K, depth = 2 * (31 - __builtin_clz((unsigned)max(K, 1)));
-        bool have = K > 1;
+        int first = top[3 * wid], last = top[3 * wid + 1], depth = top[3 * wid + 2];
+        bool have = last - first > 1;
         while (have) {
             while (last - first > kIntroThreshold) {
-                if (depth == 0) {                      // rare: the reference's heapsort
-                    if (lane == 0) heap_sort(v, first, last);
-                    wave_sync();
+                if (depth == 0) {                      // the reference's heapsort
+                    TRACE_T(h0);
+                    exact_heap_range<INV>(v, tk, pk, ts, ps, lpos, first, last, K, r_lim, e_lim,
+                                          s, lane, o.n_heap);
+                    TRACE_T(h1);
+                    TRACE_ADD(15, 0, 1);
+                    TRACE_ADD(18, h0, h1);
                     first = last;                      // sorted: no leaf
                     break;
                 }
                 --depth;
-                const int mid = first + (last - first) / 2;
-                if (lane == 0) move_median_to_first(v, first, first + 1, mid, last - 1);
-                wave_sync();
-                const double piv = tk[first];
-                // stop counts
-                int n_l = 0, n_r = 0;
-                for (int c0 = first; c0 < last; c0 += 64) {
-                    const int p = c0 + lane;
-                    const bool in = p < last;
-                    const double t = in ? tk[p] : 0.0;
-                    n_l += __builtin_popcountll(__ballot(in && p > first && !(t < piv)));
-                    n_r += __builtin_popcountll(__ballot(in && !(piv < t)));
-                }
-                // ranks, stop lists and k*
-                int a0 = 0, r0 = 0, ks = 0;
-                for (int c0 = first; c0 < last; c0 += 64) {
-                    const int p = c0 + lane;
-                    const bool in = p < last;
-                    const double t = in ? tk[p] : 0.0;
-                    const bool is_l = in && p > first && !(t < piv);
-                    const bool is_r = in && !(piv < t);
-                    const uint64_t bl = __ballot(is_l), br = __ballot(is_r);
-                    const int a = a0 + __builtin_popcountll(bl & below);   // left rank
-                    const int rb = r0 + __builtin_popcountll(br & below);  // right stops before p
-                    if (is_l) lpos[a] = p;
-                    if (is_r) rpos[n_r - 1 - rb] = p;
-                    const int after = n_r - rb - (is_r ? 1 : 0);          // right stops after p
-                    ks += __builtin_popcountll(__ballot(is_l && after > a));
-                    a0 += __builtin_popcountll(bl);
-                    r0 += __builtin_popcountll(br);
-                }
-                wave_sync();
-                int cut;
-                if (ks < n_l) cut = ks > 0 ? min(lpos[ks], rpos[ks - 1]) : lpos[0];
-                else cut = rpos[ks - 1];
-                for (int k = lane; k < ks; k += 64) {
-                    const int i = lpos[k], j = rpos[k];
-                    const double ti = tk[i], tj = tk[j];
-                    const uint32_t pi = pk[i], pj = pk[j];
-                    tk[i] = tj; pk[i] = pj;
-                    tk[j] = ti; pk[j] = pi;
-                }
+                TRACE_T(p0);
+                const int cut = exact_partition(v, tk, pk, lpos, rpos, first, last, lane, below);
+                TRACE_T(p1);
+                TRACE_ADD(16, 0, 1);
+                TRACE_ADD(17, p0, p1);
                 if (lane == 0) {
                     st_first[sp] = cut;
                     st_last[sp] = last;
@@ -1702,11 +1837,14 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
                 depth = st_depth[sp];
             }
         }
-        wave_sync();
+        __syncthreads();
         TRACE_T(x2);
-        TRACE_ADD(10, x1, x2);
+        if (wid == 0) {
+            TRACE_ADD(10, x1, x2);
+            TRACE_MAX(14, x1, x2);
+        }
         // ---- final insertion sort = stable sort inside each leaf, as ranks ----
-        for (int p = lane; p < K; p += 64) {
+        for (int p = tid; p < K; p += 64 * W) {
             const uint32_t code = leaf[p];
             const int lo = (int)(code & 0xffffu), hi = (int)(code >> 16);
             const double t = tk[p];
@@ -1718,14 +1856,17 @@ __global__ __launch_bounds__(64) void exact_wave_kernel(GridDev G, RaysDev R, Tr
             ts[r] = t;
             ps[r] = pk[p];
         }
-        wave_sync();
+        __syncthreads();
         TRACE_T(x3);
-        TRACE_ADD(11, x2, x3);
+        if (wid == 0) TRACE_ADD(11, x2, x3);
         // (the pre-sort list and the left-stop list are free now: compacted segments go there)
-        exact_walk_wave<MODE, T, F, INV>(G, o, ray, s, ts, ps, lpos, tk, lane);
-        wave_sync();
+        if (wid == 0) exact_walk_wave<MODE, T, F, INV>(G, o, ray, s, ts, ps, lpos, tk, lane);
+        __syncthreads();
         TRACE_T(x4);
-        TRACE_ADD(12, x3, x4);
+        if (wid == 0) {
+            TRACE_ADD(12, x3, x4);
+            TRACE_MAX(13, x0, x4);
+        }
     }
 }
 
@@ -1801,15 +1942,24 @@ __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* 
 
 // ---- host launchers ----------------------------------------------------------------------
 static int trace_cap(const GridDev& G) { return ((G.K + 63) / 64) * 64; }
-constexpr int kExactBlocks = 4096;   // one wave per deferred ray, 16 per CU
+constexpr int kExactBlocks = 4096;   // one workgroup per deferred ray, 16 per CU
 // The serial kernel (grids whose list does not fit LDS) keeps each wave's list in the workspace:
 // its grid, and so the workspace, is capped at one wave per CU (deferred rays are rare; the
 // waves stride over them) — 256 * K * 16 B, e.g. 56 MB at K = 13653 instead of 0.9 GB.
 constexpr int kExactSerialBlocks = 256;
-constexpr size_t kWsHead = 256;      // deferred counter, padded
+constexpr size_t kWsHead = 256;      // deferred (0), hit (64) and heap-range (128) counters
 
 static bool exact_in_lds(const GridDev& G) {
-    return exact_wave_lds(G.K) <= kExactWaveLdsMax;
+    return exact_wave_lds(G.K, 1) <= kExactWaveLdsMax;
+}
+// Waves per deferred ray (exact_wave_kernel's W): 4 unless the list does not fit LDS with their
+// stacks.  SPHRT_EXACT_WAVES=1 builds the one-wave kernel (A/B).
+#ifndef SPHRT_EXACT_WAVES
+#define SPHRT_EXACT_WAVES 4
+#endif
+constexpr int kExactWaves = SPHRT_EXACT_WAVES;
+static bool exact_multi_wave(const GridDev& G) {
+    return kExactWaves > 1 && exact_wave_lds(G.K, kExactWaves) <= kExactWaveLdsMax;
 }
 static size_t exact_scratch_bytes(const GridDev& G) {   // lists of large-K grids, one per wave
     return exact_in_lds(G) ? 0 : (size_t)kExactSerialBlocks * G.K * sizeof(Cand);
@@ -1851,6 +2001,7 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     unsigned char* ws = (unsigned char*)workspace;
     o.n_deferred = (unsigned long long*)ws;
     o.n_hits = (unsigned*)(ws + 64);
+    o.n_heap = (unsigned long long*)(ws + 128);
     o.deferred = (int64_t*)(ws + kWsHead);
     o.hits = (HitRay*)(ws + kWsHead + (((size_t)R.n * sizeof(int64_t) + 255) / 256) * 256);
     o.wedge = wedge_enabled();
@@ -1874,9 +2025,13 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,
                        o, cap);
     if (int e = check_launch("trace_kernel")) return e;
-    if (exact_in_lds(G))
+    if (exact_multi_wave(G))
+        hipLaunchKernelGGL((exact_wave_kernel<MODE, T, double, false, false, kExactWaves>),
+                           dim3(kExactBlocks), dim3(64 * kExactWaves),
+                           exact_wave_lds(G.K, kExactWaves), st, G, R, o);
+    else if (exact_in_lds(G))
         hipLaunchKernelGGL((exact_wave_kernel<MODE, T>), dim3(kExactBlocks), dim3(64),
-                           exact_wave_lds(G.K), st, G, R, o);
+                           exact_wave_lds(G.K, 1), st, G, R, o);
     else
         hipLaunchKernelGGL((exact_kernel<MODE, T>), dim3(kExactSerialBlocks), dim3(64), 0, st, G, R, o,
                            scratch);
@@ -1890,10 +2045,10 @@ using namespace sphrt;
 #ifdef SPHRT_TRACE_STAMPS
 extern "C" int sphrt_diag_trace_cycles(unsigned long long* host, int reset) {
     if (reset) {
-        unsigned long long z[16] = {};
+        unsigned long long z[24] = {};
         return hipMemcpyToSymbol(HIP_SYMBOL(g_trace_cycles), z, sizeof(z)) == hipSuccess ? 0 : 1;
     }
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace_cycles), 16 * sizeof(unsigned long long), 0,
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace_cycles), 24 * sizeof(unsigned long long), 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 #endif
@@ -2059,10 +2214,12 @@ static int launch_reference(const GridDev& G, const RaysDev& R, TraceOut<double>
                     workspace_bytes(G, R.n));
     unsigned char* ws = (unsigned char*)workspace;
     o.n_deferred = (unsigned long long*)ws;
+    o.n_heap = (unsigned long long*)(ws + 128);
+    if (hipMemsetAsync(ws, 0, kWsHead, st) != hipSuccess) return fail("memset failed");
     if (exact_in_lds(G)) {
         const int64_t blocks = R.n < 4 * kExactBlocks ? R.n : 4 * kExactBlocks;
         hipLaunchKernelGGL((exact_wave_kernel<MODE, double, F, INV, true>), dim3((unsigned)blocks),
-                           dim3(64), exact_wave_lds(G.K), st, G, R, o);
+                           dim3(64), exact_wave_lds(G.K, 1), st, G, R, o);
     } else {
         Cand* scratch = (Cand*)(ws + workspace_bytes(G, R.n) - exact_scratch_bytes(G));
         hipLaunchKernelGGL((exact_kernel<MODE, double, F, INV, true>), dim3(kExactSerialBlocks),

@@ -491,6 +491,12 @@ def test_gd_retrieval_decreases_loss(gpu):
 def _deferred_count(grid, geom, gpu):
     """Rays the wave trace defers to the exact (emulated introsort) path: the trace workspace's
     counter after a count pass (trace.hip launch_trace)."""
+    return _exact_stats(grid, geom, gpu)[0]
+
+
+def _exact_stats(grid, geom, gpu):
+    """(deferred rays, depth-limit ranges rank-sorted, ranges heap-sorted by one lane) of a count
+    pass: the trace workspace's counters (trace.hip launch_trace, exact_heap_range)."""
     from sph_raytracer_amd import _lib, raytracer as rt
     lib = _lib.load()
     plan = rt._Plan(grid, gpu)
@@ -499,7 +505,8 @@ def _deferred_count(grid, geom, gpu):
     tws = rt._workspace(lib, plan, batch.n, gpu)
     _lib.check(lib.sphrt_trace_count(plan.handle, batch.desc, _lib.ptr(counts), _lib.ptr(tws),
                                      tws.numel(), _lib.stream_of(gpu)), 'sphrt_trace_count')
-    return int(tws[:8].view(tr.int64).item())
+    head = tws[:256].cpu().view(tr.int64)
+    return int(head[0]), int(head[16]), int(head[17])
 
 
 @pytest.mark.parametrize('shape,a_full', [((64, 64, 64), False), ((17, 9, 30), False),
@@ -533,9 +540,11 @@ def test_exact_tie_rays_vs_oracle(shape, a_full, gpu):
         msg = gc.compare_segments((ptr, vox, seg), got, 5.1, f'{shape} {type(gm).__name__}')
         assert msg is None, msg
     # the geometry really exercises the exact path (rays through the origin, starts on a = 0)
-    deferred = [_deferred_count(grid, gm, gpu) for gm in geoms]
-    print('deferred rays per view:', deferred)
-    assert sum(deferred) > 0
+    stats = [_exact_stats(grid, gm, gpu) for gm in geoms]
+    print('(deferred rays, heap ranges rank-sorted, heap-sorted) per view:', stats)
+    assert sum(st[0] for st in stats) > 0
+    if shape == (64, 64, 64):     # the depth limit runs out (reference heapsort): rank-sorted
+        assert sum(st[1] for st in stats) > 0
 
 
 def test_fast_path_matches_general_path(c2, gpu):

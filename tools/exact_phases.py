@@ -33,11 +33,14 @@ def main():
     Operator(grid, geom, device=dev)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 24)()
     lib.sphrt_diag_trace_cycles(ctypes.cast(buf, ctypes.c_void_p), 0)
     n = max(buf[8], 1)
     print(json.dumps({'deferred_rays_both_passes': buf[8], 'wall_ms': wall * 1e3, 'cycles_per_ray': {
-        k: buf[9 + i] / n for i, k in enumerate(['candidates', 'partitions', 'leaf_ranks', 'walk'])}}))
+        k: buf[9 + i] / n for i, k in enumerate(['candidates', 'partitions', 'leaf_ranks', 'walk'])},
+        'max_ray_cycles': buf[13], 'max_partition_cycles': buf[14], 'heap_sorted_ranges': buf[15],
+        'wave_partitions_per_ray': buf[16] / n, 'cycles_per_partition': buf[17] / max(buf[16], 1),
+        'cycles_per_heap_range': buf[18] / max(buf[15], 1)}))
 
 
 if __name__ == '__main__':

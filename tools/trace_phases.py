@@ -38,7 +38,7 @@ def main():
         fn()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        buf = (ctypes.c_ulonglong * 16)()
+        buf = (ctypes.c_ulonglong * 24)()
         lib.sphrt_diag_trace_cycles(ctypes.cast(buf, ctypes.c_void_p), 0)
         n = max(buf[5], 1)
         ne = max(buf[8], 1)
