@@ -12,3 +12,7 @@ for c in c2 c3 c5; do
   timeout -k 10 120 python tools/pmc_trace.py --config $c --out gpurun_out/tpmc/r04_trace_${c}_pmc.json > gpurun_out/tpmc/pmc_$c.log 2>&1
 done
 ls gpurun_out/tpmc
+timeout -k 10 300 python tools/retrieval_bench.py --out gpurun_out/round/r04_retrieval_c5.json > gpurun_out/round/retrieval.log 2>&1
+head -c 400 gpurun_out/round/r04_retrieval_c5.json
+timeout -k 10 120 python tools/exact_stats.py > gpurun_out/round/r04_exact_stats.jsonl 2>&1
+cat gpurun_out/round/r04_exact_stats.jsonl
