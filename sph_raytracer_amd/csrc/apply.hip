@@ -522,8 +522,6 @@ struct Staged {
     double* len;
     float* len32;
 };
-constexpr int kStagedRows = (int)kSegPerBlock + 1;   // a block's rows start in its window
-constexpr size_t kStagedLds = (size_t)kStagedRows * (sizeof(int32_t) + sizeof(int64_t)) + 16;
 
 // Block b's gather: its rows (non-empty rows [k0, k1), each starting in the block's window) as
 // (start - s0, slot - start) in LDS when they fit in lds_cap bytes (else read from nz_row /
@@ -705,29 +703,165 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
 #ifndef SPHRT_RADIX_BITS
 #define SPHRT_RADIX_BITS 10
 #endif
-template <int ITEMS, int TM>
+// RB: bits per pass.  10 for the grids whose blocks all take the sort; 8 (a third pass, but 8 KB
+// of sort storage instead of 33 KB) behind the bucket tables, which leave the sort only the rare
+// block of many buckets: the kernel's LDS then fits 7 workgroups per CU instead of 4.
+template <int ITEMS, int TM, int RB = SPHRT_RADIX_BITS>
 struct RadixTable {
     // the count pass sorts keys only (its values are dead)
     using Sort = typename std::conditional<
         TM != kTabCount,
-        rocprim::block_radix_sort<uint32_t, kThreads, ITEMS, uint16_t, 1, 1, SPHRT_RADIX_BITS>,
+        rocprim::block_radix_sort<uint32_t, kThreads, ITEMS, uint16_t, 1, 1, RB>,
         rocprim::block_radix_sort<uint32_t, kThreads, ITEMS, rocprim::empty_type, 1, 1,
-                                  SPHRT_RADIX_BITS>>::type;
+                                  RB>>::type;
     using Storage = typename Sort::storage_type;
 };
+
+// One block's table from a two-level bitmap of its granules (the sort's result without a sort):
+// level 1 marks the occupied buckets of 512 granules (granule >> 9 < 2048: 64 words), its prefix
+// popcounts give each occupied bucket a slot; level 2 is one 16-word bitmap per slot.  A thread
+// per slot popcounts its bucket, one block scan ranks the buckets, and a granule's rank is its
+// bucket's base + the set bits below it.  Ascending distinct granules, the same tables and loc as
+// the sort.  A C3 block (1792 segments, ~640 granules) touches ~52 buckets (max ~90 in a traced
+// view; tools/table_sizes.py): blocks with more than kBucketSlots of them, or keys of more than
+// 20 bits, return false and take the sort.  SPHRT_TABLE_BUCKETS=0 builds the sort only.
+#ifndef SPHRT_TABLE_BUCKETS
+#define SPHRT_TABLE_BUCKETS 1
+#endif
+constexpr int kBucketLo = 9;                       // granules per bucket: 512 = 16 words
+constexpr int kBucketWords = 1 << (kBucketLo - 5);
+constexpr int kBucketL1 = 64;                      // level-1 words: buckets < 2048
+constexpr int kBucketSlots = 128;
+constexpr size_t kBucketLds = (2 * kBucketL1 + 4) * 4 + (size_t)kBucketSlots * kBucketWords * 6;
+template <int ITEMS, int TM, typename TabT>
+__device__ __forceinline__ bool bucket_table(int64_t* m, const int32_t* __restrict__ vox,
+                                             uint16_t* __restrict__ loc, TabT* __restrict__ tab_b,
+                                             int64_t s0, int n, int key_bits, const StageMap& sm,
+                                             unsigned char* lds, ScanShared& sh,
+                                             unsigned long long* stats, const uint32_t* xin) {
+    if (!SPHRT_TABLE_BUCKETS || key_bits > kBucketLo + 11) return false;
+    const int tid = threadIdx.x;
+    uint32_t* l1 = reinterpret_cast<uint32_t*>(lds);
+    int* pre1 = reinterpret_cast<int*>(l1 + kBucketL1);          // kBucketL1 + 1 (total last)
+    uint32_t* l2 = reinterpret_cast<uint32_t*>(pre1 + kBucketL1 + 4);
+    uint16_t* pre2 = reinterpret_cast<uint16_t*>(l2 + kBucketSlots * kBucketWords);
+    uint32_t gk[ITEMS];                           // granule, or ~0 past the block's segments
+    uint32_t va = 0u, hb = 0u;                    // voxel-in-granule (2 bits) and head bit each
+    static_assert(ITEMS <= 16, "two bits per item in one dword");
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const int p = xin ? i * kThreads + tid : tid * ITEMS + i;
+        gk[i] = 0xffffffffu;
+        if (p < n) {
+            const uint32_t x = xin ? xin[i] : (uint32_t)vox[s0 + p];
+            const uint32_t v = stage_col(x & ~kHead, sm);
+            gk[i] = v >> 2;
+            va |= (v & 3u) << (2 * i);
+            hb |= (x >> 31) << i;
+        }
+    }
+    if (tid < kBucketL1) l1[tid] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        if (gk[i] != 0xffffffffu) {
+            const uint32_t hi = gk[i] >> kBucketLo;
+            atomicOr(&l1[hi >> 5], 1u << (hi & 31));
+        }
+    }
+    __syncthreads();
+    if (tid < kBucketL1) {                       // wave 0: slots of the occupied buckets
+        const int c = __builtin_popcount(l1[tid]);
+        const int inc = wave_incl_sum(c);
+        pre1[tid] = inc - c;
+        if (tid == kBucketL1 - 1) pre1[kBucketL1] = inc;
+    }
+    __syncthreads();
+    const int nbk = pre1[kBucketL1];
+    if (nbk > kBucketSlots) {
+        __syncthreads();                          // (the sort reuses the LDS)
+        return false;
+    }
+    for (int w = tid; w < nbk * kBucketWords; w += kThreads) l2[w] = 0u;
+    __syncthreads();
+    uint32_t slot_w[ITEMS];                       // level-2 word of each segment's granule
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        slot_w[i] = 0u;
+        if (gk[i] != 0xffffffffu) {
+            const uint32_t hi = gk[i] >> kBucketLo, lo = gk[i] & ((1u << kBucketLo) - 1u);
+            const uint32_t w1 = l1[hi >> 5];
+            const int slot = pre1[hi >> 5] + __builtin_popcount(w1 & ((1u << (hi & 31)) - 1u));
+            slot_w[i] = (uint32_t)slot * kBucketWords + (lo >> 5);
+            atomicOr(&l2[slot_w[i]], 1u << (lo & 31));
+        }
+    }
+    __syncthreads();
+    int cnt = 0;
+    if (tid < nbk) {
+#pragma unroll
+        for (int j = 0; j < kBucketWords; ++j) cnt += __builtin_popcount(l2[tid * kBucketWords + j]);
+    }
+    int n_tab;
+    int run = block_excl_count(cnt, n_tab, sh);
+    if (TM != kTabFill) {
+        if (tid == 0) {
+            if (n_tab > kMaxGran) {
+                m[5] = -1;
+                atomicAdd(stats, 1ull);
+            } else {
+                m[5] = n_tab;
+                atomic_max_sparse(stats + 1, (unsigned long long)n_tab);
+            }
+        }
+        if (TM == kTabCount || n_tab > kMaxGran) return true;
+    }
+    if (tid < nbk) {
+        int w = 0;                                // level-1 word holding occupied bucket `tid`
+#pragma unroll
+        for (int step = kBucketL1 / 2; step > 0; step >>= 1)
+            if (w + step < kBucketL1 && pre1[w + step] <= tid) w += step;
+        uint32_t bits = l1[w];
+        for (int k = tid - pre1[w]; k > 0; --k) bits &= bits - 1;   // its (tid - pre1[w])-th bit
+        const uint32_t hi = (uint32_t)w * 32 + (uint32_t)__builtin_ctz(bits);
+        for (int j = 0; j < kBucketWords; ++j) {
+            pre2[tid * kBucketWords + j] = (uint16_t)run;
+            uint32_t b = l2[tid * kBucketWords + j];
+            while (b) {
+                const int k = __builtin_ctz(b);
+                b &= b - 1;
+                tab_b[run++] = (TabT)((hi << kBucketLo) | (uint32_t)(j * 32 + k));
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        if (gk[i] != 0xffffffffu) {
+            const int p = xin ? i * kThreads + tid : tid * ITEMS + i;
+            const uint32_t lo = gk[i] & 31u;
+            const int rank = pre2[slot_w[i]] + __builtin_popcount(l2[slot_w[i]] & ((1u << lo) - 1u));
+            loc[s0 + p] = loc_code(rank, (va >> (2 * i)) & 3u, ((hb >> i) & 1u) != 0);
+        }
+    }
+    return true;
+}
 
 // One block's table from a sort of its n <= ITEMS * kThreads segments (block-uniform call).
 // xin: the block's voxels already in registers (xin[i]: segment i * kThreads + t, the staged
 // gather's striped order — the sort takes any arrangement, each value carries its position),
 // else loaded from vox (segment ITEMS * t + i).
-template <int ITEMS, int TM, typename TabT>
+template <int ITEMS, int TM, typename TabT, int RB = SPHRT_RADIX_BITS>
 __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restrict__ vox,
                                             uint16_t* __restrict__ loc, TabT* __restrict__ tab_b,
                                             int64_t s0, int n, int key_bits, const StageMap& sm,
                                             unsigned char* ts_raw, uint32_t* last_key,
                                             ScanShared& sh, unsigned long long* stats,
                                             const uint32_t* xin = nullptr) {
-    using RT = RadixTable<ITEMS, TM>;
+    if (bucket_table<ITEMS, TM, TabT>(m, vox, loc, tab_b, s0, n, key_bits, sm, ts_raw, sh, stats,
+                                      xin))
+        return;
+    using RT = RadixTable<ITEMS, TM, RB>;
     auto& ts = *reinterpret_cast<typename RT::Storage*>(ts_raw);
     const int tid = threadIdx.x;
     uint32_t key[ITEMS];
@@ -792,23 +926,25 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
 // that deduplicated the granules before a smaller sort measured slower at C3, 1268 -> 1503 us,
 // and was removed in round 4.)  Blocks of more than 2048 segments (the last row's overhang; few) are left
 // to local_table_big_kernel: apart, this kernel is sized for the 8-key sort's registers (72
-// VGPRs, 7 waves per SIMD instead of 4 with the 16-key sort inline: C3 1244 -> 1120 us).
+// VGPRs, 7 waves per SIMD instead of 4 with the 16-key sort inline: C3 1244 -> 1120 us).  With
+// the bucket tables (round 4) 8 waves per SIMD: C3 1341 -> 1285 us.
 #ifndef SPHRT_TAB_WAVES
-#define SPHRT_TAB_WAVES 7   // minimum waves per SIMD the 8-key table kernel's registers aim for
+#define SPHRT_TAB_WAVES 8   // minimum waves per SIMD the 8-key table kernel's registers aim for
 #endif
-template <int TM, typename TabT, int ITEMS>
+template <int TM, typename TabT, int ITEMS, int RB = SPHRT_RADIX_BITS>
 constexpr size_t table_lds() {
-    return sizeof(typename RadixTable<ITEMS, TM>::Storage);
+    const size_t sort = sizeof(typename RadixTable<ITEMS, TM, RB>::Storage);
+    return sort > kBucketLds ? sort : kBucketLds;
 }
-template <int TM, typename TabT = int32_t>
+template <int TM, typename TabT = int32_t, int RB = SPHRT_RADIX_BITS>
 __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
     unsigned long long* stats, const double* __restrict__ len, float* __restrict__ len32,
     Staged S = Staged{}, int64_t n_blocks = 0) {
-    constexpr size_t kSortLds = table_lds<TM, TabT, 8>();
-    __shared__ __attribute__((aligned(16)))
-    unsigned char ts_raw[kSortLds > kStagedLds ? kSortLds : kStagedLds];
+    // (the staged gather's rows share it: up to ~1060 rows per block in LDS, more from global
+    // memory — a C3 block has ~13)
+    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, 8, RB>()];
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
     int64_t* m = blocks + kBlockFields * (int64_t)blockIdx.x;
@@ -829,7 +965,7 @@ __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_k
     }
     if (n > 8 * kThreads) return;                 // local_table_big_kernel's
     TabT* tab_b = tab + (int64_t)blockIdx.x * tab_stride;
-    radix_table<8, TM, TabT>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key, sh,
+    radix_table<8, TM, TabT, RB>(m, vox, loc, tab_b, s0, (int)n, key_bits, sm, ts_raw, last_key, sh,
                              stats, staged ? xs : nullptr);
 }
 
@@ -838,12 +974,12 @@ __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_k
 // grid of n_blocks / kBigScan workgroups (C3: ~6 % of the blocks are big; 256 blocks per
 // workgroup left ~25 sorts in series per workgroup, 110 us).
 constexpr int kBigScan = 32;
-template <int TM, typename TabT = int32_t>
+template <int TM, typename TabT = int32_t, int RB = SPHRT_RADIX_BITS>
 __global__ __launch_bounds__(kThreads) void local_table_big_kernel(
     int64_t* __restrict__ blocks, int64_t n_blocks, const int32_t* __restrict__ vox,
     uint16_t* __restrict__ loc, TabT* __restrict__ tab, int64_t tab_stride, int key_bits,
     StageMap sm, unsigned long long* stats) {
-    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, 16>()];
+    __shared__ __attribute__((aligned(16))) unsigned char ts_raw[table_lds<TM, TabT, 16, RB>()];
     __shared__ uint32_t last_key[kThreads];
     __shared__ ScanShared sh;
     __shared__ int n_big;
@@ -863,7 +999,7 @@ __global__ __launch_bounds__(kThreads) void local_table_big_kernel(
         const int64_t bb = (int64_t)blockIdx.x * kBigScan + big[i];
         int64_t* m = blocks + kBlockFields * bb;
         const int64_t s0 = m[2];
-        radix_table<16, TM, TabT>(m, vox, loc, tab + bb * tab_stride, s0, (int)(m[3] - s0),
+        radix_table<16, TM, TabT, RB>(m, vox, loc, tab + bb * tab_stride, s0, (int)(m[3] - s0),
                                   key_bits, sm, ts_raw, last_key, sh, stats);
         __syncthreads();                          // the sort storage is reused by the next one
     }
@@ -1684,6 +1820,14 @@ static int launch_tables(unsigned nb, hipStream_t st, int64_t* blocks, const int
                          uint16_t* loc, TabT* tab, int64_t stride, int kb, const StageMap& sm,
                          unsigned long long* stats, const double* len = nullptr,
                          float* len32 = nullptr, const Staged& S = Staged{}) {
+    if (SPHRT_TABLE_BUCKETS && kb <= kBucketLo + 11) {   // bucket tables, 8-bit sort behind
+        hipLaunchKernelGGL((local_table_radix_kernel<TM, TabT, 8>), dim3(nb), dim3(kThreads), 0, st,
+                           blocks, vox, loc, tab, stride, kb, sm, stats, len, len32, S, (int64_t)nb);
+        hipLaunchKernelGGL((local_table_big_kernel<TM, TabT, 8>), dim3((nb + kBigScan - 1) / kBigScan),
+                           dim3(kThreads), 0, st, blocks, (int64_t)nb, vox, loc, tab, stride, kb, sm,
+                           stats);
+        return check_launch("local_table_radix_kernel");
+    }
     hipLaunchKernelGGL((local_table_radix_kernel<TM, TabT>), dim3(nb), dim3(kThreads), 0, st,
                        blocks, vox, loc, tab, stride, kb, sm, stats, len, len32, S, (int64_t)nb);
     hipLaunchKernelGGL((local_table_big_kernel<TM, TabT>), dim3((nb + kBigScan - 1) / kBigScan),
