@@ -718,19 +718,19 @@ struct RadixTable {
 };
 
 // One block's table from a two-level bitmap of its granules (the sort's result without a sort):
-// level 1 marks the occupied buckets of 512 granules (granule >> 9 < 2048: 64 words), its prefix
+// level 1 marks the occupied buckets of 512 granules (granule >> 9 < 4096: 128 words), its prefix
 // popcounts give each occupied bucket a slot; level 2 is one 16-word bitmap per slot.  A thread
 // per slot popcounts its bucket, one block scan ranks the buckets, and a granule's rank is its
 // bucket's base + the set bits below it.  Ascending distinct granules, the same tables and loc as
 // the sort.  A C3 block (1792 segments, ~640 granules) touches ~52 buckets (max ~90 in a traced
-// view; tools/table_sizes.py): blocks with more than kBucketSlots of them, or keys of more than
-// 20 bits, return false and take the sort.  SPHRT_TABLE_BUCKETS=0 builds the sort only.
+// view): blocks with more than kBucketSlots of them, or keys of more than 21 bits, return false
+// and take the sort.  SPHRT_TABLE_BUCKETS=0 builds the sort only.
 #ifndef SPHRT_TABLE_BUCKETS
 #define SPHRT_TABLE_BUCKETS 1
 #endif
 constexpr int kBucketLo = 9;                       // granules per bucket: 512 = 16 words
 constexpr int kBucketWords = 1 << (kBucketLo - 5);
-constexpr int kBucketL1 = 64;                      // level-1 words: buckets < 2048
+constexpr int kBucketL1 = 128;                     // level-1 words: buckets < 4096
 constexpr int kBucketSlots = 128;
 constexpr size_t kBucketLds = (2 * kBucketL1 + 4) * 4 + (size_t)kBucketSlots * kBucketWords * 6;
 template <int ITEMS, int TM, typename TabT>
@@ -739,7 +739,7 @@ __device__ __forceinline__ bool bucket_table(int64_t* m, const int32_t* __restri
                                              int64_t s0, int n, int key_bits, const StageMap& sm,
                                              unsigned char* lds, ScanShared& sh,
                                              unsigned long long* stats, const uint32_t* xin) {
-    if (!SPHRT_TABLE_BUCKETS || key_bits > kBucketLo + 11) return false;
+    if (!SPHRT_TABLE_BUCKETS || key_bits > kBucketLo + 12) return false;
     const int tid = threadIdx.x;
     uint32_t* l1 = reinterpret_cast<uint32_t*>(lds);
     int* pre1 = reinterpret_cast<int*>(l1 + kBucketL1);          // kBucketL1 + 1 (total last)
@@ -770,11 +770,13 @@ __device__ __forceinline__ bool bucket_table(int64_t* m, const int32_t* __restri
         }
     }
     __syncthreads();
-    if (tid < kBucketL1) {                       // wave 0: slots of the occupied buckets
-        const int c = __builtin_popcount(l1[tid]);
+    if (tid < 64) {                               // wave 0: slots of the occupied buckets
+        static_assert(kBucketL1 == 128, "two level-1 words per lane");
+        const int a = __builtin_popcount(l1[2 * tid]), c = a + __builtin_popcount(l1[2 * tid + 1]);
         const int inc = wave_incl_sum(c);
-        pre1[tid] = inc - c;
-        if (tid == kBucketL1 - 1) pre1[kBucketL1] = inc;
+        pre1[2 * tid] = inc - c;
+        pre1[2 * tid + 1] = inc - c + a;
+        if (tid == 63) pre1[kBucketL1] = inc;
     }
     __syncthreads();
     const int nbk = pre1[kBucketL1];
@@ -1820,7 +1822,9 @@ static int launch_tables(unsigned nb, hipStream_t st, int64_t* blocks, const int
                          uint16_t* loc, TabT* tab, int64_t stride, int kb, const StageMap& sm,
                          unsigned long long* stats, const double* len = nullptr,
                          float* len32 = nullptr, const Staged& S = Staged{}) {
-    if (SPHRT_TABLE_BUCKETS && kb <= kBucketLo + 11) {   // bucket tables, 8-bit sort behind
+    // bucket tables, 8-bit sort behind (keys of 21 bits keep the 10-bit one: the transposed
+    // tables' rays from every view span more buckets than a block has slots, and sort)
+    if (SPHRT_TABLE_BUCKETS && kb <= kBucketLo + 11) {
         hipLaunchKernelGGL((local_table_radix_kernel<TM, TabT, 8>), dim3(nb), dim3(kThreads), 0, st,
                            blocks, vox, loc, tab, stride, kb, sm, stats, len, len32, S, (int64_t)nb);
         hipLaunchKernelGGL((local_table_big_kernel<TM, TabT, 8>), dim3((nb + kBigScan - 1) / kBigScan),

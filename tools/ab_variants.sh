@@ -9,7 +9,7 @@ C=$1; P=$2; shift 2
 O=gpurun_out/ab; mkdir -p $O
 for v in tree "$@"; do
   lib=""; [ $v != tree ] && lib=sph_raytracer_amd/lib/variants/libsphrt_$v.so
-  SPHRT_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_${C}_$v -o run --output-format csv -- python tools/operator_time.py --config $C --reps 5 > $O/op_${C}_$v.json 2>$O/op_${C}_$v.err
+  SPHRT_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_${C}_$v -o run --output-format csv -- python tools/operator_time.py --config $C --reps 5 $OPT_ARGS > $O/op_${C}_$v.json 2>$O/op_${C}_$v.err
   f=$(find $O/prof_${C}_$v -name "*kernel_stats.csv"); cp $f $O/${C}_${v}_kernel_stats.csv
   echo "== $v $(cat $O/op_${C}_$v.json)"; grep -iE "$P" $f | cut -d, -f1-4 | cut -c1-150 || true
 done

@@ -21,6 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='c3')
     ap.add_argument('--reps', type=int, default=7)
+    ap.add_argument('--adjoint', action='store_true',
+                    help='also the first op.T(y) of each Operator (builds the transposed CSR)')
     args = ap.parse_args()
     import bench
     from sph_raytracer_amd import Operator
@@ -29,20 +31,24 @@ def main():
     grid, geom = bench.build_geometry(cfg, 0, 1)
     x = torch.rand(cfg[0], dtype=cfg[4], device=dev)
     op = Operator(grid, geom, device=dev)        # warm-up: HIP and allocator initialisation
-    op(x)
+    y = op(x)
+    if args.adjoint:
+        op.T(y)
     del op
     times = []
     for _ in range(args.reps):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         op = Operator(grid, geom, device=dev)
-        op(x)
+        y = op(x)
+        if args.adjoint:
+            op.T(y)
         torch.cuda.synchronize(dev)
         times.append(time.perf_counter() - t0)
         del op
     times.sort()
     env = {k: v for k, v in os.environ.items() if k.startswith('SPHRT_')}
-    print(json.dumps({'config': args.config, 'operator_ms_median': 1e3 * times[len(times) // 2],
+    print(json.dumps({'config': args.config, 'adjoint': args.adjoint, 'operator_ms_median': 1e3 * times[len(times) // 2],
                       'operator_ms_min': 1e3 * times[0], 'reps': args.reps, 'env': env}))
 
 
