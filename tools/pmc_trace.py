@@ -28,6 +28,8 @@ def main():
     ap.add_argument('--count-pass', action='store_true',
                     help='profile tools/trace_time.py (the two-pass COUNT kernel, which the '
                          'SPHRT_TRACE_ABL ablation builds cut short) instead of trace_bench.py')
+    ap.add_argument('--match', default='trace_kernel',
+                    help='kernels whose name contains this (e.g. screen_kernel)')
     args = ap.parse_args()
     counters = args.counters.split(',') if args.counters else COUNTERS
     d = os.path.join(ROOT, 'gpurun_out', 'pmc_trace')
@@ -42,13 +44,13 @@ def main():
     for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r['Kernel_Name'].split('(')[0].replace('void ', '')
-            if 'trace_kernel' in name:
+            if args.match in name:
                 vals[name][r['Counter_Name']].append(float(r['Counter_Value']))
     dur = defaultdict(list)
     for f in glob.glob(os.path.join(d, '**', '*kernel_trace.csv'), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r['Kernel_Name'].split('(')[0].replace('void ', '')
-            if 'trace_kernel' in name:
+            if args.match in name:
                 dur[name].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) * 1e-9)
     rec = {'config': args.config, 'counters': counters, 'lib': os.environ.get('SPHRT_LIB'),
            'kernels': {}}
