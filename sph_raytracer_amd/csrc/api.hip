@@ -202,6 +202,15 @@ static sphrt_plan* plan_over(const sphrt_grid_desc* gd, int device, void* dmem, 
     for (int j = 1; j < G.nba; ++j) a_asc &= gd->a_b[j] > gd->a_b[j - 1] ? 1 : 0;
     G.e_asc = e_asc;
     G.a_asc = a_asc;
+    // evenly spaced boundaries (linspace grids): within 1e-9 of a spacing of b0 + i h
+    auto even = [](const double* b, int n) {
+        if (n < 2 || !(b[n - 1] > b[0])) return 0;
+        const double h = (b[n - 1] - b[0]) / (n - 1);
+        for (int i = 0; i < n; ++i)
+            if (!(fabs(b[i] - (b[0] + i * h)) <= 1e-9 * h)) return 0;
+        return 1;
+    };
+    G.uni = even(gd->r_b, G.nbr) | (even(gd->e_b, G.nbe) << 1) | (even(gd->a_b, G.nba) << 2);
     G.r_b = (const double*)dmem;   // the rest of the block follows it (GridDev accessors)
     return p;
 }

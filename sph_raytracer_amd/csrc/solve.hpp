@@ -27,6 +27,7 @@ struct GridDev {
     double plane_par_tol;  // a_torch parallel threshold (raytracer.py:521)
     double r_outer;        // r_b[nr]
     int e_asc, a_asc;      // e_b / a_b strictly ascending (segment bounds may binary-search them)
+    int uni;               // bit 0 / 1 / 2: r_b / e_b / a_b evenly spaced (counted arithmetically)
     // One table block: r_b (nbr) | cos(e_b)**2 (nbe) | cos(a_b) (nba) | sin(a_b) (nba) | e_b (nbe)
     // | a_b (nba) as doubles, then e_flags (nbe bytes; bit0: cos(e_b) >= 0, bit1: shadow test
     // exempt, e_b ~ pi/2).  One pointer instead of seven: the trace kernel's arguments stay in

@@ -1101,9 +1101,25 @@ __device__ __forceinline__ int first_ge(const double* b, int n, double v) {
     }
     return lo;
 }
-// Entries of the ascending b[0, n) inside [lo, hi].
-__device__ __forceinline__ int count_in(const double* b, int n, double lo, double hi) {
+// Evenly spaced b (GridDev::uni): the index range from the spacing, widened by 1e-6 of a spacing
+// (a superset of the binary search's: the counts are upper bounds) — no chain of dependent LDS
+// loads.  C3 screen 126.5 -> 107.0 us, the same bound totals at C2 / C3 / C5
+// (tools/bound_check.py); the bound itself costs ~25 us of it (ablated: 101 us).
+__device__ __forceinline__ int first_ge_even(const double* b, int n, double v) {
+    const double x = (v - b[0]) * ((n - 1) / (b[n - 1] - b[0])) - 1e-6;
+    return x <= 0.0 ? 0 : x >= (double)n ? n : (int)__builtin_ceil(x);
+}
+// Entries of the ascending b[0, n) inside [lo, hi] (an upper bound when `even`).
+__device__ __forceinline__ int count_in(const double* b, int n, double lo, double hi,
+                                        bool even = false) {
     if (!(lo <= hi)) return 0;
+    if (even) {
+        const double ih = (n - 1) / (b[n - 1] - b[0]);
+        const double xa = (lo - b[0]) * ih - 1e-6, xz = (hi - b[0]) * ih + 1e-6;
+        const int a = xa <= 0.0 ? 0 : xa >= (double)n ? n : (int)__builtin_ceil(xa);
+        const int z = xz < 0.0 ? -1 : xz >= (double)(n - 1) ? n - 1 : (int)__builtin_floor(xz);
+        return z >= a ? z - a + 1 : 0;
+    }
     const int a = first_ge(b, n, lo);
     int l = a, h = n;                                   // first entry > hi
     while (l < h) {
@@ -1139,7 +1155,9 @@ __device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok, c
     const double ta = fmax(g.tc - t1c, 0.0), tb = g.tc + t1c;
     if (!(tb >= ta)) return 2;                       // (NaN: a miss; behind the start: nothing)
     const double eps = 1e-9;
-    const int n_s = G.nbr - first_ge(rb, G.nbr, g.dd * (1.0 - 1e-12));
+    const int n_s = G.nbr - ((G.uni & 1)
+                                 ? first_ge_even(rb, G.nbr, g.dd * (1.0 - 1e-12))
+                                 : first_ge(rb, G.nbr, g.dd * (1.0 - 1e-12)));
     const double ax = g.x0 + ta * g.w0, ay = g.x1 + ta * g.w1, az = g.x2 + ta * g.w2;
     const double bx = g.x0 + tb * g.w0, by = g.x1 + tb * g.w1, bz = g.x2 + tb * g.w2;
     int b_a = G.nba;
@@ -1160,7 +1178,7 @@ __device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok, c
             const int k1 = min(2, (int)__builtin_floor((a_hi - lo) / two_pi) + 1);
             int c = 0;
             for (int k = k0; k <= k1; ++k)
-                c += count_in(ab, G.nba, lo + k * two_pi, hi + k * two_pi);
+                c += count_in(ab, G.nba, lo + k * two_pi, hi + k * two_pi, G.uni & 4);
             if (__builtin_isfinite(lo) && __builtin_isfinite(hi)) b_a = min(c + 2, G.nba);
         }
     }
@@ -1173,10 +1191,10 @@ __device__ int segment_bound(const GridDev& G, const RayGeo& g, bool start_ok, c
         int c;
         if (ts > ta && ts < tb) {
             const double th_s = polar(g.x0 + ts * g.w0, g.x1 + ts * g.w1, g.x2 + ts * g.w2);
-            c = count_in(eb, G.nbe, fmin(th_a, th_s) - m, fmax(th_a, th_s) + m) +
-                count_in(eb, G.nbe, fmin(th_s, th_b) - m, fmax(th_s, th_b) + m);
+            c = count_in(eb, G.nbe, fmin(th_a, th_s) - m, fmax(th_a, th_s) + m, G.uni & 2) +
+                count_in(eb, G.nbe, fmin(th_s, th_b) - m, fmax(th_s, th_b) + m, G.uni & 2);
         } else {
-            c = count_in(eb, G.nbe, fmin(th_a, th_b) - m, fmax(th_a, th_b) + m);
+            c = count_in(eb, G.nbe, fmin(th_a, th_b) - m, fmax(th_a, th_b) + m, G.uni & 2);
         }
         if (__builtin_isfinite(th_a) && __builtin_isfinite(th_b)) b_e = min(c + 4, 2 * G.nbe);
     }
@@ -1229,10 +1247,21 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
     }
     const bool listed = hit;
     const uint64_t m = __ballot(listed);
-    if (m == 0) return;
     unsigned base = 0;
-    if (lane == __builtin_ctzll(m)) base = atomicAdd(o.n_hits, (unsigned)__popcll(m));
-    base = __shfl(base, __builtin_ctzll(m));
+    // one atomic per workgroup on the list's counter instead of one per wave: all waves with a
+    // hit queue on that one address (C3 screen 200 -> 127 us, C5 55 -> 31 us)
+    __shared__ unsigned wcnt[4], wbase;
+    const int wid = threadIdx.x >> 6;
+    if (lane == 0) wcnt[wid] = (unsigned)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        wbase = tot ? atomicAdd(o.n_hits, tot) : 0u;
+    }
+    __syncthreads();
+    if (m == 0) return;
+    base = wbase;
+    for (int w = 0; w < wid; ++w) base += wcnt[w];
     if (listed) {
         HitRay h;
         h.g = g;

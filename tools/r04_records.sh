@@ -16,3 +16,5 @@ timeout -k 10 300 python tools/retrieval_bench.py --out gpurun_out/round/r04_ret
 head -c 400 gpurun_out/round/r04_retrieval_c5.json
 timeout -k 10 120 python tools/exact_stats.py > gpurun_out/round/r04_exact_stats.jsonl 2>&1
 cat gpurun_out/round/r04_exact_stats.jsonl
+timeout -k 10 120 python tools/bound_check.py > gpurun_out/round/r04_bound_check.jsonl 2>&1
+cat gpurun_out/round/r04_bound_check.jsonl
