@@ -177,6 +177,12 @@ int sphrt_trace_compact(int64_t n, const int64_t *bound_ptr, const int32_t *svox
  * the same with r*cos and r*sin rounded to float (the host tensors are float32). */
 int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const double *frame,
                     const double *row, const double *col, double *rays, void *stream);
+/* The same rays in a per-view trace order (the ConeCirc wedge order of the Operator's trace):
+ * rays[v][k] is pixel order[k] of view v (order: a permutation of the h*w pixels, device
+ * memory) and ray_id[v*h*w + k] = v*h*w + order[k] (int32; n_views*h*w < 2^31). */
+int sphrt_rays_cone_ordered(int64_t n_views, int64_t h, int64_t w, int circ, const double *frame,
+                            const double *row, const double *col, const int64_t *order,
+                            double *rays, int32_t *ray_id, void *stream);
 
 /* ---- row index of the trace, built once (the apply kernels' work partition) ---------------- */
 /* A traced operator: the CSR above plus

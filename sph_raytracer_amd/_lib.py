@@ -80,6 +80,8 @@ _SIGNATURES = [
                                  c_vp, ctypes.c_size_t, c_vp]),
     ('sphrt_trace_compact', c_int, [c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ('sphrt_rays_cone', c_int, [c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ('sphrt_rays_cone_ordered', c_int, [c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                        c_vp, c_vp]),
     ('sphrt_csr_blocks', c_i64, [c_i64]),
     ('sphrt_csr_index_workspace_bytes', ctypes.c_size_t, [c_i64]),
     ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),

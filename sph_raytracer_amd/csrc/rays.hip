@@ -19,12 +19,16 @@ __global__ __launch_bounds__(256) void cone_rays_kernel(int64_t n_views, int64_t
                                                         int circ, const double* __restrict__ frame,
                                                         const double* __restrict__ row,
                                                         const double* __restrict__ col,
-                                                        double* __restrict__ rays) {
+                                                        double* __restrict__ rays,
+                                                        const int64_t* __restrict__ order,
+                                                        int32_t* __restrict__ ray_id) {
     const int64_t n = n_views * h * w;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t view = i / (h * w);
-        const int64_t pix = i - view * h * w;
+        const int64_t slot = i - view * h * w;
+        const int64_t pix = order ? order[slot] : slot;   // the pixel this trace row holds
+        if (ray_id) ray_id[i] = (int32_t)(view * h * w + pix);
         const int64_t a = pix / w, b = pix - a * w;
         const double* f = frame + 9 * view;          // look, right, up
         double p, q;                                 // coefficients of right and up
@@ -58,16 +62,35 @@ __global__ __launch_bounds__(256) void cone_rays_kernel(int64_t n_views, int64_t
 
 using namespace sphrt;
 
-extern "C" int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ,
-                               const double* frame, const double* row, const double* col,
-                               double* rays, void* stream) {
+static int rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const double* frame,
+                     const double* row, const double* col, double* rays, const int64_t* order,
+                     int32_t* ray_id, void* stream) {
     if (n_views < 0 || h < 0 || w < 0) return fail("bad detector shape");
     if (!frame || !row || !col || !rays) return fail("null pointer");
     const int64_t n = n_views * h * w;
     if (n == 0) return 0;
+    if (ray_id && n > 0x7fffffff) return fail("too many rays for int32 ray ids");
     StreamGuard guard(stream);
     const int64_t blocks = (n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536;
     hipLaunchKernelGGL(cone_rays_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                       n_views, h, w, circ, frame, row, col, rays);
+                       n_views, h, w, circ, frame, row, col, rays, order, ray_id);
     return check_launch("cone_rays_kernel");
+}
+
+extern "C" int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ,
+                               const double* frame, const double* row, const double* col,
+                               double* rays, void* stream) {
+    return rays_cone(n_views, h, w, circ, frame, row, col, rays, nullptr, nullptr, stream);
+}
+
+// The same rays in a per-view trace order: row k of view v holds pixel order[k] (a permutation
+// of the h * w pixels, on the device), ray_id[v h w + k] = v h w + order[k].  One launch instead
+// of generating, gathering (index_select) and numbering the rays in four (C5 Operator: the ray
+// ids' torch arithmetic and the gather with their host gaps).
+extern "C" int sphrt_rays_cone_ordered(int64_t n_views, int64_t h, int64_t w, int circ,
+                                       const double* frame, const double* row, const double* col,
+                                       const int64_t* order, double* rays, int32_t* ray_id,
+                                       void* stream) {
+    if (!order || !ray_id) return fail("null pointer");
+    return rays_cone(n_views, h, w, circ, frame, row, col, rays, order, ray_id, stream);
 }

@@ -243,12 +243,22 @@ class _ConeRays:
     def stage(self, staging):
         self.slot = staging.add(self.host)
 
-    def launch(self, dev, staging=None):
-        """The rays (*shape, 3) on `dev`, from the staged copy or a copy of their own."""
+    def launch(self, dev, staging=None, order=None):
+        """The rays (*shape, 3) on `dev`, from the staged copy or a copy of their own.  order (a
+        device int64 permutation of a view's pixels): each view's rays in that order, returned
+        with the geometry ray of every row (int32) — _permute_rays in the generating launch."""
         packed = staging.get(self.slot, self.host) if staging is not None else self.host.to(dev)
         frame_d, row_d, col_d = packed.split(self.sizes)
         rays = tr.empty(self.shape + (3,), dtype=tr.float64, device=dev)
-        _lib.check(_lib.load().sphrt_rays_cone(
+        lib = _lib.load()
+        if order is not None:
+            ray_id = tr.empty(math.prod(self.shape), dtype=tr.int32, device=dev)
+            _lib.check(lib.sphrt_rays_cone_ordered(
+                self.n_views, self.h, self.w, int(self.circ), _lib.ptr(frame_d), _lib.ptr(row_d),
+                _lib.ptr(col_d), _lib.ptr(order), _lib.ptr(rays), _lib.ptr(ray_id),
+                _lib.stream_of(dev)), 'sphrt_rays_cone_ordered')
+            return rays, ray_id
+        _lib.check(lib.sphrt_rays_cone(
             self.n_views, self.h, self.w, int(self.circ), _lib.ptr(frame_d), _lib.ptr(row_d),
             _lib.ptr(col_d), _lib.ptr(rays), _lib.stream_of(dev)), 'sphrt_rays_cone')
         return rays
@@ -829,15 +839,25 @@ class Operator:
         stg = _Staging()
         self._plan = _Plan(self.grid, dev, staging=stg)
         cone = _ConeRays.of(self.geom)
+        perm, s_perm = None, None
         if cone is not None:
             cone.stage(stg)
+            perm = _trace_order(self.geom, tr.empty(cone.shape + (3,), device='meta'))
+            if perm is not None and perm.numel() == cone.h * cone.w:   # per view: staged too
+                s_perm = stg.add(perm)
         xs_h, st_h = _RayBatch.host_starts(self.grid, self.geom.ray_starts)
         s_xs, s_st = stg.add(xs_h), stg.add(st_h)
         stg.upload(dev)
         self._plan.attach(stg)
-        rays = cone.launch(dev, stg) if cone is not None else self.geom.rays
-        perm = _trace_order(self.geom, rays)
         ray_id = None
+        if s_perm is not None:         # trace in wedges, generated in that order
+            rays, ray_id = cone.launch(dev, stg, order=stg.get(s_perm, perm))
+            perm = None
+        elif cone is not None:
+            rays = cone.launch(dev, stg)
+        else:
+            rays = self.geom.rays
+            perm = _trace_order(self.geom, rays)
         xs_d, st_d = stg.get(s_xs, xs_h), stg.get(s_st, st_h)
         if perm is not None and rays.dim() == 4 and perm.numel() > math.prod(rays.shape[-3:-1]):
             # an order across views (studies): starts and start voxels follow their rays

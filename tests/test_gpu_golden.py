@@ -168,6 +168,31 @@ def test_device_rays_bit_identical(gpu):
         assert tr.equal(got.cpu(), g.rays), type(g).__name__
 
 
+def test_device_rays_in_trace_order(gpu):
+    """sphrt_rays_cone_ordered: each view's rays generated in a per-view pixel order equal the
+    geometry's rays gathered in that order, bit for bit, and every row's ray id is its geometry
+    ray (the ConeCirc wedge order of the Operator's trace, and a random permutation)."""
+    import torch as tr
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom
+    from sph_raytracer_amd.raytracer import _ConeRays, _wedge_order
+    th = tr.linspace(0, 2 * tr.pi, 5)
+    cases = [
+        sum(ConeCircGeom((30, 24), pos=(5 * tr.cos(a), 5 * tr.sin(a), 1), fov=(0, 45)) for a in th),
+        ConeCircGeom((9, 13), pos=(2, 3, 4), fov=(5, 40), spacing='log'),
+        sum(ConeRectGeom((12, 20), pos=(5 * tr.cos(a), 5 * tr.sin(a), 1)) for a in th),
+    ]
+    gen = tr.Generator().manual_seed(5)
+    for g in cases:
+        cone = _ConeRays.of(g)
+        h, w = cone.h, cone.w
+        for perm in (_wedge_order(h, w), tr.randperm(h * w, generator=gen)):
+            rays, ray_id = cone.launch(gpu, order=perm.to(gpu))
+            flat = g.rays.reshape(cone.n_views, h * w, 3)
+            assert tr.equal(rays.cpu().reshape(cone.n_views, h * w, 3), flat[:, perm])
+            want = (tr.arange(cone.n_views)[:, None] * (h * w) + perm).reshape(-1).to(tr.int32)
+            assert tr.equal(ray_id.cpu(), want)
+
+
 def _csr(op):
     c = op._csr
     return (c['row_ptr'].cpu(), c['vox'][:c['total']].cpu(), c['len'][:c['total']].cpu())
