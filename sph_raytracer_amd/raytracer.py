@@ -132,7 +132,17 @@ class _Staging:
         return len(self._offs) - 1
 
     def upload(self, dev):
-        self._dev = tr.concat(self._parts).to(dev) if self._parts else None
+        """One host-to-device copy of the blobs, from pinned memory (torch's caching host
+        allocator) so the host goes on to launch the first kernels while it runs."""
+        if not self._parts:
+            self._dev = None
+            return
+        if tr.device(dev).type == 'cuda' and os.environ.get('SPHRT_PINNED_UPLOAD', '1') != '0':
+            buf = tr.empty(self._size, dtype=tr.uint8, pin_memory=True)
+            tr.cat(self._parts, out=buf)
+            self._dev = buf.to(dev, non_blocking=True)
+        else:
+            self._dev = tr.concat(self._parts).to(dev)
 
     def get(self, slot, like):
         """The device copy of slot `slot` with the dtype and shape of host tensor `like`."""
