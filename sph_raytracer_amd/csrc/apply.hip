@@ -724,7 +724,9 @@ struct RadixTable {
 // bucket's base + the set bits below it.  Ascending distinct granules, the same tables and loc as
 // the sort.  A C3 block (1792 segments, ~640 granules) touches ~52 buckets (max ~90 in a traced
 // view): blocks with more than kBucketSlots of them, or keys of more than 21 bits, return false
-// and take the sort.  SPHRT_TABLE_BUCKETS=0 builds the sort only.
+// and take the sort.  SPHRT_TABLE_BUCKETS=0 builds the sort only; at run time the environment
+// variable of that name set to 0 sorts every block (tests: bucket tables == sorted tables), the
+// launch marking key_bits with kSortOnly.
 #ifndef SPHRT_TABLE_BUCKETS
 #define SPHRT_TABLE_BUCKETS 1
 #endif
@@ -732,6 +734,7 @@ constexpr int kBucketLo = 9;                       // granules per bucket: 512 =
 constexpr int kBucketWords = 1 << (kBucketLo - 5);
 constexpr int kBucketL1 = 128;                     // level-1 words: buckets < 4096
 constexpr int kBucketSlots = 128;
+constexpr int kSortOnly = 256;                     // key_bits flag: no bucket tables
 constexpr size_t kBucketLds = (2 * kBucketL1 + 4) * 4 + (size_t)kBucketSlots * kBucketWords * 6;
 template <int ITEMS, int TM, typename TabT>
 __device__ __forceinline__ bool bucket_table(int64_t* m, const int32_t* __restrict__ vox,
@@ -880,8 +883,9 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
             val[i] = (uint16_t)((p << 3) | ((x >> 31) << 2) | (v & 3u));
         }
     }
-    if constexpr (TM != kTabCount) typename RT::Sort().sort(key, val, ts, 0, key_bits);  // blocked:
-    else typename RT::Sort().sort(key, ts, 0, key_bits);         // thread t: [ITEMS t, ITEMS t + ITEMS)
+    const int kbits = key_bits & (kSortOnly - 1);
+    if constexpr (TM != kTabCount) typename RT::Sort().sort(key, val, ts, 0, kbits);  // blocked:
+    else typename RT::Sort().sort(key, ts, 0, kbits);         // thread t: [ITEMS t, ITEMS t + ITEMS)
     last_key[tid] = key[ITEMS - 1];
     __syncthreads();
     uint32_t prev = tid > 0 ? last_key[tid - 1] : 0xffffffffu;
@@ -1822,6 +1826,8 @@ static int launch_tables(unsigned nb, hipStream_t st, int64_t* blocks, const int
                          uint16_t* loc, TabT* tab, int64_t stride, int kb, const StageMap& sm,
                          unsigned long long* stats, const double* len = nullptr,
                          float* len32 = nullptr, const Staged& S = Staged{}) {
+    const char* env = getenv("SPHRT_TABLE_BUCKETS");   // (read per build: tests toggle it)
+    if (env && env[0] == '0') kb |= kSortOnly;
     // bucket tables, 8-bit sort behind (keys of 21 bits keep the 10-bit one: the transposed
     // tables' rays from every view span more buckets than a block has slots, and sort)
     if (SPHRT_TABLE_BUCKETS && kb <= kBucketLo + 11) {

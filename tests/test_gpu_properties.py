@@ -1190,6 +1190,58 @@ def test_gd_direct_declines_what_it_cannot_run(gpu, monkeypatch):
     assert tr.equal(c1.cpu(), ca.cpu())
 
 
+@pytest.mark.parametrize('case', ['c3_views', 'long_rows', 'c4_paired', 'c3_adjoint'])
+def test_bucket_tables_equal_sorted_tables(case, gpu, monkeypatch):
+    """The granule tables from the two-level bucket bitmaps (apply.hip bucket_table) equal the
+    block radix sort's bit for bit — blocks, loc, every used table entry (SPHRT_TABLE_BUCKETS=0
+    sorts every block): C3-like 20-bit keys (buckets, the 8-bit sort behind), long rows (blocks
+    over 2048 segments: the 16-key kernel), C4-like time-paired tables (21-bit keys) and C3-like
+    transposed tables (21-bit keys, many blocks past the bucket slots: the 10-bit sort)."""
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom, Operator, SphericalGrid
+    dynamic = case == 'c4_paired'
+    if case in ('c3_views', 'c3_adjoint'):
+        grid, geom = _orbit(6, (32, 64), grid_shape=(128, 128, 128))
+    elif case == 'long_rows':
+        grid = SphericalGrid(shape=(2500, 16, 16))
+        geom = ConeRectGeom((6, 8), pos=(3, 0.01, 0.02), fov=(3, 3))
+    else:
+        th = tr.linspace(0, 2 * tr.pi, 36)      # 36 slices x 50^3: 2^20+ granules, 21-bit keys
+        grid = SphericalGrid(shape=(36, 50, 50, 50))
+        geom = sum(ConeCircGeom(shape=(20, 30), pos=(5 * tr.cos(a), 5 * tr.sin(a), 1), fov=(0, 45))
+                   for a in th)
+
+    def tables(flag):
+        monkeypatch.setenv('SPHRT_TABLE_BUCKETS', flag)
+        op = Operator(grid, geom, device=gpu, dynamic=dynamic)
+        csr = op._csr
+        if case == 'c3_adjoint':
+            keep = op._transposed()['keep']
+            blocks, loc, tab, stride = keep[6], keep[7], keep[8], op._transposed()['desc'].tab_stride
+        elif case == 'c4_paired':
+            op(tr.rand(grid.shape, dtype=tr.float32, device=gpu))
+            pair = [v for k, v in csr.items() if isinstance(k, tuple) and k[0] == 'paired']
+            assert pair and pair[0] is not None
+            blocks, loc, tab = pair[0]['keep'][1:4]
+            stride = pair[0]['desc'].tab_stride
+        else:
+            blocks, loc, tab, stride = csr['blocks'], csr['loc'], csr['tab'], csr['desc'].tab_stride
+        n_seg = csr['total']
+        bl = blocks.cpu().view(-1, 6)
+        tab = tab.cpu()
+        n_tab = bl[:, 5].tolist()
+        used = tr.cat([tab[b * stride:b * stride + k] for b, k in enumerate(n_tab) if k > 0]
+                      or [tab[:0]])
+        keep = tr.zeros(n_seg, dtype=tr.bool)
+        for b, k in enumerate(n_tab):
+            if k >= 0:
+                keep[int(bl[b, 2]):int(bl[b, 3])] = True
+        return bl, used, loc[:n_seg].cpu()[keep]
+
+    a, b = tables('1'), tables('0')
+    for name, x, y in zip(('blocks', 'tab', 'loc'), a, b):
+        assert tr.equal(x, y), name
+
+
 @pytest.mark.parametrize('case', ['c3_views', 'long_rows', 'c2_views', 'tiny_grid'])
 def test_staged_table_build_equals_compaction(case, gpu, monkeypatch):
     """The one-pass trace's staging moved into the CSR by the table build
