@@ -1,14 +1,22 @@
 #!/usr/bin/env python3
 """Benchmark: steady-state forward Operator throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c5] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5]
+                    [--scaling weak|strong] [--no-cpu-baseline] [--no-strong-legs]
 
 Workload (default, BASELINE configs[1] = SURVEY §8(d) C2): a (50,50,50) SphericalGrid seen by a
 circular orbit of 50 ConeRectGeom((50,100), fov=(45,45)) views, 250,000 rays, float32 density.
 A step is one ``op(x)`` forward call on the cached trace (the reference's Operator.__call__,
 raytracer.py:692-713) — the drop-in call including its host overhead.  With N GPUs (one process
-each, torchrun) every rank traces its own 50-view slice of a 50*N-view orbit (weak scaling) and
-the image stack is all-gathered over RCCL every step (the only exchange of the path).
+each, torchrun or this script's own launcher) every rank traces its own 50-view slice of a
+50*N-view orbit (weak scaling); views are independent, so the step has no collective, and the
+image stack is all-gathered over RCCL once after the loop.
+
+Strong scaling (BASELINE configs[3] and [4] as defined): ``--scaling strong --config c4`` shards
+ONE 50-view / 50-slice dynamic volume over the ranks (each rank its own time slices; a step is
+its forward + dynamic gradient), ``--config c5`` times the static_retrieval.py gd loop with the
+64 views sharded (one gradient all_reduce per iteration; a step is one iteration).  The default
+C2 run reports both legs too (``strong``), each checked against one GPU over the whole orbit.
 
 One JSON line on rank 0: value = rays/s over all ranks; roofline of the forward kernel
 (algorithmic bytes per launch / its mean duration from HIP events over graph-replayed
@@ -181,6 +189,305 @@ def cpu_baseline(cfg, sample_views, reps):
             'host_cpus': os.cpu_count()}
 
 
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-300))
+
+
+class _Ranks:
+    """This process's place in the job: the process group (None at N=1), its GPU, and the
+    collective helpers every leg shares (a barrier + device sync; the max of host floats over
+    ranks)."""
+
+    def __init__(self, dist, dev, world, rank):
+        self.dist, self.dev, self.world, self.rank = dist, dev, world, rank
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+        torch.cuda.synchronize(self.dev)
+
+    def max_over_ranks(self, vals):
+        if self.dist is None:
+            return list(vals)
+        on = self.dev if self.dist.get_backend() == 'nccl' else 'cpu'
+        tt = torch.tensor(vals, dtype=torch.float64, device=on)
+        self.dist.all_reduce(tt, op=self.dist.ReduceOp.MAX)
+        return tt.tolist()
+
+    def timed(self, fn, reps):
+        """Run fn() `reps` times between barrier + sync brackets -> max seconds over ranks."""
+        self.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(self.dev)
+        self.barrier()
+        return self.max_over_ranks([time.perf_counter() - t0])[0]
+
+
+def strong_c4(rk, steps, warmup, check=True):
+    """BASELINE configs[3], strong-scaled: ONE dynamic (50,50,50,50) volume seen by a 50-view
+    ConeCirc (100,50) orbit with view i <-> time slice i (examples/dynamic_measurements.py:18-48,
+    raytracer.py:703-712), its 50 views and their time slices sharded over the ranks (7,7,6,...
+    at N=8: SURVEY §8(e)) through ShardedOperator.  A step is this rank's forward of its slices
+    plus its gradient of 0.5*||A x - m||^2 (the residual, then the dynamic adjoint through the
+    time-paired transposed CSR): no communication inside the step, every rank owns disjoint
+    slices.  The image stack is all-gathered once after the loop.  Outside the timed region every
+    rank checks the gathered stack and the gathered gradient against a single-GPU Operator of the
+    whole orbit (the same rays; float32 sums grouped by other workgroup blocks: ~1e-7)."""
+    from sph_raytracer_amd import Operator
+    cfg = CONFIGS['c4']
+    grid, geom = build_geometry(cfg, 0, 1)          # the whole orbit, on every rank
+    g = torch.Generator().manual_seed(4)
+    x = torch.rand(tuple(grid.shape), dtype=torch.float32, generator=g).to(rk.dev)
+    m = torch.rand(tuple(geom.shape), dtype=torch.float32, generator=g).to(rk.dev)
+    n_views = int(geom.shape[0])
+    rk.barrier()
+    t0 = time.perf_counter()
+    if rk.dist is None:
+        op = Operator(grid, geom, device=rk.dev, dynamic=True)
+        lo, hi, sop = 0, n_views, None
+        fwd = op
+        dshape = tuple(x.shape)
+
+        def adj(r):
+            return op._apply_adjoint(r, dshape, r.dtype, r.device)
+    else:
+        from sph_raytracer_amd.distributed import ShardedOperator
+        sop = ShardedOperator(grid, geom, device=rk.dev, dynamic=True)
+        op, lo, hi = sop.local, sop.lo, sop.hi
+        fwd, adj = sop, sop.T_local
+    y0 = fwd(x)
+    torch.cuda.synchronize(rk.dev)
+    t_op = time.perf_counter() - t0
+    m_loc = m[lo:hi]
+
+    def step():
+        r = fwd(x)
+        r.sub_(m_loc)
+        return adj(r)
+
+    for _ in range(max(warmup, 2)):     # (the first adjoint builds the time-paired transpose)
+        grad = step()
+    dt = rk.timed(step, steps)
+    t_op, = rk.max_over_ranks([t_op])
+    out = {'workload': 'C4 strong: ONE dynamic (50,50,50,50) volume, 50-view ConeCirc (100,50) '
+                       'orbit, view i <-> time i; views/slices sharded over the ranks',
+           'scaling': 'strong', 'rays': int(math.prod(geom.shape)), 'views': n_views,
+           'views_this_rank': hi - lo, 'steps': steps, 'ms_per_step': dt / steps * 1e3,
+           'rays_per_s': math.prod(geom.shape) * steps / dt,
+           'operator_first_forward_ms': t_op * 1e3,
+           'what': 'step = forward of this rank\'s time slices + the gradient of '
+                   '0.5*||A x - m||^2 for them (residual, dynamic adjoint); float32'}
+    grad = step()
+    y_loc = fwd(x)
+    if sop is not None:
+        rk.barrier()
+        t0 = time.perf_counter()
+        stack = sop.gather(y_loc)
+        torch.cuda.synchronize(rk.dev)
+        out['final_gather_ms'] = rk.max_over_ranks([time.perf_counter() - t0])[0] * 1e3
+        out['backend'] = rk.dist.get_backend()
+        g_full = sop._all_gather_rows(grad.reshape(hi - lo, -1), ()).reshape(x.shape)
+    else:
+        stack, g_full = y_loc, grad
+    out['stack_shape'] = list(stack.shape)
+    if check:       # against one GPU over the whole orbit (outside the timed region)
+        single = Operator(grid, geom, device=rk.dev, dynamic=True)
+        ys = single(x)
+        gs = single._apply_adjoint(ys - m, tuple(x.shape), x.dtype, x.device)
+        out['stack_rel_diff_vs_1gpu'] = _rel(stack, ys)
+        out['grad_rel_diff_vs_1gpu'] = _rel(g_full, gs)
+        out['matches_1gpu'] = bool(out['stack_rel_diff_vs_1gpu'] <= 1e-5 and
+                                   out['grad_rel_diff_vs_1gpu'] <= 1e-5)
+        del single
+    out['_op'], out['_x'] = op, (x[lo:hi] if sop is not None else x)
+    del y0
+    return out
+
+
+C5_ITERATIONS = 100     # examples/static_retrieval.py:57
+
+
+def strong_c5(rk, iterations, check=True):
+    """BASELINE configs[4], strong-scaled: the static_retrieval.py loop (examples/
+    static_retrieval.py:42-57, retrieval.py:88-120) on C5 (64^3 grid, 64-view ConeCirc (100,50)
+    orbit; FullyDenseModel, SquareLoss + NegRegularizer, Adam lr 0.1, float64 coefficients), the
+    64 views sharded over the ranks: distributed.gd, i.e. per iteration the local forward, the
+    residual, the local adjoint, one all_reduce(sum) of the 64^3 gradient (RCCL), the identical
+    Adam step on every rank.  Timed: one whole gd call of `iterations` iterations (plan set-up,
+    the final forward and the stack's all-gather included), after a 3-iteration warm-up call.
+    Checked (outside the timing) against retrieval.gd on one GPU over the whole orbit with the
+    same gathered measurements: only the gradient's summation order differs."""
+    from sph_raytracer_amd import Operator, retrieval
+    from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
+    from sph_raytracer_amd.model import FullyDenseModel
+    cfg = CONFIGS['c5']
+    grid, geom = build_geometry(cfg, 0, 1)
+    truth = torch.zeros(tuple(grid.shape), dtype=torch.float64, device=rk.dev)
+    truth[:, 32:, :32] = 1                       # static_retrieval.py:22-24 at 64^3
+    truth[:, :32, 32:] = 1
+    model = FullyDenseModel(grid)
+    rk.barrier()
+    t0 = time.perf_counter()
+    if rk.dist is None:
+        op = sop = Operator(grid, geom, device=rk.dev)
+        y_loc = op(truth)
+
+        def run(k):
+            return retrieval.gd(op, y_loc.clone(), model, num_iterations=k, lr=1e-1,
+                                loss_fns=[SquareLoss(), NegRegularizer()], progress_bar=False)
+    else:
+        from sph_raytracer_amd.distributed import ShardedOperator, gd as dgd
+        sop = ShardedOperator(grid, geom, device=rk.dev)
+        op = sop.local
+        y_loc = sop(truth)
+
+        def run(k):
+            return dgd(sop, y_loc.clone(), model, num_iterations=k, lr=1e-1,
+                       loss_fns=[SquareLoss(), NegRegularizer()])
+    torch.cuda.synchronize(rk.dev)
+    t_op = time.perf_counter() - t0
+    run(3)                          # warm-up: the transposed CSR, the kernels' first launches
+    rk.barrier()
+    res = []
+    dt = rk.timed(lambda: res.append(run(iterations)), 1)
+    t1 = rk.timed(lambda: run(1), 1)
+    t_op, = rk.max_over_ranks([t_op])
+    coeffs, stack, losses = res[0]
+    fid = losses[next(iter(losses))]
+    n_rays = int(math.prod(geom.shape))
+    out = {'workload': 'C5 strong: static_retrieval.py loop, (64,64,64) grid, 64-view ConeCirc '
+                       '(100,50) orbit, FullyDenseModel, SquareLoss + NegRegularizer, Adam lr 0.1, '
+                       'f64; views sharded over the ranks, one gradient all_reduce per iteration',
+           'scaling': 'strong', 'rays': n_rays, 'views': int(geom.shape[0]),
+           'views_this_rank': int(y_loc.shape[0]), 'iterations': iterations,
+           'ms_per_iteration': dt / iterations * 1e3,
+           'ms_per_iteration_marginal': (dt - t1) / max(iterations - 1, 1) * 1e3,
+           'gd_call_ms': dt * 1e3, 'gd_1_iteration_call_ms': t1 * 1e3,
+           'rays_per_s': n_rays * iterations / dt,
+           'operator_first_forward_ms': t_op * 1e3,
+           'fidelity_first': fid[0], 'fidelity_last': fid[-1],
+           'what': 'one gd call of `iterations` iterations (forward + residual + adjoint + '
+                   'gradient all_reduce + Adam each), plan set-up and final forward/all-gather '
+                   'included; marginal = (t(K) - t(1)) / (K - 1)'}
+    if rk.dist is not None:
+        out['backend'] = rk.dist.get_backend()
+    if check and rk.dist is not None:    # (at N=1 the timed run is the single-GPU loop itself)
+        single = Operator(grid, geom, device=rk.dev)
+        fns = [SquareLoss(), NegRegularizer()]
+        c1, _, l1 = retrieval.gd(single, sop.gather(y_loc), model, num_iterations=iterations,
+                                 lr=1e-1, loss_fns=fns, progress_bar=False)
+        a, b = torch.tensor(fid), torch.tensor(l1[fns[0]])
+        out['coeffs_max_abs_diff_vs_1gpu'] = float((coeffs - c1).abs().max())
+        out['sqloss_max_rel_diff_vs_1gpu'] = float(((a - b).abs() / b.abs()).max())
+        out['matches_1gpu'] = bool(out['coeffs_max_abs_diff_vs_1gpu'] <= 1e-9 and
+                                   out['sqloss_max_rel_diff_vs_1gpu'] <= 1e-9)
+        del single
+    out['_op'], out['_x'] = op, truth
+    return out
+
+
+def _public(leg):
+    return {k: v for k, v in leg.items() if not k.startswith('_')}
+
+
+def roofline(op, x, config, k_ms, k_method):
+    """The forward kernel's roofline: ALGORITHMIC bytes per launch (s_y + 4 +
+    S*(4 + s_len + s_rho) per ray; f32 path s_len = s_rho = 4) over its mean launch duration
+    `k_ms` (HIP events, kernel_time_ms), next to the HBM traffic of the newest committed
+    rocprofv3 --pmc record of this kernel and config (profiles/rNN_forward_<config>_pmc.json)."""
+    kname = op._forward_kernel_name(x)
+    traffic, traffic_src = None, None
+    for tag in ('r06', 'r05', 'r04', 'r03', 'r02', 'r01'):
+        pmc = os.path.join(ROOT, 'profiles', f'{tag}_forward_{config}_pmc.json')
+        if not os.path.exists(pmc):
+            continue
+        rec_pmc = json.load(open(pmc))
+        if rec_pmc.get('kernel') == kname and rec_pmc.get('config') == config:
+            traffic, traffic_src = rec_pmc['traffic_bytes_per_launch'], os.path.relpath(pmc, ROOT)
+            break
+    es = x.element_size()
+    alg_bytes = op._csr['n'] * (es + 4) + op._csr['total'] * (4 + es + es)
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    return {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+            'achieved_basis': 'algorithmic bytes (SURVEY 8(d): s_y + 4 + S*(4 + s_len + '
+                              's_rho) per ray; density gathers counted as HBM)',
+            'traffic_gbs': traffic / (k_ms * 1e-3) / 1e9 if traffic else None,
+            'traffic_frac': traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
+            'traffic_source': traffic_src, 'kernel': kname,
+            'kernel_ms': k_ms, 'bytes_per_launch': alg_bytes, 'timing': k_method}
+
+
+def strong_legs(rk, steps, warmup):
+    """The strong-scaled C4 and C5 legs the default run reports beside its headline, so that
+    every `bench.py --gpus N` run (the driver's N = 1, 2, 4, 8 scaling runs included) also
+    records BASELINE configs[3] and configs[4] as they are defined.  A leg that raises is
+    reported as its error (identically on every rank: the legs issue the same collectives)."""
+    legs = {}
+    for name, fn in (('c4', lambda: strong_c4(rk, max(steps, 20), warmup)),
+                     ('c5_retrieval', lambda: strong_c5(rk, C5_ITERATIONS))):
+        try:
+            legs[name] = _public(fn())
+        except Exception as exc:      # informative legs: never lose the headline line to them
+            log(f'strong leg {name} failed: {exc!r}')
+            legs[name] = {'error': repr(exc)}
+        torch.cuda.empty_cache()
+    return legs
+
+
+def strong_main(args, rk):
+    """`--scaling strong --config c4|c5`: the JSON line's value is the strong-scaled leg's
+    rays/s (C4: forward + dynamic gradient steps; C5: gd iterations, each a forward and an
+    adjoint of all 320,000 rays), over all ranks."""
+    cfg = CONFIGS[args.config]
+    torch.cuda.reset_peak_memory_stats(rk.dev)
+    if args.config == 'c4':
+        leg = strong_c4(rk, args.steps, args.warmup)
+        ms, dtype = leg['ms_per_step'], torch.float32
+    else:
+        leg = strong_c5(rk, args.steps)
+        ms, dtype = leg['ms_per_iteration'], torch.float64
+    peak_gb = torch.cuda.max_memory_allocated(rk.dev) / 1e9
+    op, x = leg['_op'], leg['_x']
+    k_ms, k_method = kernel_time_ms(op, x, reps=50)
+    rec = {
+        'metric': METRIC,
+        'value': leg['rays_per_s'],
+        'unit': 'rays/s',
+        'n_gpus': rk.world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': ms,
+        'higher_is_better': True,
+        'scaling': 'strong',
+        'vs_baseline': None,
+        'dtype': 'f32' if dtype == torch.float32 else 'f64',
+        'data': 'synthetic (torch.rand density / the static_retrieval.py phantom, reference '
+                'geometry)',
+        'config': {'workload': leg['workload'], 'grid': list(cfg[0]), 'views': leg['views'],
+                   'detector': list(cfg[2]), 'rays': leg['rays'],
+                   'views_this_rank': leg['views_this_rank'],
+                   'parallelism': f'obs/time-sharded x{rk.world} (strong)'},
+        'peak_gb_resident': peak_gb,
+        'strong': _public(leg),
+        'roofline': roofline(op, x, args.config, k_ms, k_method),
+    }
+    rec['roofline']['scope'] = 'this rank\'s local forward kernel'
+    if rk.rank == 0 and rk.world == 1 and not args.no_cpu_baseline:
+        try:
+            rec['cpu_baseline'] = cpu_baseline(cfg, args.cpu_sample_views, args.cpu_reps)
+            rec['cpu_baseline']['scope'] = 'the forward only'
+        except Exception as exc:
+            rec['cpu_baseline'] = {'value': None, 'error': repr(exc)}
+    else:
+        rec['cpu_baseline'] = None
+    if rk.rank == 0:
+        print(json.dumps(rec), flush=True)
+
+
 def spawn_ranks(n):
     """Run this script as `n` child ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one
     GPU each), as torch.distributed.run would; rank 0 prints the JSON line.  Returns the exit
@@ -239,7 +546,17 @@ def main():
     ap.add_argument('--cpu-reps', type=int, default=10)
     ap.add_argument('--cpu-cold-views', type=int, default=None,
                     help='views of the cold CPU sample (default: 10, C3: 2)')
+    ap.add_argument('--scaling', default='weak', choices=('weak', 'strong'),
+                    help='weak (default): every rank its own views of a views*N orbit; strong '
+                         '(c4, c5): ONE workload sharded over the ranks (c4: forward + dynamic '
+                         'gradient per step; c5: the static_retrieval.py gd loop, one step = one '
+                         'iteration)')
+    ap.add_argument('--no-strong-legs', action='store_true',
+                    help='skip the strong-scaled C4 / C5 legs the default run reports beside '
+                         'the headline')
     args = ap.parse_args()
+    if args.scaling == 'strong' and args.config not in ('c4', 'c5'):
+        ap.error('--scaling strong is defined for --config c4 and c5')
 
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         # `python bench.py --gpus N` without a launcher: start the N ranks here, before this
@@ -269,18 +586,13 @@ def main():
     cfg = CONFIGS[args.config]
     shape, n_views, det, kind, dtype, desc = cfg
     torch.manual_seed(0)
-
-    def barrier():
+    rk = _Ranks(dist, dev, world, rank)
+    barrier, max_over_ranks = rk.barrier, rk.max_over_ranks
+    if args.scaling == 'strong':
+        strong_main(args, rk)
         if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-
-    def max_over_ranks(vals):
-        # host floats -> their max over ranks (RCCL: a device tensor; gloo: a host one)
-        on = dev if dist.get_backend() == 'nccl' else 'cpu'
-        tt = torch.tensor(vals, dtype=torch.float64, device=on)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        return tt.tolist()
+            dist.destroy_process_group()
+        return
 
     # ---- cold: geometry + trace + first forward ----------------------------------------------
     torch.cuda.reset_peak_memory_stats(dev)
@@ -373,10 +685,30 @@ def main():
     log('legs ' + json.dumps([['first', 1], ['warmup', args.warmup], ['steps', args.steps]] +
                              ([['final_gather_fwd', 1]] if dist is not None else []) +
                              [['cold', 3], ['pcie', 3 + reps_h], ['graph', 1 + 4 * k_reps]] +
-                             ([['adjoint', 3 + adj_steps]] if not grid.dynamic else [])))
+                             [['adjoint', 3 + adj_steps]]))
     # the adjoint (op.T, static grids; BASELINE configs[2] is a forward + adjoint run): the
     # transposed CSR is built by the first call (untimed), then `adj_steps` calls are timed
     adjoint = None
+    if grid.dynamic:
+        # the dynamic gradient (the autograd backward of raytracer.py:710, which
+        # the reference's Operator.T refuses): the time-paired transposed CSR through the same
+        # table kernel, built by the first of 3 untimed calls
+        y_adj = torch.rand(tuple(op.geom.shape), dtype=dtype, device=dev)
+        dshape = tuple(x.shape)
+
+        def adj_step():
+            return op._apply_adjoint(y_adj, dshape, dtype, dev)
+        for _ in range(3):
+            adj_step()
+        t_adj = rk.timed(adj_step, adj_steps) / adj_steps
+        n_vox = math.prod(shape)
+        adj_bytes = n_vox * (x.element_size() + 4) + total_seg * (4 + 2 * x.element_size())
+        adjoint = {'ms_per_step': t_adj * 1e3, 'rays_per_s': n_rays * world / t_adj,
+                   'alg_GBps_per_gpu': adj_bytes / t_adj / 1e9, 'steps': adj_steps,
+                   'what': 'dynamic gradient: the adjoint of the view <-> time pairing (the '
+                           'time-paired CSR transposed once, then the same table kernel); '
+                           'per-step wall time incl. launch; bytes as SURVEY 8(d) with voxels '
+                           '(T x vol) as rows'}
     if not grid.dynamic:
         y_adj = torch.rand(tuple(op.geom.shape), dtype=dtype, device=dev)
         for _ in range(3):
@@ -397,21 +729,7 @@ def main():
                    'what': 'op.T(y), y = torch.rand(geom.shape): the transposed CSR (built by the '
                            'first of 3 untimed calls) through the same table kernel; per-step '
                            'wall time incl. launch; bytes as SURVEY 8(d) with voxels as rows'}
-    kname = op._forward_kernel_name(x)
-    traffic, traffic_src = None, None
-    # HBM bytes per launch from the newest committed rocprofv3 --pmc passes of this kernel
-    for tag in ('r06', 'r05', 'r04', 'r03', 'r02', 'r01'):
-        pmc = os.path.join(ROOT, 'profiles', f'{tag}_forward_{args.config}_pmc.json')
-        if not os.path.exists(pmc):
-            continue
-        rec_pmc = json.load(open(pmc))
-        if rec_pmc.get('kernel') == kname and rec_pmc.get('config') == args.config:
-            traffic, traffic_src = rec_pmc['traffic_bytes_per_launch'], os.path.relpath(pmc, ROOT)
-            break
-    # bytes/ray = s_y + 4 + S*(4 + s_len + s_rho); f32 path s_len = s_rho = 4
-    es = x.element_size()
-    alg_bytes = n_rays * (es + 4) + total_seg * (4 + es + es)
-    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    roof = roofline(op, x, args.config, k_ms, k_method)
 
     rec = {
         'metric': METRIC,
@@ -440,15 +758,10 @@ def main():
                  'what': 'geometry + Operator trace + first forward (median of 3, warm process; '
                          'operator_*: Operator init + first forward only, the reference\'s cold '
                          'definition; first_in_process includes HIP/torch initialisation)'},
-        'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
-                     'achieved_basis': 'algorithmic bytes (SURVEY 8(d): s_y + 4 + S*(4 + s_len + '
-                                       's_rho) per ray; density gathers counted as HBM)',
-                     'traffic_gbs': traffic / (k_ms * 1e-3) / 1e9 if traffic else None,
-                     'traffic_frac': traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
-                     'traffic_source': traffic_src, 'kernel': kname,
-                     'kernel_ms': k_ms, 'bytes_per_launch': alg_bytes, 'timing': k_method},
+        'roofline': roof,
     }
+    if not args.no_strong_legs and args.config == 'c2':
+        rec['strong'] = strong_legs(rk, args.steps, args.warmup)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             rec['cpu_baseline'] = cpu_baseline(cfg, args.cpu_sample_views, args.cpu_reps)

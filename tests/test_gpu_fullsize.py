@@ -1,4 +1,5 @@
-"""Parity at the full BASELINE sizes of C3 and C4, every ray against the C oracle.
+"""Parity at the full BASELINE sizes of C2, C3, C4 and C5, every ray against the C
+oracle.
 
 C3: (128,128,128) grid, 128-view orbit x ConeRect (128,256) = 4.19 M rays, ~115 M segments —
 the production path of the HBM roofline run: the multi-wave forward with (4,2,4) brick staging,
@@ -188,3 +189,80 @@ def test_c4_full_forward_and_gradient_vs_oracle(c4, gpu):
     rec = op._paired(50, per_view)
     assert rec is not None and rec['desc'].n_cols == 50 * n_vox and rec['desc'].tab_bytes == 4
     assert rec['desc'].order & 2          # one contiguous block range per XCD
+
+
+def _static_forward_adjoint(grid, geom, op, ref, n_vox, gpu, seed, what):
+    """Static forward (float64, float32) and adjoint op.T (float64, float32) of every ray /
+    voxel against the oracle's segments; each call is made three times (the general path, then
+    the steady-state bindings: the C++ fast path and T's transposed-CSR binding)."""
+    ptr, vox, seg = _flat(ref)
+    ray = np.repeat(np.arange(len(ptr) - 1), np.diff(ptr))
+    g = tr.Generator().manual_seed(seed)
+    x = tr.rand(grid.shape, dtype=tr.float64, generator=g)
+    y = tr.rand(tuple(geom.shape), dtype=tr.float64, generator=g)
+    want = np.bincount(ray, x.numpy().reshape(-1)[vox] * seg, minlength=len(ptr) - 1)
+    for dt, tol in ((tr.float64, gc.F64_RTOL), (tr.float32, gc.F32_RTOL)):
+        xd = x.to(gpu, dt)
+        for _ in range(3):
+            got = op(xd).cpu().numpy().reshape(-1)
+            err = gc.rel_close(got, want, tol)
+            assert err <= tol, f'{what} forward {dt} rel err {err:.3g}'
+    want_t = np.bincount(vox, y.numpy().reshape(-1)[ray] * seg, minlength=n_vox)
+    scale = np.abs(want_t).max()
+    for dt, tol in ((tr.float64, 1e-10), (tr.float32, 1e-5)):
+        yd = y.to(gpu, dt)
+        for _ in range(3):
+            got = op.T(yd).cpu().numpy().reshape(-1)
+            err = float(np.abs(got - want_t).max() / scale)
+            assert err <= tol, f'{what} adjoint {dt} rel err {err:.3g}'
+
+
+@pytest.fixture(scope='module')
+def c2(gpu):
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(50, (50, 100), 'rect', (50, 50, 50))
+    op = Operator(grid, geom, device=gpu)
+    ref, n_vox = _oracle_trace(grid, geom)
+    return grid, geom, op, ref, n_vox
+
+
+def test_c2_full_trace_vs_oracle(c2):
+    """All 250 k rays of the headline config (BASELINE configs[1]): voxel sequences exact,
+    lengths 1e-12 — the one-wave path (bitmap granule tables, no brick staging)."""
+    grid, geom, op, ref, _ = c2
+    assert op._csr['n'] == 50 * 50 * 100 and op._csr['ray_id'] is None
+    _compare_all(ref, _gpu_views(op, 50), 5.1, 'C2')
+
+
+def test_c2_full_forward_and_adjoint_vs_oracle(c2, gpu):
+    """C2 forward and adjoint over every ray / voxel, general and steady-state paths."""
+    grid, geom, op, ref, n_vox = c2
+    assert op._csr['desc'].stage_brick[0] == 0      # one resident wave: natural layout
+    _static_forward_adjoint(grid, geom, op, ref, n_vox, gpu, 21, 'C2')
+
+
+@pytest.fixture(scope='module')
+def c5(gpu):
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(64, (100, 50), 'circ', (64, 64, 64))
+    op = Operator(grid, geom, device=gpu)
+    ref, n_vox = _oracle_trace(grid, geom)
+    return grid, geom, op, ref, n_vox
+
+
+def test_c5_full_trace_vs_oracle(c5):
+    """All 320 k rays of the retrieval config (BASELINE configs[4]): the ConeCirc wedge trace
+    order (rays generated in trace order on the device), ~2 k exact-path tie rays per trace
+    (ring 0 passes through the origin), reordered to geometry order."""
+    grid, geom, op, ref, _ = c5
+    assert op._csr['n'] == 64 * 100 * 50 and op._csr['ray_id'] is not None
+    _compare_all(ref, _gpu_views(op, 64), 5.1, 'C5')
+
+
+def test_c5_full_forward_and_adjoint_vs_oracle(c5, gpu):
+    """C5 forward (float64 half tables, brick staging, alternating block order) and adjoint (the
+    transposed CSR of a trace-ordered CSR) over every ray / voxel."""
+    grid, geom, op, ref, n_vox = c5
+    desc = op._csr['desc']
+    assert tuple(desc.stage_brick) == (4, 2, 4) and desc.n_blocks > 256 * 6
+    _static_forward_adjoint(grid, geom, op, ref, n_vox, gpu, 51, 'C5')
