@@ -1771,6 +1771,8 @@ extern "C" int sphrt_csr_index_staged(const int64_t* row_ptr, int64_t n_rays, in
                                       const int32_t* ray_ids, int32_t* nz_row, void* workspace,
                                       void* stream) {
     if (!nz_row && n_rays > 0) return fail("null nz_row");
+    // (nz_row and the staged gather index rows as int32)
+    if (n_rays > 0x7fffffff) return fail("the staged index needs n_rays < 2^31");
     return csr_index(row_ptr, n_rays, nullptr, row_ray, empty_ray, blocks, n_blocks, ray_ids,
                      nz_row, workspace, stream);
 }
@@ -1951,6 +1953,7 @@ extern "C" int sphrt_csr_local_build_staged(const sphrt_csr* c, int64_t* blocks,
         !stats || !slot || !nz_row || !svox || !slen)
         return fail("incomplete staged CSR for the granule tables");
     if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
+    if (c->n_rays > 0x7fffffff) return fail("the staged table build needs n_rays < 2^31");
     StageMap sm;
     if (!stage_map(c, sm)) return fail("inconsistent brick staging fields");
     const int64_t cols = table_cols(c);

@@ -495,7 +495,7 @@ def _seg_alloc(total):
     return max((total + 15) // 16 * 16, 16)
 
 
-def _tables_one_pass(desc, nblocks, dev):
+def _tables_one_pass(desc, nblocks, dev, free=None):
     """Whether _local_tables builds in one pass (wide tables fit comfortably in free memory and
     SPHRT_TABLES is not 'twopass'); decides desc.tab_bytes (16-bit entries when every granule
     index fits: <= 2^18 columns, half the table bytes the forward streams)."""
@@ -503,7 +503,18 @@ def _tables_one_pass(desc, nblocks, dev):
     desc.tab_bytes = 2 if (cols + 3) // 4 <= 65536 else 4
     wide_bytes = nblocks * _lib.TAB_WIDE * desc.tab_bytes
     return (os.environ.get('SPHRT_TABLES', 'onepass') != 'twopass' and
-            wide_bytes <= 0.3 * tr.cuda.mem_get_info(dev)[0])
+            wide_bytes <= 0.3 * (tr.cuda.mem_get_info(dev)[0] if free is None else free))
+
+
+def _staged_fits(desc, nblocks, total, free):
+    """Whether the staged table build fits: it keeps the one-pass trace's staging (12 B per bound
+    slot, allocated already) alive while it writes the final CSR (vox 4 + len 8 + len32 4 + loc 2
+    = 18 B per segment) and the wide tables, so its peak is staging + CSR + tables, against the
+    compaction path's staging + 12 B per segment (the staging is freed before the tables).  Taken
+    only when the CSR and the wide tables fit in half the free memory; otherwise the staging is
+    compacted first (C3 peak 3.04 -> 4.60 GB with the staged build)."""
+    need = 18 * _seg_alloc(total) + nblocks * _lib.TAB_WIDE * desc.tab_bytes
+    return need <= 0.5 * free
 
 
 def _local_tables(lib, desc, blocks, nblocks, total, dev, stream, staged=None):
@@ -941,8 +952,11 @@ class Operator:
         c.n_cols = math.prod(self.grid.shape[-3:])
         shape3 = tuple(int(v) for v in self.grid.shape[-3:])
         _set_stage(c, shape3, _stage_brick(nblocks))
-        staged = (staging is not None and os.environ.get('SPHRT_TABLE_STAGED', '1') != '0' and
-                  _tables_one_pass(c, nblocks, dev))
+        staged = staging is not None and os.environ.get('SPHRT_TABLE_STAGED', '1') != '0'
+        if staged:
+            free = tr.cuda.mem_get_info(dev)[0]
+            staged = (_tables_one_pass(c, nblocks, dev, free) and
+                      _staged_fits(c, nblocks, total, free))
         if staging is not None and not staged:
             vox, seg_len = _compact_staging(lib, n, row_ptr, total, staging, dev, stream)
             staging = None

@@ -3,7 +3,10 @@
 `operator_seconds`) on a bench config, median of --reps warm repetitions; for A/B runs of
 environment switches (e.g. SPHRT_TABLE_SORT=radix) and under rocprofv3 for the kernel split.
 
-    python tools/operator_time.py --config c3 [--reps 7]
+    python tools/operator_time.py --config c3 [--reps 7] [--ftype float32] [--invalid]
+
+--ftype float32 / --invalid time the reference-mode trace (sphrt_trace_reference: every ray
+through the exact path, count then fill; raytracer.py:48-173 with those options).
 """
 import argparse
 import json
@@ -23,6 +26,8 @@ def main():
     ap.add_argument('--reps', type=int, default=7)
     ap.add_argument('--adjoint', action='store_true',
                     help='also the first op.T(y) of each Operator (builds the transposed CSR)')
+    ap.add_argument('--ftype', default='float64', choices=('float64', 'float32'))
+    ap.add_argument('--invalid', action='store_true')
     args = ap.parse_args()
     import bench
     from sph_raytracer_amd import Operator
@@ -30,7 +35,8 @@ def main():
     cfg = bench.CONFIGS[args.config]
     grid, geom = bench.build_geometry(cfg, 0, 1)
     x = torch.rand(cfg[0], dtype=cfg[4], device=dev)
-    op = Operator(grid, geom, device=dev)        # warm-up: HIP and allocator initialisation
+    kw = dict(ftype=getattr(torch, args.ftype), invalid=args.invalid)
+    op = Operator(grid, geom, device=dev, **kw)   # warm-up: HIP and allocator initialisation
     y = op(x)
     if args.adjoint:
         op.T(y)
@@ -39,17 +45,22 @@ def main():
     for _ in range(args.reps):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        op = Operator(grid, geom, device=dev)
+        op = Operator(grid, geom, device=dev, **kw)
         y = op(x)
         if args.adjoint:
             op.T(y)
         torch.cuda.synchronize(dev)
         times.append(time.perf_counter() - t0)
+        op_n = op._csr['n']
         del op
     times.sort()
     env = {k: v for k, v in os.environ.items() if k.startswith('SPHRT_')}
-    print(json.dumps({'config': args.config, 'adjoint': args.adjoint, 'operator_ms_median': 1e3 * times[len(times) // 2],
-                      'operator_ms_min': 1e3 * times[0], 'reps': args.reps, 'env': env}))
+    med = times[len(times) // 2]
+    n = int(op_n)
+    print(json.dumps({'config': args.config, 'adjoint': args.adjoint, 'ftype': args.ftype,
+                      'invalid': args.invalid, 'operator_ms_median': 1e3 * med,
+                      'operator_ms_min': 1e3 * times[0], 'rays': n,
+                      'rays_per_s_median': n / med, 'reps': args.reps, 'env': env}))
 
 
 if __name__ == '__main__':
