@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Exact-path counters of a count pass over a bench configuration: deferred rays and depth-limit
-ranges rank-sorted in parallel / heap-sorted by one lane (trace.hip exact_heap_range).
+ranges rank-sorted in parallel / heap-sorted by one lane (trace.hip exact_heap_range); hit rays.
 
     python tools/exact_stats.py [c2 c3 c4 c5]
 """
@@ -29,7 +29,8 @@ def main(cfgs):
                                          tws.numel(), _lib.stream_of(dev)), 'sphrt_trace_count')
         head = tws[:256].cpu().view(tr.int64)
         print(json.dumps({'config': name, 'rays': batch.n, 'deferred': int(head[0]),
-                          'heap_rank_sorted': int(head[16]), 'heap_serial': int(head[17])}))
+                          'heap_rank_sorted': int(head[16]), 'heap_serial': int(head[17]),
+                          'hit_rays': int(tws[64:68].cpu().view(tr.int32)[0])}))
 
 
 if __name__ == '__main__':
