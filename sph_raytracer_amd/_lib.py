@@ -182,7 +182,7 @@ def load_fast():
     global _fast
     if _fast is None:
         _fast = False
-        if os.path.exists(FAST_PATH) and os.environ.get('SPHRT_NO_FASTPATH') != '1':
+        if os.path.exists(FAST_PATH):
             import importlib.util
             spec = importlib.util.spec_from_file_location('_sphrt_fast', FAST_PATH)
             mod = importlib.util.module_from_spec(spec)

@@ -25,36 +25,19 @@ namespace sphrt {
 
 constexpr uint32_t kHead = 0x80000000u;
 constexpr int kThreads = 256;
-#ifndef SPHRT_FWD_MINB64
-#define SPHRT_FWD_MINB64 5   // resident float64 forward workgroups per CU the registers aim for
-#endif
-#ifndef SPHRT_FWD_MINB32
-#define SPHRT_FWD_MINB32 6   // the same for float32
-#endif
-// Segments per forward thread (8: 256-thread workgroups, 16: 128-thread ones — half the waves,
-// so half the per-wave scan / close / address instructions for the same segments), per density
-// dtype, and the waves per SIMD the 16-segment kernels' registers aim for.  Measured with 16 for
+constexpr int kFwdMinB64 = 5;   // resident float64 forward workgroups per CU the registers aim for
+constexpr int kFwdMinB32 = 6;   // the same for float32
+// Segments per forward thread: 8 (256-thread workgroups).  16 (128-thread ones: half the waves,
+// so half the per-wave scan / close / address instructions for the same segments) measured for
 // float32: C2 6.7 -> 7.7 us, C5 34.4 -> 37.6 us, C3 236 -> 241 us (the longer serial chain per
 // thread costs more than the saved issue slots), so 8 everywhere.
-#ifndef SPHRT_FWD_P32
-#define SPHRT_FWD_P32 8
-#endif
-#ifndef SPHRT_FWD_P64
-#define SPHRT_FWD_P64 8
-#endif
-#ifndef SPHRT_FWD_MINW16
-#define SPHRT_FWD_MINW16 5
-#endif
 // 64-bit min/max as plain selects (HIP's min<int64_t>/max<int64_t> went through double
 // conversions on VALU even for uniform operands).
 __host__ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
 __host__ __device__ __forceinline__ int64_t imax64(int64_t a, int64_t b) { return a > b ? a : b; }
 constexpr int kPer = 8;                         // segments per thread per pass
 constexpr int kPass = kThreads * kPer;          // 2048 segments per pass
-#ifndef SPHRT_SEG_PER_BLOCK
-#define SPHRT_SEG_PER_BLOCK 1792
-#endif
-constexpr int64_t kSegPerBlock = SPHRT_SEG_PER_BLOCK;   // row starts per workgroup (leaves room
+constexpr int64_t kSegPerBlock = 1792;          // row starts per workgroup (leaves room
                                                 // for the last row's overhang inside one pass)
 constexpr int kBlockFields = 6;                 // empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab
 constexpr int kLocalMax = 4096;                 // segments per workgroup with a granule table
@@ -69,18 +52,6 @@ enum { kTabCount = 0, kTabFill = 1, kTabBuild = 2 };
 constexpr int kTabWide = SPHRT_TAB_WIDE;
 static_assert(kTabWide >= kMaxGran, "wide tables hold every table");
 
-// Diagnostic build only (-DSPHRT_FWD_STAMPS, tools/fwd_timeline.py): s_memrealtime (100 MHz)
-// stamps of wave 0 of every forward workgroup at its phase boundaries.
-#ifdef SPHRT_FWD_STAMPS
-__device__ unsigned long long g_fwd_stamps[1 << 20];
-#define FWD_STAMP(i)                                                                          \
-    do {                                                                                      \
-        if (threadIdx.x == 0 && blockIdx.x < (1u << 17))                                      \
-            g_fwd_stamps[8 * blockIdx.x + (i)] = __builtin_amdgcn_s_memrealtime();            \
-    } while (0)
-#else
-#define FWD_STAMP(i) do {} while (0)
-#endif
 
 // ---- index --------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void mark_rows_kernel(const int64_t* row_ptr, int64_t n,
@@ -340,10 +311,7 @@ __device__ __forceinline__ void seg_step(int& h, float& s) {
 // float32 forwards stitch a row's runs across threads in float too (the segmented scan's DPP
 // steps and wave totals at half the width): C2 forward 6.68 -> 6.37 us, C5 28.3 -> 27.5 us, C3
 // unchanged; largest relative difference from float64 accumulation 1.8e-7 -> 2.5e-7 (C2-C5,
-// forward and adjoint).  SPHRT_FWD_STITCH32=0 at build time stitches in double (A/B studies).
-#ifndef SPHRT_FWD_STITCH32
-#define SPHRT_FWD_STITCH32 1
-#endif
+// forward and adjoint).
 template <int W = 4, typename S = double>
 __device__ __forceinline__ S block_excl_segsum1(bool has, S tail, bool& tot_has,
                                                      S& tot_sum, int (&hs)[4],
@@ -700,13 +668,11 @@ __global__ __launch_bounds__(kThreads) void local_table_bitmap_kernel(
 // O(volume): at C3 (2 M voxels, 64 k workgroups) 10.6 ms of bitmap work.  Identical output.
 // 10 bits per pass (rocprim's match ranking): C3's 19-bit granule keys in 2 passes instead of
 // the default 8-bit 3 (local_table_radix_kernel 1324 -> 1240 us; 6 bits: 1404 us).
-#ifndef SPHRT_RADIX_BITS
-#define SPHRT_RADIX_BITS 10
-#endif
+constexpr int kRadixBits = 10;
 // RB: bits per pass.  10 for the grids whose blocks all take the sort; 8 (a third pass, but 8 KB
 // of sort storage instead of 33 KB) behind the bucket tables, which leave the sort only the rare
 // block of many buckets: the kernel's LDS then fits 7 workgroups per CU instead of 4.
-template <int ITEMS, int TM, int RB = SPHRT_RADIX_BITS>
+template <int ITEMS, int TM, int RB = kRadixBits>
 struct RadixTable {
     // the count pass sorts keys only (its values are dead)
     using Sort = typename std::conditional<
@@ -724,12 +690,8 @@ struct RadixTable {
 // bucket's base + the set bits below it.  Ascending distinct granules, the same tables and loc as
 // the sort.  A C3 block (1792 segments, ~640 granules) touches ~52 buckets (max ~90 in a traced
 // view): blocks with more than kBucketSlots of them, or keys of more than 21 bits, return false
-// and take the sort.  SPHRT_TABLE_BUCKETS=0 builds the sort only; at run time the environment
-// variable of that name set to 0 sorts every block (tests: bucket tables == sorted tables), the
-// launch marking key_bits with kSortOnly.
-#ifndef SPHRT_TABLE_BUCKETS
-#define SPHRT_TABLE_BUCKETS 1
-#endif
+// and take the sort.  At run time SPHRT_TABLE_BUCKETS=0 sorts every block (tests: bucket tables
+// == sorted tables), the launch marking key_bits with kSortOnly.
 constexpr int kBucketLo = 9;                       // granules per bucket: 512 = 16 words
 constexpr int kBucketWords = 1 << (kBucketLo - 5);
 constexpr int kBucketL1 = 128;                     // level-1 words: buckets < 4096
@@ -742,7 +704,7 @@ __device__ __forceinline__ bool bucket_table(int64_t* m, const int32_t* __restri
                                              int64_t s0, int n, int key_bits, const StageMap& sm,
                                              unsigned char* lds, ScanShared& sh,
                                              unsigned long long* stats, const uint32_t* xin) {
-    if (!SPHRT_TABLE_BUCKETS || key_bits > kBucketLo + 12) return false;
+    if (key_bits > kBucketLo + 12) return false;
     const int tid = threadIdx.x;
     uint32_t* l1 = reinterpret_cast<uint32_t*>(lds);
     int* pre1 = reinterpret_cast<int*>(l1 + kBucketL1);          // kBucketL1 + 1 (total last)
@@ -856,7 +818,7 @@ __device__ __forceinline__ bool bucket_table(int64_t* m, const int32_t* __restri
 // xin: the block's voxels already in registers (xin[i]: segment i * kThreads + t, the staged
 // gather's striped order — the sort takes any arrangement, each value carries its position),
 // else loaded from vox (segment ITEMS * t + i).
-template <int ITEMS, int TM, typename TabT, int RB = SPHRT_RADIX_BITS>
+template <int ITEMS, int TM, typename TabT, int RB = kRadixBits>
 __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restrict__ vox,
                                             uint16_t* __restrict__ loc, TabT* __restrict__ tab_b,
                                             int64_t s0, int n, int key_bits, const StageMap& sm,
@@ -934,16 +896,14 @@ __device__ __forceinline__ void radix_table(int64_t* m, const int32_t* __restric
 // to local_table_big_kernel: apart, this kernel is sized for the 8-key sort's registers (72
 // VGPRs, 7 waves per SIMD instead of 4 with the 16-key sort inline: C3 1244 -> 1120 us).  With
 // the bucket tables (round 4) 8 waves per SIMD: C3 1341 -> 1285 us.
-#ifndef SPHRT_TAB_WAVES
-#define SPHRT_TAB_WAVES 8   // minimum waves per SIMD the 8-key table kernel's registers aim for
-#endif
-template <int TM, typename TabT, int ITEMS, int RB = SPHRT_RADIX_BITS>
+constexpr int kTabWaves = 8;   // minimum waves per SIMD the 8-key table kernel's registers aim for
+template <int TM, typename TabT, int ITEMS, int RB = kRadixBits>
 constexpr size_t table_lds() {
     const size_t sort = sizeof(typename RadixTable<ITEMS, TM, RB>::Storage);
     return sort > kBucketLds ? sort : kBucketLds;
 }
-template <int TM, typename TabT = int32_t, int RB = SPHRT_RADIX_BITS>
-__global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_kernel(
+template <int TM, typename TabT = int32_t, int RB = kRadixBits>
+__global__ __launch_bounds__(kThreads, kTabWaves) void local_table_radix_kernel(
     int64_t* __restrict__ blocks, const int32_t* __restrict__ vox, uint16_t* __restrict__ loc,
     TabT* __restrict__ tab, int64_t tab_stride, int key_bits, StageMap sm,
     unsigned long long* stats, const double* __restrict__ len, float* __restrict__ len32,
@@ -980,7 +940,7 @@ __global__ __launch_bounds__(kThreads, SPHRT_TAB_WAVES) void local_table_radix_k
 // grid of n_blocks / kBigScan workgroups (C3: ~6 % of the blocks are big; 256 blocks per
 // workgroup left ~25 sorts in series per workgroup, 110 us).
 constexpr int kBigScan = 32;
-template <int TM, typename TabT = int32_t, int RB = SPHRT_RADIX_BITS>
+template <int TM, typename TabT = int32_t, int RB = kRadixBits>
 __global__ __launch_bounds__(kThreads) void local_table_big_kernel(
     int64_t* __restrict__ blocks, int64_t n_blocks, const int32_t* __restrict__ vox,
     uint16_t* __restrict__ loc, TabT* __restrict__ tab, int64_t tab_stride, int key_bits,
@@ -1143,19 +1103,8 @@ __device__ __forceinline__ void stage_granules_early(const T* __restrict__ rho,
     }
 }
 
-// Segment-stream loads (read once per launch).  SPHRT_FWD_NT=1: non-temporal (A/B study).
-#ifndef SPHRT_FWD_NT
-#define SPHRT_FWD_NT 0
-#endif
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 stream_load(const uint4* p) {
-    if constexpr (SPHRT_FWD_NT) {
-        const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
-        return make_uint4(v.x, v.y, v.z, v.w);
-    } else {
-        return *p;
-    }
-}
+// Segment-stream loads (read once per launch; non-temporal loads measured C3 f64 375 -> 506 us).
+__device__ __forceinline__ uint4 stream_load(const uint4* p) { return *p; }
 
 // Segment lengths of one chunk of P segments as aligned 16-byte vectors.
 template <typename L, int P>
@@ -1306,7 +1255,7 @@ enum FwdMode { kFwdTable = 0, kFwdGather = 1, kFwdDynamic = 2 };
 // launch (~1500 workgroups) be resident at once; float64 stops at 5 (no spills).
 template <typename T, int P>
 constexpr int fwd_min_blocks() {
-    return P == kPer ? (sizeof(T) == 8 ? SPHRT_FWD_MINB64 : SPHRT_FWD_MINB32) : SPHRT_FWD_MINW16;
+    return P == kPer ? (sizeof(T) == 8 ? kFwdMinB64 : kFwdMinB32) : 5;
 }
 
 template <typename T>
@@ -1348,7 +1297,6 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     // arrives: the first pass (rows of block b start in [b*kSegPerBlock, (b+1)*kSegPerBlock),
     // so its first pass is [b*kSegPerBlock, +kPass)) and the granule table (fixed stride).
     const int64_t blk = block_of(xcd_chunk);
-    FWD_STAMP(0);
     const int64_t base0 = blk * kSegPerBlock;
     const int64_t last_chunk = imax64((n_seg + P - 1) / P, 1) - 1;   // clamp for loads
     RawChunk<L, local, P> raw;
@@ -1454,7 +1402,6 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
         stage_granules_late<T, TabT, THR>(density, tab_b, kEarlyRounds<T, THR>, (int)n_tab, g_full,
                                           dens);
     int64_t rbase = 0;                            // rows started in earlier passes
-    FWD_STAMP(1);
 #pragma clang loop unroll(disable)   // (also no peeling: one copy of the pass body)
     for (int64_t c = 0; c < nc; ++c) {
         const T* rho = density + c * cs;
@@ -1463,9 +1410,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             stage_granules_late<T, TabT, THR>(rho, tab_b, 0, (int)n_tab, g_full, dens);
             stage_partial_tail<T, TabT, THR>(rho, tab_b, (int)n_tab, n_cols, dens);
         }
-        FWD_STAMP(2);
-        using Stitch = typename std::conditional<SPHRT_FWD_STITCH32 && sizeof(T) == 4, float,
-                                                  double>::type;
+        using Stitch = typename std::conditional<sizeof(T) == 4, float, double>::type;
         Stitch carry = 0;                   // open run entering the pass
         rbase = 0;
 #pragma clang loop unroll(disable)
@@ -1497,7 +1442,6 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             }
             // (table mode: the full barrier also retires the granule LDS-DMA)
             const int hb = block_excl_count1<local, W>(hcount, pass_heads, sh.cnt[par]);
-            FWD_STAMP(3);
             pass_heads = __builtin_amdgcn_readfirstlane(pass_heads);
             // rows this thread closes: the run open at its start (row hb-1) and its first own row
             // (row hb) are fetched now, under the segmented scan; further ones (rare) at the store
@@ -1582,7 +1526,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             }
             // Products and thread-local runs in A (float for a float density: the reference's own
             // precision, 4-cycle VALU ops instead of 8-cycle f64 ones); runs that cross threads are
-            // stitched in Stitch (A as well, SPHRT_FWD_STITCH32).
+            // stitched in Stitch (A as well).
             A p[P];
 #pragma unroll
             for (int k = 0; k < P; ++k) p[k] = (A)rv[k] * (A)l[k];
@@ -1612,7 +1556,6 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             const Stitch ex = block_excl_segsum1<W, Stitch>(hmask != 0, (Stitch)tail, tot_has, tot_sum,
                                                  sh.has[par], sh.sum[par]);
             par ^= 1;
-            FWD_STAMP(4);
             // the run open at this thread's start: the segmented prefix of the earlier threads,
             // plus the carry of earlier passes when no earlier thread of this pass saw a head
             const Stitch run0 = hb > 0 ? ex : carry + ex;
@@ -1643,7 +1586,6 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
         }
     }
     zero_empty();
-    FWD_STAMP(5);
 }
 
 // ---- adjoint (float64 atomics into a float64 accumulator) -------------------------------------
@@ -1793,12 +1735,6 @@ extern "C" int sphrt_csr_runs(const sphrt_csr* c, int32_t* runs, int64_t* stats,
     return check_launch("block_runs");
 }
 
-#ifdef SPHRT_FWD_STAMPS
-extern "C" int sphrt_diag_fwd_stamps(unsigned long long* host, int64_t n) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_stamps), n * sizeof(unsigned long long), 0,
-                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
-}
-#endif
 
 // The float32 lengths a count / build launch writes: len32 when the caller set it with len
 // (sphrt.h: the table launch then fills the float32 copy), else none.
@@ -1832,7 +1768,7 @@ static int launch_tables(unsigned nb, hipStream_t st, int64_t* blocks, const int
     if (env && env[0] == '0') kb |= kSortOnly;
     // bucket tables, 8-bit sort behind (keys of 21 bits keep the 10-bit one: the transposed
     // tables' rays from every view span more buckets than a block has slots, and sort)
-    if (SPHRT_TABLE_BUCKETS && kb <= kBucketLo + 11) {
+    if (kb <= kBucketLo + 11) {
         hipLaunchKernelGGL((local_table_radix_kernel<TM, TabT, 8>), dim3(nb), dim3(kThreads), 0, st,
                            blocks, vox, loc, tab, stride, kb, sm, stats, len, len32, S, (int64_t)nb);
         hipLaunchKernelGGL((local_table_big_kernel<TM, TabT, 8>), dim3((nb + kBigScan - 1) / kBigScan),
@@ -2018,28 +1954,20 @@ static int check_csr(const sphrt_csr* c, int64_t n_chan, int64_t div) {
 
 // The granule tables apply to static channels whose granules are 16-byte (float) / 32-byte
 // (double) aligned; anything else takes the per-segment gather through vox.
-#ifndef SPHRT_TABLE_LDS_MAX
-#define SPHRT_TABLE_LDS_MAX (64 * 1024)   // C5 f64 (49 KB): table 64.0 us vs per-segment gather 73.3 us
-#endif
-constexpr size_t kTableLdsMax = SPHRT_TABLE_LDS_MAX;   // dynamic LDS for the staged granules, per workgroup
+// dynamic LDS for the staged granules, per workgroup (C5 f64, 49 KB: table 64.0 us vs per-segment
+// gather 73.3 us)
+constexpr size_t kTableLdsMax = 64 * 1024;
 
 // Early granule DMA (forward_kernel EDMA) needs whole granules only: no partial last granule.
-// SPHRT_FWD_EDMA=0 at build time keeps the chunk-first order everywhere (A/B studies).
-#ifndef SPHRT_FWD_EDMA
-#define SPHRT_FWD_EDMA 1
-#endif
-// SPHRT_FWD_HALF=0 (build time, or the environment at launch) keeps whole float64 tables (A/B
-// studies, tests).
-#ifndef SPHRT_FWD_HALF
-#define SPHRT_FWD_HALF 1
-#endif
+// SPHRT_FWD_HALF=0 in the environment at launch keeps whole float64 tables (tests: half tables
+// give the whole tables' sums bit for bit).
 static bool half_tables_on() {
     const char* e = getenv("SPHRT_FWD_HALF");
-    return SPHRT_FWD_HALF != 0 && !(e && e[0] == '0');
+    return !(e && e[0] == '0');
 }
 
 static bool early_dma(const sphrt_csr* c) {
-    return SPHRT_FWD_EDMA && table_cols(c) % 4 == 0 &&
+    return table_cols(c) % 4 == 0 &&
            (size_t)(kGranEarly * kThreads + 1) * 4 * 8 <= kTableLdsMax;
 }
 
@@ -2066,13 +1994,8 @@ static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int
 // columns) takes one contiguous range per XCD, so that an XCD's rays stay on few slices (C4: f32
 // 20.3 -> 18.9 us, f64 28.4 -> 26.5 us against runs of 64).
 static int fwd_chunk(const sphrt_csr* c, size_t elem) {
-    static const int forced = [] {     // SPHRT_XCD_CHUNK=k: runs of k blocks (A/B studies)
-        const char* e = getenv("SPHRT_XCD_CHUNK");
-        return e ? atoi(e) : -1;
-    }();
     const int64_t bytes = c->n_cols * (int64_t)elem;
-    int k = forced >= 0 ? forced
-            : (c->order & 2) ? INT32_MAX
+    int k = (c->order & 2) ? INT32_MAX
             : bytes > (int64_t)(4 << 20) ? 64
             : c->n_blocks <= 256 * 6 ? INT32_MAX
             : bytes > (int64_t)(1 << 20) ? 64 : 0;
@@ -2082,21 +2005,21 @@ static int fwd_chunk(const sphrt_csr* c, size_t elem) {
 template <typename T, typename L>
 static int launch_forward(const sphrt_csr* c, const L* len, const T* density, int64_t n_chan,
                           int64_t chan_stride, int64_t div, T* out, int64_t ocs, void* stream) {
-    constexpr int P = sizeof(T) == 4 ? SPHRT_FWD_P32 : SPHRT_FWD_P64;   // segments per thread
+    constexpr int P = kPer;                         // segments per thread
     const dim3 grid((unsigned)c->n_blocks), block(kPass / P);
     StreamGuard guard(stream);
     hipStream_t st = (hipStream_t)stream;
     const int chunk = fwd_chunk(c, sizeof(T));
     StageMap sm;
     if (!stage_map(c, sm)) return fail("inconsistent brick staging fields");
-#define SPHRT_FWD_ARGS(TabT, D, CS, COLS) c->blocks, c->vox, c->loc, (const TabT*)c->tab, len,    \
+#define FWD_ARGS(TabT, D, CS, COLS) c->blocks, c->vox, c->loc, (const TabT*)c->tab, len,    \
                        c->row_ray, c->empty_ray, D, n_chan, CS, div, out, ocs, c->n_rays,          \
                        c->n_segments, COLS, c->tab_stride, chunk
     const T* td = sm.on ? (const T*)c->stage : density;      // what the table kernel gathers
     const int64_t tcs = sm.on ? c->stage_cols : chan_stride;
     if (div > 0) {
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic, int32_t, false, P>), grid, block, 0, st,
-                           SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, nullptr);
+                           FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, nullptr);
     } else if (use_tables(c, td, n_chan, tcs, div)) {
         if (sm.on && (!c->stage || (int64_t)sizeof(T) * n_chan * c->stage_cols > c->stage_bytes))
             return fail("brick stage buffer missing or too small for this call");
@@ -2119,46 +2042,43 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
         size_t lds = (size_t)((half ? kHalfTab
                                : edma ? imax64(c->tab_stride, kGranEarly * kThreads)
                                       : c->tab_stride) + 1) * 4 * sizeof(T);   // + zero granule
-#ifdef SPHRT_FWD_LDS_MIN
-        lds = lds < (size_t)SPHRT_FWD_LDS_MIN ? (size_t)SPHRT_FWD_LDS_MIN : lds;
-#endif
-#define SPHRT_FWD_TABLE(TabT, E, R, H)                                                            \
+#define FWD_TABLE(TabT, E, R, H)                                                            \
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, TabT, E, P, R, H>), grid, block, lds, \
-                           st, SPHRT_FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
-#define SPHRT_FWD_TABLE_R(TabT, E, H)                                                             \
+                           st, FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
+#define FWD_TABLE_R(TabT, E, H)                                                             \
         do {                                                                                      \
-            if (c->runs) SPHRT_FWD_TABLE(TabT, E, true, H);                                       \
-            else SPHRT_FWD_TABLE(TabT, E, false, H);                                              \
+            if (c->runs) FWD_TABLE(TabT, E, true, H);                                       \
+            else FWD_TABLE(TabT, E, false, H);                                              \
         } while (0)
-#define SPHRT_FWD_TABLE_E(TabT)                                                                   \
+#define FWD_TABLE_E(TabT)                                                                   \
         do {                                                                                      \
             if (half) {                                                                           \
-                if constexpr (sizeof(T) == 8 && P == kPer) { SPHRT_FWD_TABLE_R(TabT, true, true); } \
+                if constexpr (sizeof(T) == 8 && P == kPer) { FWD_TABLE_R(TabT, true, true); } \
             } else if (edma) {                                                                    \
-                SPHRT_FWD_TABLE_R(TabT, true, false);                                             \
+                FWD_TABLE_R(TabT, true, false);                                             \
             } else {                                                                              \
-                SPHRT_FWD_TABLE_R(TabT, false, false);                                            \
+                FWD_TABLE_R(TabT, false, false);                                            \
             }                                                                                     \
         } while (0)
         if (c->tab_bytes == 2) {
-            SPHRT_FWD_TABLE_E(uint16_t);
+            FWD_TABLE_E(uint16_t);
         } else {
-            SPHRT_FWD_TABLE_E(int32_t);
+            FWD_TABLE_E(int32_t);
         }
-#undef SPHRT_FWD_TABLE_E
-#undef SPHRT_FWD_TABLE_R
-#undef SPHRT_FWD_TABLE
+#undef FWD_TABLE_E
+#undef FWD_TABLE_R
+#undef FWD_TABLE
         if (c->n_fallback > 0) {   // (natural vox, natural density)
             if (int e = check_launch("forward_kernel<table>")) return e;
             hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0,
-                               st, SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 1,
+                               st, FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 1,
                                nullptr);
         }
     } else {
         hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0, st,
-                           SPHRT_FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, nullptr);
+                           FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, nullptr);
     }
-#undef SPHRT_FWD_ARGS
+#undef FWD_ARGS
     return check_launch(sizeof(T) == 4 ? "forward_kernel<f32>" : "forward_kernel<f64>");
 }
 

@@ -161,11 +161,7 @@ __global__ __launch_bounds__(kLossThreads) void adam_neg_kernel(
 
 static unsigned loss_grid(int64_t n) {
     const int64_t b = (n + kLossThreads - 1) / kLossThreads;
-    static const int64_t cap = [] {   // SPHRT_LOSS_BLOCKS: A/B studies
-        const char* e = getenv("SPHRT_LOSS_BLOCKS");
-        return (int64_t)(e ? atoi(e) : kLossMaxBlocks);
-    }();
-    return (unsigned)(b < cap ? (b > 0 ? b : 1) : cap);
+    return (unsigned)(b < kLossMaxBlocks ? (b > 0 ? b : 1) : kLossMaxBlocks);
 }
 
 }  // namespace sphrt

@@ -41,45 +41,8 @@ enum { MODE_COUNT = 0, MODE_FILL = 1, MODE_INTEGRATE = 2, MODE_EMIT = 3, MODE_BO
 constexpr int kNone = 0x7fffffff;  // "no update" in the forward-fill scans
 constexpr int kWavesPerBlock = 4;
 
-// Diagnostic build only (-DSPHRT_TRACE_STAMPS, tools/trace_phases.py): s_memtime cycles per trace
-// phase summed over all hit rays (0 solve+push, 1 sort, 2 tie check, 3 fill/lengths, 4 emit);
-// exact_wave_kernel: 8 rays, 9..12 its phases, 13 / 14 the largest ray / partition phase, 15
-// depth-limit ranges; 16 / 17 partitions below the top levels and their cycles, 18 depth-limit
-// cycles.
-#ifdef SPHRT_TRACE_STAMPS
-__device__ unsigned long long g_trace_cycles[24];   // 8..18: exact_wave_kernel
-#define TRACE_T(var) const uint64_t var = __builtin_amdgcn_s_memtime()
-#define TRACE_ADD(i, a, b) \
-    do { if (lane == 0) atomicAdd(&g_trace_cycles[i], (unsigned long long)((b) - (a))); } while (0)
-#define TRACE_MAX(i, a, b) \
-    do { if (lane == 0) atomicMax(&g_trace_cycles[i], (unsigned long long)((b) - (a))); } while (0)
-#else
-#define TRACE_MAX(i, a, b) do {} while (0)
-#define TRACE_T(var) do {} while (0)
-#define TRACE_ADD(i, a, b) do {} while (0)
-#endif
 constexpr size_t kLdsBytes = 160 * 1024;        // LDS per CU; one workgroup may take all of it
 
-// Ablation builds only (-DSPHRT_TRACE_ABL=k, tools/abl_trace.sh): trace_one stops after phase k
-// (1 solve + list, 2 sort, 3 tie check, 4 fill; inside phase 1: 11 after the shells, 12 after
-// the cones) with a zero segment count — wrong results by design; the PMC difference between
-// consecutive stops is the phase's instruction count.
-#ifdef SPHRT_TRACE_ABL
-#define TRACE_ABL(k)                                                                          \
-    do {                                                                                      \
-        if (SPHRT_TRACE_ABL == (k)) {                                                         \
-            if ((MODE == MODE_COUNT || MODE == MODE_EMIT) && lane == 0) o.counts[ray] = 0;    \
-            wave_sync();                                                                      \
-            return;                                                                           \
-        }                                                                                     \
-    } while (0)
-#else
-#define TRACE_ABL(k) do {} while (0)
-#endif
-
-#ifndef SPHRT_SORT_INLINE
-#define SPHRT_SORT_INLINE
-#endif
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -131,10 +94,7 @@ __device__ __forceinline__ int scan_last(int v, int /*lane*/) {
 // xor 16 / 31 inside 32 lanes, the gfx950 32-lane swap for xor 32.
 // xor 4 / 8 through ds_swizzle (the LDS crossbar, no VALU issue) instead of two row shifts and a
 // select (three VALU instructions per dword).  Trace kernel, same box, round 4: C3 3126 -> 3113,
-// C5 525 -> 520, C2 124.6 -> 122.4 us (profiles/r04_trace_ab.txt); 0 restores the row shifts.
-#ifndef SPHRT_XLANE_SWZ
-#define SPHRT_XLANE_SWZ 1
-#endif
+// C5 525 -> 520, C2 124.6 -> 122.4 us (profiles/r04_trace_ab.txt).
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
@@ -146,10 +106,7 @@ __device__ __forceinline__ uint32_t xlane(uint32_t x, int lane) {
     else if constexpr (X == 3) return dpp_mov<0x1B>(x);            // quad_perm [3,2,1,0]
     else if constexpr (X == 7) return dpp_mov<0x141>(x);           // row_half_mirror
     else if constexpr (X == 15) return dpp_mov<0x140>(x);          // row_mirror
-    else if constexpr ((X == 4 || X == 8) && !SPHRT_XLANE_SWZ) {  // row_shl / row_shr by X
-        const uint32_t up = dpp_mov<0x100 + X>(x), dn = dpp_mov<0x110 + X>(x);
-        return (lane & X) ? dn : up;
-    } else if constexpr (X == 4 || X == 8 || X == 16 || X == 31) {
+    else if constexpr (X == 4 || X == 8 || X == 16 || X == 31) {
         return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (X << 10) | 0x1F);
     } else if constexpr (X == 32) {
         const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
@@ -273,7 +230,7 @@ __device__ __forceinline__ int finish_sort(const uint64_t (&k)[M], uint64_t* key
 //
 // Full sort: the bitonic network over all F <= 64*M entries.
 template <int M>
-__device__ SPHRT_SORT_INLINE int sort_regs(uint64_t* keys, uint32_t* pays, int F, int Sf, int cap, int lane,
+__device__ int sort_regs(uint64_t* keys, uint32_t* pays, int F, int Sf, int cap, int lane,
                           uint64_t cmask) {
     uint64_t k[M];
     const int front = F - Sf;
@@ -293,7 +250,7 @@ __device__ SPHRT_SORT_INLINE int sort_regs(uint64_t* keys, uint32_t* pays, int F
 // shell run and the padding between, the list is bitonic and one merge stage (log2(64 M)
 // half-cleaner layers) sorts it.  C3 (F ~153, ~88 shell entries): 28 + 8 layers on 2 + 4
 // registers instead of 36 on 4.
-// Merge path (SPHRT_MERGE_PATH): the shell run A (ascending composite keys: keys[Sn-1] ..
+// Merge path: the shell run A (ascending composite keys: keys[Sn-1] ..
 // keys[0], then keys[cap-1], keys[cap-2], ...) and the sorted other entries B (keys[Sn ..
 // Sn+O)) merged by rank — lane L finds how many of A precede output L*M (a binary search along
 // its diagonal), then takes its M outputs in turn — instead of log2(64 M) half-cleaner layers
@@ -302,10 +259,7 @@ __device__ SPHRT_SORT_INLINE int sort_regs(uint64_t* keys, uint32_t* pays, int F
 // radii).
 // On for lists of more than 128 entries (M >= 4): trace kernel, same box, C3 3193 -> 3175 us,
 // C5 540 -> 530 us; C2's shorter lists (M <= 2) measured 123.5 -> 125.3 us and keep the bitonic
-// merge.  SPHRT_MERGE_PATH=0: off everywhere.
-#ifndef SPHRT_MERGE_PATH
-#define SPHRT_MERGE_PATH 1
-#endif
+// merge.
 __device__ __forceinline__ uint64_t shell_run(const uint64_t* keys, int Sn, int cap, int i) {
     return i < Sn ? keys[Sn - 1 - i] : keys[cap - 1 - (i - Sn)];
 }
@@ -344,7 +298,7 @@ __device__ __forceinline__ bool shell_run_ascending(const uint64_t* keys, int Sn
 }
 
 template <int M, int M2>
-__device__ SPHRT_SORT_INLINE int merge_sort(uint64_t* keys, uint32_t* pays, int F, int Sn, int Sf, int cap,
+__device__ int merge_sort(uint64_t* keys, uint32_t* pays, int F, int Sn, int Sf, int cap,
                            int lane, uint64_t cmask) {
     const int S = Sn + Sf, O = F - S;
     {
@@ -365,7 +319,7 @@ __device__ SPHRT_SORT_INLINE int merge_sort(uint64_t* keys, uint32_t* pays, int 
     }
     constexpr int P = 64 * M;
     uint64_t k[M];
-    if (SPHRT_MERGE_PATH && M >= 4 && shell_run_ascending(keys, Sn, S, cap, lane)) {
+    if (M >= 4 && shell_run_ascending(keys, Sn, S, cap, lane)) {
         merge_path<M>(keys, F, Sn, S, cap, lane, k);
         return finish_sort<M>(k, keys, pays, F, lane, cmask);
     }
@@ -571,7 +525,7 @@ struct FillState {
 // when head + count <= gcap — an emit slot that fits; no LDS round trip, no copy loop).
 enum { kFillNone = 0, kFillLds = 1, kFillGlobal = 2 };
 template <int M, int STORE>
-__device__ SPHRT_SORT_INLINE int fill_regs(const GridDev& G, const uint64_t* keys, const uint32_t* pays, int F,
+__device__ int fill_regs(const GridDev& G, const uint64_t* keys, const uint32_t* pays, int F,
                          int lane, const FillState& fs, double* seg_len, int32_t* seg_vox,
                          int64_t gbase = 0, int64_t gcap = 0, int head = 0) {
     uint64_t kb[M];
@@ -710,7 +664,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
                           const int sa, const int64_t ray, uint64_t* keys, uint32_t* pays,
                           const int cap, const int lane, const TraceOut<T>& o) {
     // ---- 1. crossings -> LDS list (finite, t >= 0), min finite negative distance ----------
-    TRACE_T(ts0);
     // the ray's output slot bounds, loaded now: their round trip overlaps the solves instead of
     // following the sort
     int64_t slot0 = 0, slot1 = 0;
@@ -866,7 +819,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
             push(v && keep(to) && !(to == ti && ro == ri), to, nbr + j, ro, true);
         }
         s_near = base;
-        TRACE_ABL(11);                  // (ablation: after the shells)
         const int ce0 = 2 * nbr;
         for (int j0 = nbe > 64 ? first_may_cross(nbe, lane, cone_ok) : 0; j0 < nbe; j0 += 64) {
             const int j = j0 + lane;
@@ -884,7 +836,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
             push(v && keep(ta), ta, ce0 + j, ra);
             push(v && keep(tb) && !(tb == ta && rb == ra), tb, ce0 + nbe + j, rb);
         }
-        TRACE_ABL(12);                  // (ablation: after the cones)
         const int ca0 = 2 * nbr + 2 * nbe;
         for (int k0 = 0; k0 < p_count; k0 += 64) {
             const bool v = k0 + lane < p_count;
@@ -932,9 +883,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     wave_sync();
 
     // ---- 2. sort by (distance, candidate) ------------------------------------------------
-    TRACE_ABL(1);
-    TRACE_T(ts1);
-    TRACE_ADD(0, ts0, ts1);
     int sflags = 2;          // bit 0: repair the order; bit 1: look for ambiguous ties
     const int n_other = F - s_near - nfar;   // entries outside the shells' sorted run
     if (pair_fmt) sort_lds(keys, pays, F, lane);
@@ -953,9 +901,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     }
     if (sflags & 1) fix_near_ties(keys, pays, F, lane);
 
-    TRACE_ABL(2);
-    TRACE_T(ts2);
-    TRACE_ADD(1, ts1, ts2);
     const int r_lim = 2 * nbr, e_lim = 2 * nbr + 2 * nbe, start_c = G.K - 1;
     const int start_vals[3] = {sr, se, sa};
     if ((sflags & 2) && ambiguous_ties(keys, pays, F, lane, r_lim, e_lim, start_c, start_vals)) {
@@ -968,9 +913,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     }
 
     // ---- 3. forward fill, lengths, compaction ----------------------------------------------
-    TRACE_ABL(3);
-    TRACE_T(ts3);
-    TRACE_ADD(2, ts2, ts3);
     // every distance behind the start is integrated in the start voxel (raytracer.py:126,140)
     const int head = (start_ok && tneg < 0.0) ? 1 : 0;
     double* seg_len = reinterpret_cast<double*>(keys);
@@ -1041,9 +983,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
     }
 
     // ---- 4. emit ---------------------------------------------------------------------------
-    TRACE_ABL(4);
-    TRACE_T(ts4);
-    TRACE_ADD(3, ts3, ts4);
     if (MODE == MODE_COUNT) {
         if (lane == 0) o.counts[ray] = head + nseg;
     } else if (MODE == MODE_FILL || MODE == MODE_EMIT) {
@@ -1080,14 +1019,6 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
         }
     }
     wave_sync();
-    TRACE_T(ts5);
-    TRACE_ADD(4, ts4, ts5);
-#ifdef SPHRT_TRACE_STAMPS
-    if (lane == 0) {
-        atomicAdd(&g_trace_cycles[5], 1ull);
-        atomicAdd(&g_trace_cycles[6], (unsigned long long)F);
-    }
-#endif
 }
 
 // ---- segment-count bounds for the one-pass trace (MODE_BOUND) -------------------------------
@@ -1272,21 +1203,16 @@ __global__ __launch_bounds__(256) void screen_kernel(GridDev G, RaysDev R, Trace
     }
 }
 
-// Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
-// image looks like.  Every lane evaluates the (wave-uniform) ray set-up itself.
-template <int MODE, typename T>
 // Trace workgroups of kWavesPerBlock waves (scaled for fewer).  Each wave drains a fixed stride
 // of the hit list, so more, shorter-lived workgroups let the dispatcher balance the rays' unequal
 // costs: one-pass emit, µs, grid 2048 / 4096 / 8192 / 16384 (same box, rocprofv3): C3 3495 /
 // 3317 / 3238 / 3200, C5 579 / 575 / 555 / 534, C4 380 / 358 / 352 / 351, C2 129 / 124 / 124 /
 // 127 (profiles/r03_trace_grid_sweep.json).
-#ifndef SPHRT_TRACE_GRID
-#define SPHRT_TRACE_GRID 16384
-#endif
-#ifndef SPHRT_TRACE_MIN_BLOCKS
-#define SPHRT_TRACE_MIN_BLOCKS 4
-#endif
-__global__ __launch_bounds__(256, SPHRT_TRACE_MIN_BLOCKS) void trace_kernel(GridDev G, TraceOut<T> o,
+constexpr int kTraceGrid = 16384;
+// Trace the hit rays, one per wave at a time, strided over the list: balanced whatever the
+// image looks like.  Every lane evaluates the (wave-uniform) ray set-up itself.
+template <int MODE, typename T>
+__global__ __launch_bounds__(256, 4) void trace_kernel(GridDev G, TraceOut<T> o,
                                                                             int cap) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63;
@@ -1774,7 +1700,6 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
         double x[3], d[3];
         int s[3];
         load_ray(R, ray, x, d, s);
-        TRACE_T(x0);
         const RayGeoT<F> g = exact_geo<F>(x, d);
         exact_list<ALL>(G, R, g, x, d, tid, 64 * W, [&](int c, double t, int reg) {
             tk[c] = t;
@@ -1797,10 +1722,7 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
             __syncthreads();
             continue;
         }
-        TRACE_T(x1);
         if (wid == 0) {
-            TRACE_ADD(8, 0, 1);
-            TRACE_ADD(9, x0, x1);
         }
         // ---- partition phase (uniform control flow per wave) ----
         // the top levels, breadth-first: range w of level l splits into ranges w and w + 2^l
@@ -1830,21 +1752,13 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
         while (have) {
             while (last - first > kIntroThreshold) {
                 if (depth == 0) {                      // the reference's heapsort
-                    TRACE_T(h0);
                     exact_heap_range<INV>(v, tk, pk, ts, ps, lpos, first, last, K, r_lim, e_lim,
                                           s, lane, o.n_heap);
-                    TRACE_T(h1);
-                    TRACE_ADD(15, 0, 1);
-                    TRACE_ADD(18, h0, h1);
                     first = last;                      // sorted: no leaf
                     break;
                 }
                 --depth;
-                TRACE_T(p0);
                 const int cut = exact_partition(v, tk, pk, lpos, rpos, first, last, lane, below);
-                TRACE_T(p1);
-                TRACE_ADD(16, 0, 1);
-                TRACE_ADD(17, p0, p1);
                 if (lane == 0) {
                     st_first[sp] = cut;
                     st_last[sp] = last;
@@ -1867,10 +1781,7 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
             }
         }
         __syncthreads();
-        TRACE_T(x2);
         if (wid == 0) {
-            TRACE_ADD(10, x1, x2);
-            TRACE_MAX(14, x1, x2);
         }
         // ---- final insertion sort = stable sort inside each leaf, as ranks ----
         for (int p = tid; p < K; p += 64 * W) {
@@ -1886,15 +1797,10 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
             ps[r] = pk[p];
         }
         __syncthreads();
-        TRACE_T(x3);
-        if (wid == 0) TRACE_ADD(11, x2, x3);
         // (the pre-sort list and the left-stop list are free now: compacted segments go there)
         if (wid == 0) exact_walk_wave<MODE, T, F, INV>(G, o, ray, s, ts, ps, lpos, tk, lane);
         __syncthreads();
-        TRACE_T(x4);
         if (wid == 0) {
-            TRACE_ADD(12, x3, x4);
-            TRACE_MAX(13, x0, x4);
         }
     }
 }
@@ -1908,13 +1814,7 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
 // step of 64 rays per wave, C3 compact_kernel 774 -> 707 us against a cap of 8192 workgroups on
 // one box.  8 chunks of 64 segments per step (loads before stores) instead of 4: C3 699 -> 669,
 // 700 -> 660 and 694 -> 688 us on three boxes.
-#ifndef SPHRT_COMPACT_BLOCKS
-#define SPHRT_COMPACT_BLOCKS (1 << 30)
-#endif
-#ifndef SPHRT_COMPACT_U
-#define SPHRT_COMPACT_U 8
-#endif
-constexpr int kCompactU = SPHRT_COMPACT_U;   // 64-segment chunks per step, loads before stores
+constexpr int kCompactU = 8;   // 64-segment chunks per step, loads before stores
 __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* __restrict__ slot,
                                                       const int64_t* __restrict__ row_ptr,
                                                       const int32_t* __restrict__ svox,
@@ -1982,11 +1882,8 @@ static bool exact_in_lds(const GridDev& G) {
     return exact_wave_lds(G.K, 1) <= kExactWaveLdsMax;
 }
 // Waves per deferred ray (exact_wave_kernel's W): 4 unless the list does not fit LDS with their
-// stacks.  SPHRT_EXACT_WAVES=1 builds the one-wave kernel (A/B).
-#ifndef SPHRT_EXACT_WAVES
-#define SPHRT_EXACT_WAVES 4
-#endif
-constexpr int kExactWaves = SPHRT_EXACT_WAVES;
+// stacks.
+constexpr int kExactWaves = 4;
 static bool exact_multi_wave(const GridDev& G) {
     return kExactWaves > 1 && exact_wave_lds(G.K, kExactWaves) <= kExactWaveLdsMax;
 }
@@ -2050,7 +1947,7 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     if constexpr (MODE == MODE_BOUND) return 0;
     if (!(steps & kTrace)) return 0;
     // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
-    const int64_t grid = SPHRT_TRACE_GRID * kWavesPerBlock / waves;
+    const int64_t grid = kTraceGrid * kWavesPerBlock / waves;
     hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,
                        o, cap);
     if (int e = check_launch("trace_kernel")) return e;
@@ -2071,16 +1968,6 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
 
 using namespace sphrt;
 
-#ifdef SPHRT_TRACE_STAMPS
-extern "C" int sphrt_diag_trace_cycles(unsigned long long* host, int reset) {
-    if (reset) {
-        unsigned long long z[24] = {};
-        return hipMemcpyToSymbol(HIP_SYMBOL(g_trace_cycles), z, sizeof(z)) == hipSuccess ? 0 : 1;
-    }
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace_cycles), 24 * sizeof(unsigned long long), 0,
-                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
-}
-#endif
 
 extern "C" size_t sphrt_trace_workspace_bytes(const sphrt_plan* plan, int64_t n) {
     if (!plan || n < 0) return 0;
@@ -2141,7 +2028,7 @@ extern "C" int sphrt_trace_compact(int64_t n, const int64_t* bound_ptr, const in
         return fail("null compact argument");
     StreamGuard guard(stream);
     const int64_t waves = (n + 63) / 64;
-    const int64_t cap = SPHRT_COMPACT_BLOCKS;
+    const int64_t cap = (int64_t)1 << 30;
     const int64_t blocks = (waves + 3) / 4 < cap ? (waves + 3) / 4 : cap;
     hipLaunchKernelGGL(compact_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                        n, bound_ptr, row_ptr, svox, slen, vox, len);

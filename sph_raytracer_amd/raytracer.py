@@ -137,7 +137,7 @@ class _Staging:
         if not self._parts:
             self._dev = None
             return
-        if tr.device(dev).type == 'cuda' and os.environ.get('SPHRT_PINNED_UPLOAD', '1') != '0':
+        if tr.device(dev).type == 'cuda':
             buf = tr.empty(self._size, dtype=tr.uint8, pin_memory=True)
             tr.cat(self._parts, out=buf)
             self._dev = buf.to(dev, non_blocking=True)
@@ -289,8 +289,8 @@ def _geom_rays(geom, dev):
 # azimuth columns per wedge of the ConeCirc trace order; measured (C5 forward f64 / transposed
 # adjoint f64 / retrieval iteration, C4 forward): 2: 46.5 / 42.5 / 0.157 ms, 21.9; 3: 45.8 /
 # 43.5 / 0.157 ms, 21.3; 4: 45.6 / 46.7 / 0.161 ms, 21.1; 5: 45.8 / 47.7 / 0.164 ms, 21.2; 8: 48.0
-# / 48.3 / 0.167 ms, 21.5 us.  SPHRT_WEDGE overrides it (A/B studies).
-_WEDGE = int(os.environ.get('SPHRT_WEDGE', '3'))
+# / 48.3 / 0.167 ms, 21.5 us.
+_WEDGE = 3
 
 
 def _trace_order(geom, rays):

@@ -26,8 +26,8 @@ def main():
     ap.add_argument('--out', required=True)
     ap.add_argument('--counters', default=None, help='comma-separated SQ counters (one pass)')
     ap.add_argument('--count-pass', action='store_true',
-                    help='profile tools/trace_time.py (the two-pass COUNT kernel, which the '
-                         'SPHRT_TRACE_ABL ablation builds cut short) instead of trace_bench.py')
+                    help='profile tools/trace_time.py (the two-pass COUNT kernel) instead of '
+                         'trace_bench.py')
     ap.add_argument('--match', default='trace_kernel',
                     help='kernels whose name contains this (e.g. screen_kernel)')
     args = ap.parse_args()
