@@ -291,7 +291,10 @@ int sphrt_csr_local_pack(const sphrt_csr *csr, const int64_t *blocks, const void
  * segments from the staging into csr->vox (with the row-head bits), csr->len and csr->len32 and
  * builds the tables from them — the same CSR, loc and tables as sphrt_trace_compact +
  * sphrt_csr_index + sphrt_csr_local_build (csr->vox/len/len32 are written through the const
- * pointers).  The staging may be freed after it. */
+ * pointers).  The staging may be freed after it — except with csr->len NULL: the float64
+ * lengths then stay in slen (the float32 forward reads len32 only) until
+ * sphrt_trace_compact(svox = vox = NULL) moves them into the CSR on the first use that needs
+ * them; svox may be freed right away. */
 int sphrt_csr_index_staged(const int64_t *row_ptr, int64_t n_rays, int32_t *row_ray,
                            int32_t *empty_ray, int64_t *blocks, int64_t n_blocks,
                            const int32_t *ray_ids, int32_t *nz_row, void *workspace, void *stream);

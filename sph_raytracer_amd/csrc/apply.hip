@@ -498,7 +498,7 @@ struct Staged {
 // t + kThreads, ... (striped: every load and store instruction covers consecutive segments;
 // thread t taking 8t .. 8t + 7 with one search and a walk measured C3 2.59 ms for gather +
 // tables against 1.22 + 0.68 ms for tables + compaction: stride-8 accesses).  Writes vox (head
-// bit on each row's first segment), len and len32, and hands the block's voxels to the table
+// bit on each row's first segment), len32 and (when S.len is set) len, and hands the block's voxels to the table
 // build in registers when it has at most ITEMS * kThreads segments (xs[i]: segment
 // i * kThreads + t; nothing is read back).
 template <int ITEMS>
@@ -555,7 +555,7 @@ __device__ __forceinline__ void staged_gather(const Staged& S, const int64_t* bl
         const double l = S.slen[src];
         const uint32_t x = p == st ? (v | kHead) : v;
         S.vox[s0 + p] = (int32_t)x;
-        S.len[s0 + p] = l;
+        if (S.len) S.len[s0 + p] = l;            // (NULL: the float64 lengths stay in slen)
         S.len32[s0 + p] = (float)l;
         return x;
     };
@@ -1885,8 +1885,8 @@ extern "C" int sphrt_csr_local_build_staged(const sphrt_csr* c, int64_t* blocks,
                                             const int32_t* nz_row, const int32_t* svox,
                                             const double* slen,
                                             void* stream) {
-    if (!c || !c->row_ptr || !c->vox || !c->len || !c->len32 || !blocks || !loc || !tab_wide ||
-        !stats || !slot || !nz_row || !svox || !slen)
+    if (!c || !c->row_ptr || !c->vox || !c->len32 || !blocks || !loc || !tab_wide || !stats ||
+        !slot || !nz_row || !svox || !slen)
         return fail("incomplete staged CSR for the granule tables");
     if (c->n_blocks < 1 || c->n_blocks > 0x7fffffff) return fail("bad CSR block count");
     if (c->n_rays > 0x7fffffff) return fail("the staged table build needs n_rays < 2^31");

@@ -767,6 +767,31 @@ def line_integrals(grid, geom, density):
         return out.reshape(out_shape).to(device=density.device, dtype=density.dtype)
 
 
+class _TraceRecord(dict):
+    """The trace's CSR record (row_ptr, vox, len, len32, tables, ...).  After the staged table
+    build 'len', the float64 segment lengths, is not written: it stays in the one-pass trace's
+    staging (slen at its bound slots) and is moved into the CSR on the first access — the first
+    float64 forward, adjoint, time pairing or segments() — by sphrt_trace_compact(lengths only),
+    which then frees the staging.  A float32-only Operator never writes it (the table build's
+    writes at C3: 18 -> 10 B per segment)."""
+
+    def __getitem__(self, k):
+        if k == 'len' and dict.__getitem__(self, 'len') is None:
+            self._move_len()
+        return dict.__getitem__(self, k)
+
+    def _move_len(self):
+        row_ptr, bound_ptr, slen, dev = dict.pop(self, 'len_staging')
+        total, n = dict.__getitem__(self, 'total'), dict.__getitem__(self, 'n')
+        seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
+        with tr.cuda.device(dev):
+            _lib.check(_lib.load().sphrt_trace_compact(
+                n, _lib.ptr(bound_ptr), None, _lib.ptr(slen), _lib.ptr(row_ptr), None,
+                _lib.ptr(seg_len), _lib.stream_of(dev)), 'sphrt_trace_compact(len)')
+        dict.__getitem__(self, 'desc').len = seg_len.data_ptr()
+        dict.__setitem__(self, 'len', seg_len)
+
+
 # ----- the operator ---------------------------------------------------------------------------
 
 class _LineIntegral(tr.autograd.Function):
@@ -960,9 +985,9 @@ class Operator:
         if staging is not None and not staged:
             vox, seg_len = _compact_staging(lib, n, row_ptr, total, staging, dev, stream)
             staging = None
-        elif staged:
+        elif staged:      # (the float64 lengths stay in the staging: _TraceRecord)
             vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
-            seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
+            seg_len = None
         # row index for the apply kernels: head bits, non-empty row list, workgroup blocks
         row_ray = tr.empty(max(n, 1), dtype=tr.int32, device=dev)
         empty_ray = tr.empty(n + 1, dtype=tr.int32, device=dev)
@@ -982,17 +1007,21 @@ class Operator:
                                            _lib.ptr(ray_id), _lib.ptr(iws), stream),
                        'sphrt_csr_index')
         del iws
-        c.row_ptr, c.vox, c.len = row_ptr.data_ptr(), vox.data_ptr(), seg_len.data_ptr()
+        c.row_ptr, c.vox = row_ptr.data_ptr(), vox.data_ptr()
+        c.len = seg_len.data_ptr() if seg_len is not None else None
         # the float32 lengths come with the granule tables (sphrt_csr_local_build writes len32)
-        len32 = tr.empty(seg_len.shape, dtype=tr.float32, device=dev)
+        len32 = tr.empty(vox.shape, dtype=tr.float32, device=dev)
         c.row_ray, c.blocks, c.len32 = row_ray.data_ptr(), blocks.data_ptr(), len32.data_ptr()
         c.empty_ray = empty_ray.data_ptr()
         loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream,
                                        staged=(staging, nz_row) if staged else None)
+        self._csr = _TraceRecord(row_ptr=row_ptr, vox=vox, len=seg_len, len32=len32,
+                                 row_ray=row_ray, empty_ray=empty_ray, blocks=blocks, loc=loc,
+                                 tab=tab, runs=runs, nblocks=nblocks, n=n, total=total, desc=c,
+                                 ray_id=ray_id)
+        if seg_len is None:         # the staging's lengths, kept (its voxels are freed here)
+            self._csr['len_staging'] = (row_ptr, staging[0], staging[2], dev)
         del staging, nz_row
-        self._csr = dict(row_ptr=row_ptr, vox=vox, len=seg_len, len32=len32, row_ray=row_ray,
-                         empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, runs=runs,
-                         nblocks=nblocks, n=n, total=total, desc=c, ray_id=ray_id)
         self._batch = batch
 
     # -- shape logic of raytracer.py:703-712 -----------------------------------------------------
@@ -1069,8 +1098,9 @@ class Operator:
         vol = math.prod(self.grid.shape[-3:])
         if div > 0:
             rec = self._paired(d.shape[0], div)
-            if rec is not None:
+            if rec is not None:   # (the trace's lengths: the float64 ones once moved, _lengths)
                 rec['desc'].len32 = self._csr['desc'].len32
+                rec['desc'].len = self._csr['desc'].len
                 return rec['desc'], 1, rec['desc'].n_cols, 0
         return self._csr['desc'], n_chan, vol, div
 
@@ -1170,6 +1200,8 @@ class Operator:
         stream = _lib.stream_of(dev)
         n_vox = n_cols
         total = csr['total']
+        csr['len']                       # (the float64 lengths moved out of the staging, if not yet)
+        src.len = csr['desc'].len        # (a time-paired CSR shares the trace's lengths)
         col_ptr = tr.empty(n_vox + 1, dtype=tr.int64, device=dev)
         t_ray = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
         t_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
@@ -1276,6 +1308,7 @@ class Operator:
             _alternate(tdesc)
             return res.reshape(dshape).to(device=ddevice, dtype=ddtype)
         acc = tr.zeros(math.prod(dshape), dtype=tr.float64, device=dev)
+        csr['len']                       # (the float64 lengths moved out of the staging, if not yet)
         _lib.check(_lib.load().sphrt_adjoint_accumulate(
             csr['desc'], _lib.ptr(yv), int(ydt == tr.float64), n_chan, n, div, _lib.ptr(acc), vol,
             _lib.stream_of(dev)), 'sphrt_adjoint_accumulate')
