@@ -19,8 +19,8 @@ its forward + dynamic gradient), ``--config c5`` times the static_retrieval.py g
 C2 run reports both legs too (``strong``), each checked against one GPU over the whole orbit.
 
 One JSON line on rank 0: value = rays/s over all ranks; roofline of the forward kernel
-(algorithmic bytes per launch / its mean duration from HIP events over graph-replayed
-launches); cpu_baseline = the reference's forward (torch CPU on the reference's padded trace,
+(algorithmic bytes per launch / its mean launch duration from HIP events around the timed steps
+on the launch stream; the graph-replayed kernel alone beside it); cpu_baseline = the reference's forward (torch CPU on the reference's padded trace,
 oracle/ref_forward.py) on a bounded sample, timed on this host.
 """
 import argparse
@@ -620,13 +620,20 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # HIP events on the launch stream (the current stream: op(x) launches there) bracket the
+    # timed steps: their span / K is the forward's average launch duration over the timed region
+    # (the roofline's denominator; it includes the short gaps between back-to-back launches)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
+    ev0.record()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    ev1.record()
     torch.cuda.synchronize(dev)
     barrier()
     dt = time.perf_counter() - t0
+    k_ms_timed = ev0.elapsed_time(ev1) / args.steps
     gather = None
     if dist is not None:
         dt, t_cold = max_over_ranks([dt, t_cold])
@@ -679,7 +686,7 @@ def main():
 
     k_reps = 50
     adj_steps = min(args.steps, 50)      # the adjoint leg below
-    k_ms, k_method = kernel_time_ms(op, x, reps=k_reps)
+    k_ms_graph, _ = kernel_time_ms(op, x, reps=k_reps)
     # launch order of the forward kernel in this process, for tools/rocprof_legs.py (splits a
     # rocprofv3 kernel trace of this command into these legs)
     log('legs ' + json.dumps([['first', 1], ['warmup', args.warmup], ['steps', args.steps]] +
@@ -729,7 +736,11 @@ def main():
                    'what': 'op.T(y), y = torch.rand(geom.shape): the transposed CSR (built by the '
                            'first of 3 untimed calls) through the same table kernel; per-step '
                            'wall time incl. launch; bytes as SURVEY 8(d) with voxels as rows'}
-    roof = roofline(op, x, args.config, k_ms, k_method)
+    roof = roofline(op, x, args.config, k_ms_timed,
+                    'HIP events on the launch stream around the timed steps (span / K)')
+    # the same kernel back to back in a HIP graph (no host issue between launches), for reference
+    roof['kernel_ms_graph_replay'] = k_ms_graph
+    roof['frac_graph_replay'] = roof['bytes_per_launch'] / (k_ms_graph * 1e-3) / 1e9 / HBM_PEAK_GBS
 
     rec = {
         'metric': METRIC,

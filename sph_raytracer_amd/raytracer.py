@@ -1322,11 +1322,21 @@ class Operator:
             res = acc.to(ddtype)
         return res.reshape(dshape).to(ddevice)
 
-    def T(self, line_integrations):
+    def T(self, line_integrations, *, time_slices=False):
         """Back-projection of ``line_integrations`` (geom.shape) into a grid.shape volume
-        (raytracer.py:715-748).  Static grids only, like the reference."""
+        (raytracer.py:715-748).  Static grids only, like the reference (raytracer.py:733-734
+        raises for a dynamic grid) — unless ``time_slices=True``: a dynamic grid's adjoint, y of
+        shape (T, H, W) -> (T, nr, ne, na), view i back-projected into time slice i (or every
+        time step's image through the one geometry), i.e. the gradient autograd gives the
+        forward, natively (the time-paired CSR transposed)."""
         if self.grid.dynamic:
-            raise NotImplementedError
+            if not time_slices:
+                raise NotImplementedError
+            y = tr.as_tensor(line_integrations)
+            if self._csr is None:
+                raise RuntimeError('Operator was built with _compute=False')
+            dshape = (int(y.shape[0]),) + tuple(int(v) for v in self.grid.shape[1:])
+            return self._apply_adjoint(y, dshape, y.dtype, tr.device(self.device))
         fc = self._fastc_T
         if fc is not None:
             # steady state in one C call: the transposed CSR's forward (csrc/fastpath.cpp)

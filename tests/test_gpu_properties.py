@@ -606,6 +606,39 @@ def test_adjoint_fast_path_matches_general_path(c2, gpu):
     assert tr.equal(cop.T(yc), cop.T(yc)) and cop._fastc_T is None
 
 
+@pytest.mark.parametrize('dt', [tr.float64, tr.float32])
+def test_dynamic_operator_T_time_slices(gpu, dt):
+    """Operator.T on a dynamic grid: raises like the reference (raytracer.py:733-734) unless
+    time_slices=True, which gives the native time-indexed adjoint — equal to the gradient
+    autograd gives the forward (bitwise: the same transposed time-paired CSR), and for one
+    geometry over every time step, to the static adjoint of each step's image."""
+    from sph_raytracer_amd import ConeCircGeom, Operator, SphericalGrid
+    T = 5
+    grid = SphericalGrid(shape=(T, 12, 10, 16))
+    geom = sum(ConeCircGeom(shape=(24, 16), pos=(5 * tr.cos(th), 5 * tr.sin(th), 1), fov=(0, 45))
+               for th in tr.linspace(0, 2 * tr.pi, T))
+    op = Operator(grid, geom, dynamic=True, device=gpu)
+    g = tr.Generator(device=gpu).manual_seed(3)
+    x = tr.rand(grid.shape, dtype=dt, device=gpu, generator=g)
+    y = tr.rand(geom.shape, dtype=dt, device=gpu, generator=g)
+    with pytest.raises(NotImplementedError):
+        op.T(y)
+    got = op.T(y, time_slices=True)
+    assert got.shape == grid.shape and got.dtype == dt
+    xg = x.clone().requires_grad_(True)
+    (op(xg) * y).sum().backward()
+    assert tr.equal(got, xg.grad)
+    # one geometry seen at every time step: slice t = the static adjoint of image t
+    single = geom.geoms[0]
+    op1 = Operator(grid, single, device=gpu)
+    st = Operator(SphericalGrid(shape=grid.shape[1:]), single, device=gpu)
+    ys = tr.rand((T,) + tuple(single.shape), dtype=dt, device=gpu, generator=g)
+    got1 = op1.T(ys, time_slices=True)
+    want = tr.stack([st.T(ys[t]) for t in range(T)])
+    tol = 1e-12 if dt == tr.float64 else 1e-5
+    assert tr.allclose(got1, want, rtol=tol, atol=tol * float(want.abs().max()))
+
+
 def test_dynamic_pairing_forward_and_adjoint(gpu):
     """View i <-> time slice i (dynamic grid, a collection of T views): the forward runs on the
     time-paired CSR (granule tables over the flattened (T, vol) density) and the adjoint on its
