@@ -928,9 +928,14 @@ __device__ void trace_one(const GridDev& G, const RayGeo& g, const double t1c_o,
         int32_t* sv = kDirect ? o.vox : seg_vox;
         const int64_t gcap = MODE == MODE_EMIT ? slot1 - slot0 : (int64_t)INT_MAX;
         const int64_t gb = slot0 + head;
+        // (the fill reads the sorted list lane-major at its own width: 3 and 6 entries per lane
+        // for F <= 192 / 384 instead of 4 / 8 — count pass C3 2857 -> 2810 us, C5 556 -> 548 us,
+        // C2 unchanged, profiles/r05_trace_fillm_ab.jsonl)
         nseg = F <= 64 ? fill_regs<1, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head)
              : F <= 128 ? fill_regs<2, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head)
+             : F <= 192 ? fill_regs<3, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head)
              : F <= 256 ? fill_regs<4, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head)
+             : F <= 384 ? fill_regs<6, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head)
                         : fill_regs<8, kStore>(G, keys, pays, F, lane, fs, sl, sv, gb, gcap, head);
     }
     for (int c0 = 0; pair_fmt && c0 < F; c0 += 64) {

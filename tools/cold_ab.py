@@ -22,10 +22,10 @@ def main():
     ap.add_argument('--dtype', default=None, choices=(None, 'float32', 'float64'))
     args = ap.parse_args()
     sys.path.insert(0, ROOT)
+    import torch
+    import bench            # (puts ROOT first on sys.path: --pkg goes in front of it after)
     if args.pkg:
         sys.path.insert(0, os.path.abspath(os.path.join(ROOT, args.pkg)))
-    import torch
-    import bench
     from sph_raytracer_amd import Operator
     dev = torch.device('cuda', 0)
     cfg = bench.CONFIGS[args.config]

@@ -23,8 +23,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--iters', type=int, default=100)
     ap.add_argument('--out', default=None)
+    ap.add_argument('--pkg', default=None,
+                    help='directory holding another revision\'s sph_raytracer_amd (A/B)')
+    ap.add_argument('--no-autograd', action='store_true', help='skip the autograd comparison')
     args = ap.parse_args()
-    import bench
+    import bench            # (puts ROOT first on sys.path: --pkg goes in front of it after)
+    if args.pkg:
+        sys.path.insert(0, os.path.abspath(os.path.join(ROOT, args.pkg)))
     from sph_raytracer_amd import Operator, retrieval
     from sph_raytracer_amd.loss import NegRegularizer, SquareLoss
     from sph_raytracer_amd.model import FullyDenseModel
@@ -54,12 +59,15 @@ def main():
         return out, time.perf_counter() - t0
 
     (coeffs, y_hat, hist), t_gd = run()          # the autograd-free loop (retrieval._gd_direct)
-    plan = retrieval._direct_plan
-    retrieval._direct_plan = lambda *a: None     # the same loop through autograd
-    (c_ag, _, hist_ag), t_ag = run()
-    retrieval._direct_plan = plan
+    if args.no_autograd:
+        (c_ag, hist_ag, t_ag) = (coeffs, hist, float('nan'))
+    else:
+        plan = retrieval._direct_plan
+        retrieval._direct_plan = lambda *a: None     # the same loop through autograd
+        (c_ag, _, hist_ag), t_ag = run()
+        retrieval._direct_plan = plan
     fid = hist[losses[0]]
-    rec = {'config': 'C5 retrieval: 64^3 grid, 64-view ConeCirc (100,50) orbit, FullyDenseModel, '
+    rec = {'pkg': args.pkg or '.', 'config': 'C5 retrieval: 64^3 grid, 64-view ConeCirc (100,50) orbit, FullyDenseModel, '
                      'SquareLoss + NegRegularizer, Adam lr 0.1, float64',
            'rays': op._csr['n'], 'segments': op._csr['total'], 'iterations': args.iters,
            'operator_init_ms': t_init * 1e3, 'gd_total_ms': t_gd * 1e3,
