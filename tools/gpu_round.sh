@@ -28,7 +28,7 @@ if [[ $STEPS == *bench* ]]; then
 fi
 if [[ $STEPS == *prof* ]]; then
   rm -rf $OUT/prof
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --no-strong-legs > $OUT/prof_bench.json 2> $OUT/prof.err
   for f in $(find $OUT/prof -name "*kernel_stats.csv"); do head -6 "$f"; cp "$f" $OUT/${TAG}_bench_c2_kernel_stats.csv; done
   python tools/rocprof_legs.py $OUT/prof $OUT/prof.err > $OUT/${TAG}_bench_c2_rocprof_legs.json
   cat $OUT/${TAG}_bench_c2_rocprof_legs.json
