@@ -153,14 +153,14 @@ def load():
     return lib
 
 
-def _check_hash(version, path):
+def _check_hash(version, path, fast=False):
     """Refuse a library built from other sources than this tree's (build.source_hash, embedded
     as the version's 'src <hash>'): a stale binary shipped next to edited sources would
     otherwise run silently.  Trees without the sources (an installed copy) skip the check."""
     from . import build
     if not build.have_sources():
         return
-    want = build.source_hash()
+    want = build.fast_hash() if fast else build.source_hash()
     got = version.rsplit(' src ', 1)[-1] if ' src ' in version else None
     if got != want:
         raise RuntimeError(f'sph_raytracer_amd: {path} was built from sources {got}, this tree is '
@@ -187,9 +187,27 @@ def load_fast():
             spec = importlib.util.spec_from_file_location('_sphrt_fast', FAST_PATH)
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)
-            _check_hash(getattr(mod, 'version', ''), FAST_PATH)
+            _check_hash(getattr(mod, 'version', ''), FAST_PATH, fast=True)
             _fast = mod
     return _fast or None
+
+
+_construct = None
+
+
+def load_construct():
+    """The fast entry bound for Operator construction (csrc/construct.cpp: build_cone over the
+    library this module loaded), or None when the entry was not built."""
+    global _construct
+    if _construct is None:
+        _construct = False
+        fast = load_fast()
+        if fast is not None:
+            from .geometry import ConeCircGeom, ConeRectGeom, ViewGeomCollection
+            load()
+            fast.construct_bind(LIB_PATH, ConeRectGeom, ConeCircGeom, ViewGeomCollection)
+            _construct = fast
+    return _construct or None
 
 
 def address(fn):

@@ -31,30 +31,40 @@ def hipcc():
 
 
 _FLAGS = ['-O3', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off', '-munsafe-fp-atomics']
-FAST_SOURCE = 'fastpath.cpp'
+FAST_SOURCES = ['fastpath.cpp', 'construct.cpp']
+_FAST_FLAGS = ['-O2', '-std=c++17', '-fPIC', '-shared', '-ffp-contract=off']
 # sphrt_version() ends in "src <hash>"; the same text is in the library file (host rodata), so a
 # build's hash can be read without loading it
 _HASH_RE = re.compile(rb'sph_raytracer_amd [^\x00]*? src ([0-9a-f]{16})')
 
 
-def source_hash():
-    """Hash of everything the libraries are built from: the HIP/C++ sources and headers, the C
-    ABI header, the target and the compile flags (16 hex digits).  Embedded into both libraries
-    at build time (-DSPHRT_SOURCE_HASH); _lib.load() refuses a library whose hash differs from
-    the tree's, and build() rebuilds on a mismatch (not on file times)."""
+def _hash(files, flags):
     h = hashlib.sha256()
-    files = sorted(SOURCES + HEADERS + [FAST_SOURCE])
-    for name, path in [(f, os.path.join(CSRC, f)) for f in files] + \
+    for name, path in [(f, os.path.join(CSRC, f)) for f in sorted(files)] + \
             [('sphrt.h', os.path.join(ROOT, 'include', 'sphrt.h'))]:
         with open(path, 'rb') as fh:
             data = fh.read()
         h.update(name.encode() + b'\0' + str(len(data)).encode() + b'\0' + data)
-    h.update(' '.join([ARCH] + _FLAGS).encode())
+    h.update(' '.join(flags).encode())
     return h.hexdigest()[:16]
 
 
+def source_hash():
+    """Hash of everything libsphrt.so is built from: the HIP sources and headers, the C ABI
+    header, the target and the compile flags (16 hex digits).  Embedded into the library at build
+    time (-DSPHRT_SOURCE_HASH); _lib.load() refuses a library whose hash differs from the tree's,
+    and build() rebuilds on a mismatch (not on file times)."""
+    return _hash(SOURCES + HEADERS, [ARCH] + _FLAGS)
+
+
+def fast_hash():
+    """The same for _sphrt_fast.so (the CPython entry): its C++ sources, the C ABI header and its
+    flags; checked by _lib.load_fast()."""
+    return _hash(FAST_SOURCES, _FAST_FLAGS)
+
+
 def have_sources():
-    return all(os.path.exists(os.path.join(CSRC, f)) for f in SOURCES + HEADERS + [FAST_SOURCE])
+    return all(os.path.exists(os.path.join(CSRC, f)) for f in SOURCES + HEADERS + FAST_SOURCES)
 
 
 def embedded_hash(path):
@@ -73,23 +83,27 @@ def command(out=OUT, extra=()):
 
 
 def _stale(out):
-    return embedded_hash(out) != source_hash()
+    want = fast_hash() if os.path.basename(out).startswith('_sphrt_fast') else source_hash()
+    return embedded_hash(out) != want
 
 
 def fast_command(out=FAST_OUT):
-    """g++ for csrc/fastpath.cpp: host code against torch's C++ / CPython API (torch headers of the
-    interpreter that builds it), linked to the torch libraries it is loaded next to."""
+    """g++ for csrc/fastpath.cpp + construct.cpp: host code against torch's C++ / CPython API (torch
+    headers of the interpreter that builds it), linked to the torch libraries it is loaded next
+    to.  -ffp-contract=off: construct.cpp's host arithmetic (start voxels) is the exact IEEE
+    products and sums numpy does."""
     import sysconfig
     import torch
     tdir = os.path.dirname(torch.__file__)
-    return ['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-D__HIP_PLATFORM_AMD__=1',
-            '-DUSE_ROCM=1', f'-DSPHRT_SOURCE_HASH="{source_hash()}"',
+    return ['g++', *_FAST_FLAGS, '-D__HIP_PLATFORM_AMD__=1',
+            '-DUSE_ROCM=1', f'-DSPHRT_SOURCE_HASH="{fast_hash()}"',
             '-I', os.path.join(tdir, 'include'),
             '-I', os.path.join(tdir, 'include', 'torch', 'csrc', 'api', 'include'),
             '-I', '/opt/rocm/include', '-I', os.path.join(ROOT, 'include'),
             '-I', sysconfig.get_paths()['include'],
-            os.path.join(CSRC, 'fastpath.cpp'), '-L', os.path.join(tdir, 'lib'),
+            *[os.path.join(CSRC, f) for f in FAST_SOURCES], '-L', os.path.join(tdir, 'lib'),
             '-ltorch_python', '-ltorch', '-ltorch_cpu', '-lc10', '-lc10_hip',
+            '-L', '/opt/rocm/lib', '-lamdhip64', '-ldl',
             f'-Wl,-rpath,{os.path.join(tdir, "lib")}', '-o', out]
 
 
@@ -102,7 +116,7 @@ def build_fast(force=False, verbose=False):
         print(' '.join(cmd))
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError(f'g++ (fastpath.cpp) failed ({res.returncode}):\n{res.stderr[-4000:]}')
+        raise RuntimeError(f'g++ (fastpath.cpp, construct.cpp) failed ({res.returncode}):\n{res.stderr[-4000:]}')
     os.replace(tmp, FAST_OUT)
     return FAST_OUT
 

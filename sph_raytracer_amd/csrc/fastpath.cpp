@@ -164,11 +164,27 @@ PyObject* py_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     Py_RETURN_NONE;
 }
 
+}  // namespace
+
+namespace sphrt_fast {   // csrc/construct.cpp
+PyObject* construct_bind(PyObject*, PyObject* const*, Py_ssize_t);
+PyObject* construct_cone_host(PyObject*, PyObject* const*, Py_ssize_t);
+PyObject* construct_build_cone(PyObject*, PyObject* const*, Py_ssize_t);
+}  // namespace sphrt_fast
+
+namespace {
+
 PyMethodDef methods[] = {
     {"new", (PyCFunction)py_new, METH_O, "new(last_error_address) -> bindings"},
     {"add", (PyCFunction)(void (*)(void))py_add, METH_FASTCALL, "bind a density shape"},
     {"forward", (PyCFunction)(void (*)(void))py_forward, METH_FASTCALL,
      "forward(bindings, density) -> Tensor | None"},
+    {"construct_bind", (PyCFunction)(void (*)(void))sphrt_fast::construct_bind, METH_FASTCALL,
+     "construct_bind(lib_path, ConeRectGeom, ConeCircGeom, ViewGeomCollection)"},
+    {"cone_host", (PyCFunction)(void (*)(void))sphrt_fast::construct_cone_host, METH_FASTCALL,
+     "cone_host(geom, r_b, e_b, a_b, nr, ne, na) -> host values of the trace | None"},
+    {"build_cone", (PyCFunction)(void (*)(void))sphrt_fast::construct_build_cone, METH_FASTCALL,
+     "build_cone(geom, r_b, e_b, a_b, nr, ne, na, perm, n_cols, csr_address) -> CSR | None"},
     {nullptr, nullptr, 0, nullptr},
 };
 

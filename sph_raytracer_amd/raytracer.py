@@ -767,6 +767,20 @@ def line_integrals(grid, geom, density):
         return out.reshape(out_shape).to(device=density.device, dtype=density.dtype)
 
 
+# switches of the Python construction sequence: any of them set keeps Operator construction in
+# Python, as SPHRT_CONSTRUCT=python does (the parity tests and A/B runs)
+_NATIVE_OFF = ('SPHRT_TRACE', 'SPHRT_TABLES', 'SPHRT_TABLE_STAGED', 'SPHRT_RUNS',
+               'SPHRT_RAY_ORDER', 'SPHRT_BRICK')
+
+
+class _NativeBatch:
+    """What an Operator keeps of its ray batch after a native construction (debug_los prints
+    the start)."""
+
+    def __init__(self, xs, shape):
+        self.xs, self.shape = xs, shape
+
+
 class _TraceRecord(dict):
     """The trace's CSR record (row_ptr, vox, len, len32, tables, ...).  After the staged table
     build 'len', the float64 segment lengths, is not written: it stays in the one-pass trace's
@@ -880,6 +894,8 @@ class Operator:
     def _trace_on(self, dev):
         if self._reference_mode():
             return self._trace_reference(dev)
+        if self._trace_native(dev):
+            return
         lib = _lib.load()
         # plan tables, cone-ray spec and start bins: one host-to-device copy
         stg = _Staging()
@@ -923,6 +939,39 @@ class Operator:
         row_ptr, vox, seg_len, total, staging = _trace_csr(lib, self._plan, batch, dev, stream,
                                                            keep_staging=True)
         self._index(lib, dev, batch, row_ptr, vox, seg_len, total, ray_id, staging)
+
+    def _trace_native(self, dev):
+        """The construction below (cone detectors, float64, default switches) in one C++ call:
+        _sphrt_fast.build_cone (csrc/construct.cpp) computes the same host values with the same
+        torch CPU operations and runs the same one-pass trace and staged table build, without
+        the Python between kernels (C2 0.80 -> see DESIGN.md §4).  False: not applicable, or a
+        rare branch (a ray over its bound, a staging that does not fit) the Python sequence
+        handles; nothing of the Operator was set."""
+        fc = _lib.load_construct()
+        if (fc is None or _bound_hook is not None or any(k in os.environ for k in _NATIVE_OFF)
+                or os.environ.get('SPHRT_CONSTRUCT', 'native') == 'python'):
+            return False
+        shape = tuple(self.geom.shape)
+        perm = None
+        if len(shape) in (2, 3) and shape[-1] > _WEDGE:     # _trace_order (ConeCirc views)
+            perm = _wedge_order(shape[-2], shape[-1])
+        g = self.grid
+        c = _lib.CSR()
+        res = fc.build_cone(self.geom, g.r_b, g.e_b, g.a_b, g.shape.r, g.shape.e, g.shape.a, perm,
+                            math.prod(g.shape[-3:]), ctypes.addressof(c))
+        if res is None:
+            return False
+        (row_ptr, vox, len32, row_ray, empty_ray, blocks, loc, tab, runs, ray_id, bound_ptr, slen,
+         xs, total, nblocks, rshape) = res
+        self._plan = None
+        self._ray_shape = rshape
+        self._batch = _NativeBatch(xs, rshape)
+        n = math.prod(rshape)
+        self._csr = _TraceRecord(row_ptr=row_ptr, vox=vox, len=None, len32=len32, row_ray=row_ray,
+                                 empty_ray=empty_ray, blocks=blocks, loc=loc, tab=tab, runs=runs,
+                                 nblocks=nblocks, n=n, total=total, desc=c, ray_id=ray_id)
+        self._csr['len_staging'] = (row_ptr, bound_ptr, slen, dev)
+        return True
 
     def _trace_reference(self, dev):
         """Trace in reference mode: every ray through the exact path with the reference's own

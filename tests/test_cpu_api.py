@@ -325,17 +325,20 @@ def test_library_builds_and_exports_header():
 
 
 def test_library_carries_the_tree_hash(tmp_path, monkeypatch):
-    """Both libraries embed the hash of the sources + flags they were built from; it equals this
-    tree's, build() decides staleness by it (not by file times), and a library built from other
-    sources is refused at load."""
+    """Both libraries embed the hash of the sources + flags they were built from (each its own:
+    libsphrt.so its HIP sources, _sphrt_fast.so its C++ ones); it equals this tree's, build()
+    decides staleness by it (not by file times), and a library built from other sources is
+    refused at load."""
     from sph_raytracer_amd import _lib, build
     build.build()
     want = build.source_hash()
     assert len(want) == 16
     assert build.embedded_hash(build.OUT) == want == _lib.source_hash()
-    assert build.embedded_hash(build.FAST_OUT) == want
-    assert _lib.load_fast().version.endswith(want)
-    assert not build._stale(build.OUT)
+    fast = build.fast_hash()
+    assert len(fast) == 16 and fast != want
+    assert build.embedded_hash(build.FAST_OUT) == fast
+    assert _lib.load_fast().version.endswith(fast)
+    assert not build._stale(build.OUT) and not build._stale(build.FAST_OUT)
     fake = tmp_path / 'lib.so'
     fake.write_bytes(b'\0sph_raytracer_amd 0.3 (gfx950) src 0123456789abcdef\0')
     assert build.embedded_hash(str(fake)) == '0123456789abcdef' and build._stale(str(fake))
