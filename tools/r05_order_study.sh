@@ -13,3 +13,5 @@ for i in 1 2; do
   done
 done
 cut -c1-200 $O/times.jsonl
+# native construction timeline at C2 (kernel trace; gaps = host turns between launches)
+timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $O/prof_c2 -o run -- python tools/operator_time.py --config c2 --reps 5 > $O/prof_c2.log 2>&1
