@@ -516,6 +516,14 @@ __device__ __forceinline__ void staged_gather(const Staged& S, const int64_t* bl
     const bool in_lds = rs_bytes + (size_t)nrow * 8 <= lds_cap;     // (block-uniform)
     int32_t* rs = reinterpret_cast<int32_t*>(lds);
     int64_t* rd = reinterpret_cast<int64_t*>(lds + rs_bytes);
+    // grids of several waves of workgroups: each segment's row as a uint16 per segment, written
+    // row by row (a wave per row, its lanes over the row's segments) instead of a binary search
+    // over the row starts per segment (C3 table kernel 1120 -> 1107 us, C5 198 -> 190 us); a
+    // one-wave grid (C2) is bound by each workgroup's chain, which the extra barrier lengthens
+    // (35 -> 41 us), and keeps the search (profiles/r05_gather_ab.json)
+    const bool rid_ok = nb > 256 * 6 && in_lds &&
+                        rs_bytes + (size_t)nrow * 8 + (size_t)n * 2 <= lds_cap;
+    uint16_t* rid = reinterpret_cast<uint16_t*>(lds + rs_bytes + (size_t)nrow * 8);
     if (in_lds) {
         for (int t = tid; t < nrow; t += kThreads) {
             const int64_t r = S.nz_row[k0 + t];
@@ -526,10 +534,17 @@ __device__ __forceinline__ void staged_gather(const Staged& S, const int64_t* bl
         if (tid == 0) rs[nrow] = (int32_t)n;      // sentinel: the end of the last row
     }
     __syncthreads();
+    if (rid_ok) {
+        const int lane = tid & 63;
+        for (int t = tid >> 6; t < nrow; t += kThreads / 64)
+            for (int p = rs[t] + lane, e = rs[t + 1]; p < e; p += 64) rid[p] = (uint16_t)t;
+        __syncthreads();
+    }
     auto start_of = [&](int t) -> int32_t {
         return in_lds ? rs[t] : (int32_t)(S.row_ptr[S.nz_row[k0 + t]] - s0);
     };
     auto row_of = [&](int p) {                    // last row t with start(t) <= p
+        if (rid_ok) return (int)rid[p];
         int lo = 0, hi = nrow - 1;
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
