@@ -582,6 +582,52 @@ _BRICK = (4, 2, 4)   # (r, e, a) voxels per staging brick: 32 = one 128-byte flo
 _SINGLE_WAVE_BLOCKS = 256 * 6   # forward workgroups resident at once (256 CUs x 6)
 
 
+_HEAD32 = -2 ** 31      # bit 31 of an int32 (the row-head flag of vox)
+
+# Row order of the transposed CSRs (the adjoint's rows are voxels): bricks of (r, e, a) voxels,
+# brick by brick in (r, e, a) order and inside a brick in (r, e, a) order, instead of the linear
+# voxel order (azimuth fastest).  A workgroup's ~32 voxels are then a compact cluster instead of
+# an azimuth arc, and its rays (the gathered columns) compact patches of each view: fewer
+# granules and L2 lines per workgroup.  Measured (profiles/r05_trows_ab.json, transposed adjoint
+# f32 / f64 us): C3 236.5 / 328.8 -> 208.4 / 310.8 with (4,2,4) bricks ((2,4,4) 221 / 324,
+# (4,4,4) 223 / 323, (8,8,4) 233 / 335), C5 27.8 / 44.2 -> 24.9 / 40.6; a one-wave grid (C2) is
+# neutral (6.3 / 8.8 -> 6.2 / 9.0) and keeps the linear order (and its row-run records); so
+# does the time-paired transpose of a dynamic operator (C4 gradient 37.5 -> 39.6 us with bricks
+# inside each slice).  C5 retrieval 0.1272 -> 0.1189 ms per iteration (profiles/r05_trows_ab.json).
+# The rows report their voxel through the index's row ids; each voxel's segments keep their
+# order (a stable sort), and a row's place in its workgroup sets how the segmented scan
+# associates its sum: the same adjoint up to summation order (deterministic, float64 within
+# 1e-13 of the linear order: test_transposed_brick_rows_equal_linear_rows).  SPHRT_TROWS=off
+# keeps the linear order, =b0,b1,b2 sets the brick.
+_TROWS = (4, 2, 4)
+
+
+def _voxel_rows(shape3, n_cols, dev, nblocks):
+    """(vpos, vperm) int32 on `dev`: row position of every voxel (column) of a static
+    transposed CSR and the voxel of every row position, or None (linear order)."""
+    env = os.environ.get('SPHRT_TROWS', 'auto')
+    brick = None if env == 'off' else tuple(int(v) for v in env.split(',')) if env != 'auto' \
+        else _TROWS if nblocks > _SINGLE_WAVE_BLOCKS else None
+    if brick is None or n_cols != math.prod(shape3) or n_cols >= 2 ** 31:
+        return None
+    return _voxel_rows_cached(shape3, brick, str(dev))
+
+
+@functools.lru_cache(maxsize=8)
+def _voxel_rows_cached(shape3, brick, dev):
+    nr, ne, na = shape3
+    br, be, ba = brick
+    idx = tr.arange(nr * ne * na, device=dev, dtype=tr.int64)
+    r, e, a = idx // (ne * na), (idx // na) % ne, idx % na
+    nbe, nba = -(-ne // be), -(-na // ba)
+    key = (((r // br) * nbe + e // be) * nba + a // ba) * (br * be * ba) + \
+        ((r % br) * be + e % be) * ba + a % ba
+    vperm = tr.argsort(key).to(tr.int32)                  # position -> voxel
+    vpos = tr.empty_like(vperm)
+    vpos[vperm.long()] = tr.arange(vperm.numel(), device=dev, dtype=tr.int32)
+    return vpos, vperm
+
+
 # Transposed CSRs (columns = rays) are not staged by default: detector tiles of (1, 4, 8) rays
 # measured C5 adjoint f32 40.5 -> 34.5 us but f64 59.6 -> 61.5 and C3 f32 229 -> 261, f64 327 ->
 # 354 us.  SPHRT_BRICK_T=b0,b1,b2 stages them (view, row, column).
@@ -1229,7 +1275,8 @@ class Operator:
         bitwise reproducible."""
         csr = self._csr
         if 'T' not in csr:
-            csr['T'] = self._transpose_of(csr['desc'], math.prod(self.grid.shape[-3:]))
+            csr['T'] = self._transpose_of(csr['desc'], math.prod(self.grid.shape[-3:]),
+                                          csr['vox'])
         return csr['T']
 
     def _ray_shape3(self):
@@ -1241,9 +1288,11 @@ class Operator:
         shape = [1] * max(0, 3 - len(shape)) + shape
         return (math.prod(shape[:-2]), shape[-2], shape[-1])
 
-    def _transpose_of(self, src, n_cols):
-        """Transpose of the CSR `src` (columns < n_cols) with its own index and granule tables;
-        its columns (rays) are brick-staged in detector tiles for multi-wave grids."""
+    def _transpose_of(self, src, n_cols, vox):
+        """Transpose of the CSR `src` (columns < n_cols; `vox` its column tensor) with its own
+        index and granule tables; its columns (rays) are brick-staged in detector tiles for
+        multi-wave grids.  Its rows (voxels) are ordered brick by brick (_voxel_rows) and report
+        their voxel through the index's row ids."""
         csr = self._csr
         lib, dev = _lib.load(), self._cdev
         stream = _lib.stream_of(dev)
@@ -1251,6 +1300,15 @@ class Operator:
         total = csr['total']
         csr['len']                       # (the float64 lengths moved out of the staging, if not yet)
         src.len = csr['desc'].len        # (a time-paired CSR shares the trace's lengths)
+        rows = _voxel_rows(tuple(int(v) for v in self.grid.shape[-3:]), n_cols, dev,
+                           csr['nblocks'])
+        if rows is not None:             # the columns renumbered in row order for the sort
+            vpos, vperm = rows
+            v = vox[:total]
+            pos = vpos.index_select(0, v & 0x7fffffff)
+            vox_pos = tr.where(v < 0, pos | _HEAD32, pos)
+            src = _lib.CSR.from_buffer_copy(src)
+            src.vox = vox_pos.data_ptr()
         col_ptr = tr.empty(n_vox + 1, dtype=tr.int64, device=dev)
         t_ray = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
         t_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
@@ -1259,6 +1317,8 @@ class Operator:
                                            _lib.ptr(t_len), _lib.ptr(ws), ws.numel(), stream),
                    'sphrt_csr_transpose')
         del ws
+        if rows is not None:
+            del vox_pos, pos, v
         nblocks = lib.sphrt_csr_blocks(total)
         vox_list = tr.empty(n_vox, dtype=tr.int32, device=dev)
         empty_vox = tr.empty(n_vox + 1, dtype=tr.int32, device=dev)
@@ -1266,7 +1326,8 @@ class Operator:
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n_vox), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(col_ptr), n_vox, _lib.ptr(t_ray),
                                        _lib.ptr(vox_list), _lib.ptr(empty_vox), _lib.ptr(blocks),
-                                       nblocks, None, _lib.ptr(iws), stream),
+                                       nblocks, _lib.ptr(rows[1]) if rows is not None else None,
+                                       _lib.ptr(iws), stream),
                    'sphrt_csr_index(T)')
         t_len32 = tr.empty(t_len.shape, dtype=tr.float32, device=dev)   # (filled with the tables)
         c = _lib.CSR()
@@ -1346,7 +1407,9 @@ class Operator:
                 yv = yv.view(-1, n).index_select(1, self._ray_id_long()).reshape(-1)
             if paired is not None:      # columns of the flattened (T, vol) density
                 if 'transposed' not in paired:
-                    paired['transposed'] = self._transpose_of(paired['desc'], paired['desc'].n_cols)
+                    paired['transposed'] = self._transpose_of(paired['desc'],
+                                                              paired['desc'].n_cols,
+                                                              paired['keep'][0])
                 tdesc, n_chan, vol = paired['transposed']['desc'], 1, paired['desc'].n_cols
             else:
                 tdesc = self._transposed()['desc']

@@ -1328,3 +1328,34 @@ def test_staged_table_build_equals_compaction(case, gpu, monkeypatch):
     x = tr.rand(grid.shape, dtype=tr.float32, device=gpu)
     assert tr.equal(op1(x), op0(x))
     assert tr.equal(op1(x.double()), op0(x.double()))
+
+
+def test_transposed_brick_rows_equal_linear_rows(gpu, monkeypatch):
+    """The static transposed CSR's rows in voxel-brick order (_voxel_rows, multi-wave grids) give
+    the adjoint of the linear voxel order (SPHRT_TROWS=off) up to summation order — every voxel
+    keeps its segments in the same order, but a row's place in its workgroup decides how the
+    segmented scan associates its sums (float64 within 1e-13, float32 within 1e-6 relative) — and
+    stay deterministic; the rows report their voxel through the index's row ids."""
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(40, (64, 64), kind='circ', grid_shape=(64, 64, 64))
+    outs = {}
+    for mode in ('auto', 'off', 'auto'):
+        monkeypatch.setenv('SPHRT_TROWS', mode)
+        op = Operator(grid, geom, device=gpu)
+        assert op._csr['nblocks'] > 256 * 6, 'a multi-wave grid'
+        g = tr.Generator(device=gpu).manual_seed(3)
+        res = []
+        for dt in (tr.float32, tr.float64):
+            x = tr.rand(grid.shape, dtype=dt, device=gpu, generator=g).requires_grad_(True)
+            y = tr.rand(geom.shape, dtype=dt, device=gpu, generator=g)
+            (op(x) * y).sum().backward()
+            res += [x.grad, op.T(y)]
+        if mode in outs:                  # deterministic: the same bits on a fresh Operator
+            for a, b in zip(res, outs[mode]):
+                assert tr.equal(a, b)
+        outs[mode] = res
+        rows = op._transposed()['keep'][4][:200]   # the voxels the first rows report:
+        assert bool((rows[1:] > rows[:-1]).all()) == (mode == 'off')   # ascending iff linear
+    for a, b in zip(outs['auto'], outs['off']):
+        tol = 1e-13 if a.dtype == tr.float64 else 1e-6
+        assert float((a - b).abs().max()) <= tol * float(b.abs().max()), a.dtype
