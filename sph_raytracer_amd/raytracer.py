@@ -628,10 +628,14 @@ def _voxel_rows_cached(shape3, brick, dev):
     return vpos, vperm
 
 
-# Transposed CSRs (columns = rays) are not staged by default: detector tiles of (1, 4, 8) rays
-# measured C5 adjoint f32 40.5 -> 34.5 us but f64 59.6 -> 61.5 and C3 f32 229 -> 261, f64 327 ->
-# 354 us.  SPHRT_BRICK_T=b0,b1,b2 stages them (view, row, column).
-_BRICK_RAYS = None
+# Transposed CSRs (columns = rays, when they are the geometry's rays) of multi-wave grids stage
+# y in bricks of (views, rows, columns) = (8, 1, 4) rays: with the rows in voxel bricks
+# (_TROWS) a workgroup's rays are the same few pixels of many views, which such a brick puts in
+# one 128-byte line (C3 transposed adjoint f32 208 -> 193 us, f64 310 -> 304 us; (16,1,4) 194 /
+# 302, (4,2,4) 198 / 314, (1,4,8) 234 / 366, (4,4,4) 214 / 340: profiles/r05_brickt_study.jsonl).
+# Before the voxel-brick rows, detector tiles lost (C3 f32 229 -> 261 us with (1, 4, 8)).
+# SPHRT_BRICK_T=off / b0,b1,b2 overrides.
+_BRICK_RAYS = (8, 1, 4)
 
 
 def _stage_brick(nblocks, env_name='SPHRT_BRICK', brick=_BRICK):
