@@ -183,6 +183,14 @@ int sphrt_rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const doubl
 int sphrt_rays_cone_ordered(int64_t n_views, int64_t h, int64_t w, int circ, const double *frame,
                             const double *row, const double *col, const int64_t *order,
                             double *rays, int32_t *ray_id, void *stream);
+/* The same rays in tiles across views: rays is laid out (h, w / tw, n_views / tv, tv, tw, 3) —
+ * each tile holds tw neighbouring pixels of one detector row seen from tv consecutive views —
+ * and ray_id[i] = the geometry ray (v * h * w + pixel) of row i (int32; n_views * h * w < 2^31).
+ * tv must divide n_views and tw must divide w.  The Operator traces orbits in this order
+ * (raytracer._view_tiles); ray starts broadcast over it with per-dim strides (sphrt_rays). */
+int sphrt_rays_cone_tiled(int64_t n_views, int64_t h, int64_t w, int circ, const double *frame,
+                          const double *row, const double *col, int64_t tv, int64_t tw,
+                          double *rays, int32_t *ray_id, void *stream);
 
 /* ---- row index of the trace, built once (the apply kernels' work partition) ---------------- */
 /* A traced operator: the CSR above plus

@@ -82,6 +82,8 @@ _SIGNATURES = [
     ('sphrt_rays_cone', c_int, [c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     ('sphrt_rays_cone_ordered', c_int, [c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                         c_vp, c_vp]),
+    ('sphrt_rays_cone_tiled', c_int, [c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                      c_vp, c_vp, c_vp]),
     ('sphrt_csr_blocks', c_i64, [c_i64]),
     ('sphrt_csr_index_workspace_bytes', ctypes.c_size_t, [c_i64]),
     ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),

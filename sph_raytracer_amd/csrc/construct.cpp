@@ -53,6 +53,7 @@ struct Lib {
     decltype(&sphrt_last_error) last_error = nullptr;
     decltype(&sphrt_rays_cone) rays_cone = nullptr;
     decltype(&sphrt_rays_cone_ordered) rays_cone_ordered = nullptr;
+    decltype(&sphrt_rays_cone_tiled) rays_cone_tiled = nullptr;
     decltype(&sphrt_trace_workspace_bytes) trace_workspace_bytes = nullptr;
     decltype(&sphrt_scan_workspace_bytes) scan_workspace_bytes = nullptr;
     decltype(&sphrt_scan_counts) scan_counts = nullptr;
@@ -485,6 +486,7 @@ PyObject* construct_bind(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     SPHRT_SYM(last_error, "sphrt_last_error")
     SPHRT_SYM(rays_cone, "sphrt_rays_cone")
     SPHRT_SYM(rays_cone_ordered, "sphrt_rays_cone_ordered")
+    SPHRT_SYM(rays_cone_tiled, "sphrt_rays_cone_tiled")
     SPHRT_SYM(trace_workspace_bytes, "sphrt_trace_workspace_bytes")
     SPHRT_SYM(scan_workspace_bytes, "sphrt_scan_workspace_bytes")
     SPHRT_SYM(scan_counts, "sphrt_scan_counts")
@@ -542,22 +544,34 @@ PyObject* construct_cone_host(PyObject*, PyObject* const* args, Py_ssize_t nargs
     return nullptr;
 }
 
-// build_cone(geom, r_b, e_b, a_b, nr, ne, na, perm, n_cols, csr_address) ->
+// build_cone(geom, r_b, e_b, a_b, nr, ne, na, perm, tiles, n_cols, csr_address) ->
 //   (row_ptr, vox, len32, row_ray, empty_ray, blocks, loc, tab, runs, ray_id, bound_ptr, slen,
 //    xs, total, n_blocks, ray_shape) | None
 // perm: the ConeCirc wedge order of one view (raytracer._wedge_order, CPU int64) or None; used
-// for ConeCirc views only (raytracer._trace_order).  csr_address: a zeroed sphrt_csr the call
-// fills (the Operator's _lib.CSR).  Runs on the current HIP device and stream.
+// for ConeCirc views only (raytracer._trace_order).  tiles: (tv, tw) view tiles of an orbit
+// (raytracer._view_tiles; the trace order then, perm unused) or None.  csr_address: a zeroed
+// sphrt_csr the call fills (the Operator's _lib.CSR).  Runs on the current HIP device and
+// stream.
 PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-    if (nargs != 10 || !g_bound) {
+    if (nargs != 11 || !g_bound) {
         PyErr_SetString(PyExc_TypeError, "build_cone(geom, r_b, e_b, a_b, nr, ne, na, perm, "
-                                         "n_cols, csr_address) after bind");
+                                         "tiles, n_cols, csr_address) after bind");
         return nullptr;
     }
     int64_t nbins[3];
     if (!prelude_args(args, nbins)) return nullptr;
-    const int64_t n_cols = PyLong_AsLongLong(args[8]);
-    auto* c = static_cast<sphrt_csr*>(PyLong_AsVoidPtr(args[9]));
+    int64_t tv = 0, tw = 0;
+    if (args[8] != Py_None) {
+        std::vector<int64_t> t;
+        if (!int_seq(args[8], t) || t.size() != 2 || t[0] < 1 || t[1] < 1) {
+            PyErr_SetString(PyExc_ValueError, "tiles: (tv, tw) or None");
+            return nullptr;
+        }
+        tv = t[0];
+        tw = t[1];
+    }
+    const int64_t n_cols = PyLong_AsLongLong(args[9]);
+    auto* c = static_cast<sphrt_csr*>(PyLong_AsVoidPtr(args[10]));
     if (PyErr_Occurred()) return nullptr;
     struct PlanGuard {
         sphrt_plan* p = nullptr;
@@ -571,8 +585,10 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
             if (PyErr_Occurred()) return nullptr;
             Py_RETURN_NONE;
         }
+        const bool tiled = tv > 0 && P.n_views > 1;
+        if (tiled && (P.n_views % tv != 0 || P.w % tw != 0)) Py_RETURN_NONE;
         at::Tensor perm;
-        if (P.circ_kind && args[7] != Py_None) {
+        if (!tiled && P.circ_kind && args[7] != Py_None) {
             if (!THPVariable_Check(args[7])) Py_RETURN_NONE;
             perm = THPVariable_Unpack(args[7]);
             if (perm.scalar_type() != at::kLong || !perm.is_contiguous() ||
@@ -604,9 +620,13 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
               "sphrt_plan_create_external");
         sphrt_plan* const plan = guard.p;
 
-        // rays on the device (sphrt_rays_cone[_ordered]), geometry shape (..., 3)
-        std::vector<int64_t> rshape = P.shape;
-        std::vector<int64_t> full = rshape;
+        // rays on the device (sphrt_rays_cone[_ordered|_tiled]): the geometry shape (..., 3),
+        // or the view-tile layout (h, w / tw, n_views / tv, tv, tw, 3)
+        const std::vector<int64_t> rshape = P.shape;
+        std::vector<int64_t> bshape = tiled ? std::vector<int64_t>{P.h, P.w / tw, P.n_views / tv,
+                                                                   tv, tw}
+                                            : rshape;
+        std::vector<int64_t> full = bshape;
         full.push_back(3);
         const int64_t n = P.n_views * P.h * P.w;
         at::Tensor rays = at::empty(full, on_dev.dtype(at::kDouble));
@@ -614,7 +634,13 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
         const double* frame_d = (const double*)dptr(s_frame);
         const double* row_d = (const double*)dptr(s_row);
         const double* col_d = (const double*)dptr(s_col);
-        if (s_perm >= 0) {
+        if (tiled) {
+            ray_id = at::empty({n}, on_dev.dtype(at::kInt));
+            check(g_lib.rays_cone_tiled(P.n_views, P.h, P.w, P.spec.circ, frame_d, row_d, col_d,
+                                        tv, tw, rays.data_ptr<double>(),
+                                        ray_id.data_ptr<int32_t>(), stream),
+                  "sphrt_rays_cone_tiled");
+        } else if (s_perm >= 0) {
             ray_id = at::empty({n}, on_dev.dtype(at::kInt));
             check(g_lib.rays_cone_ordered(P.n_views, P.h, P.w, P.spec.circ, frame_d, row_d, col_d,
                                           (const int64_t*)dptr(s_perm), rays.data_ptr<double>(),
@@ -628,12 +654,15 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
         // _RayBatch over the staged starts (broadcast against the rays, raytracer.py:76-80)
         const at::Tensor xs_keep = staged.narrow(0, S.offs[s_xs], nbytes(P.xs))
                                        .view(at::kDouble).view(P.xs.sizes());
+        // tiles: the view starts (V, 1, 1, 3) as (1, 1, V / tv, tv, 1, 3) over the tile layout
+        const at::Tensor xs_b = tiled ? xs_keep.reshape({1, 1, P.n_views / tv, tv, 1, 3}) : xs_keep;
+        if ((int64_t)bshape.size() > SPHRT_MAX_DIMS) Py_RETURN_NONE;
         sphrt_rays rd{};
-        rd.ndim = (int32_t)rshape.size();
-        const auto xs_str = xs_keep.expand(full).strides();
+        rd.ndim = (int32_t)bshape.size();
+        const auto xs_str = xs_b.expand(full).strides();
         const auto ry_str = rays.strides();
-        for (size_t i = 0; i < rshape.size(); ++i) {
-            rd.shape[i] = rshape[i];
+        for (size_t i = 0; i < bshape.size(); ++i) {
+            rd.shape[i] = bshape[i];
             rd.xs_stride[i] = xs_str[i];
             rd.rays_stride[i] = ry_str[i];
         }

@@ -36,6 +36,8 @@ struct Binding {
     int64_t n_chan, n_vox, div, n;
     std::vector<int64_t> out_shape;  // the call's result shape (contiguous, n_chan * n or n)
     int64_t stage_bytes;             // > 0: brick-staged CSR, a stage buffer of this size per call
+    at::Tensor perm;                 // defined: the input is read as input.view(-1)[perm] (the
+                                     // adjoint of a trace in another ray order: y in trace order)
 };
 
 struct Bindings {
@@ -77,10 +79,10 @@ PyObject* py_new(PyObject*, PyObject* arg) {
 }
 
 // add(capsule, in_sizes, is_f64, device, fn_address, csr_address, n_chan, n_vox, div, n, out_shape,
-//     stage_bytes)
+//     stage_bytes[, perm])
 PyObject* py_add(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-    if (nargs != 12) {
-        PyErr_SetString(PyExc_TypeError, "add() takes 12 arguments");
+    if (nargs != 12 && nargs != 13) {
+        PyErr_SetString(PyExc_TypeError, "add() takes 12 or 13 arguments");
         return nullptr;
     }
     auto* b = static_cast<Bindings*>(PyCapsule_GetPointer(args[0], kCapsule));
@@ -98,6 +100,13 @@ PyObject* py_add(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     if (PyErr_Occurred() || !int_tuple(args[10], x.out_shape)) return nullptr;
     x.stage_bytes = PyLong_AsLongLong(args[11]);
     if (PyErr_Occurred()) return nullptr;
+    if (nargs == 13 && args[12] != Py_None) {
+        if (!THPVariable_Check(args[12])) {
+            PyErr_SetString(PyExc_TypeError, "perm: a device index tensor or None");
+            return nullptr;
+        }
+        x.perm = THPVariable_Unpack(args[12]);
+    }
     if (!x.fn || !x.csr) {
         PyErr_SetString(PyExc_ValueError, "null forward entry point or CSR");
         return nullptr;
@@ -136,6 +145,7 @@ PyObject* py_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
         if (x.dtype != dt || x.device != dev || !sizes.equals(x.in_sizes)) continue;
         at::Tensor out = at::empty(x.out_shape, d.options());
         void* stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+        const at::Tensor src = x.perm.defined() ? d.reshape({-1}).index_select(0, x.perm) : d;
         const void* csr = x.csr;
         sphrt_csr staged;
         at::Tensor stage;      // this call's brick stage (caching allocator, current stream)
@@ -146,7 +156,7 @@ PyObject* py_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
             staged.stage_bytes = x.stage_bytes;
             csr = &staged;
         }
-        const int rc = x.fn(csr, d.const_data_ptr(), x.n_chan, x.n_vox, x.div,
+        const int rc = x.fn(csr, src.const_data_ptr(), x.n_chan, x.n_vox, x.div,
                             out.mutable_data_ptr(), x.n, stream);
         // multi-wave CSRs alternate their block order from call to call (raytracer._alternate)
         if (rc == 0) {

@@ -15,19 +15,31 @@
 
 namespace sphrt {
 
+// tv > 0: rays in tiles across views — row i of the (h, w / tw, n_views / tv, tv, tw) layout
+// holds pixel (a, cb * tw + cc) of view vg * tv + vi (sphrt_rays_cone_tiled).
 __global__ __launch_bounds__(256) void cone_rays_kernel(int64_t n_views, int64_t h, int64_t w,
                                                         int circ, const double* __restrict__ frame,
                                                         const double* __restrict__ row,
                                                         const double* __restrict__ col,
                                                         double* __restrict__ rays,
                                                         const int64_t* __restrict__ order,
-                                                        int32_t* __restrict__ ray_id) {
+                                                        int32_t* __restrict__ ray_id, int64_t tv,
+                                                        int64_t tw) {
     const int64_t n = n_views * h * w;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t view = i / (h * w);
-        const int64_t slot = i - view * h * w;
-        const int64_t pix = order ? order[slot] : slot;   // the pixel this trace row holds
+        int64_t view, pix;
+        if (tv > 0) {
+            const int64_t cc = i % tw, vi = (i / tw) % tv, q = i / (tw * tv);
+            const int64_t vg = q % (n_views / tv), r = q / (n_views / tv);
+            const int64_t cb = r % (w / tw), a = r / (w / tw);
+            view = vg * tv + vi;
+            pix = a * w + cb * tw + cc;
+        } else {
+            view = i / (h * w);
+            const int64_t slot = i - view * h * w;
+            pix = order ? order[slot] : slot;            // the pixel this trace row holds
+        }
         if (ray_id) ray_id[i] = (int32_t)(view * h * w + pix);
         const int64_t a = pix / w, b = pix - a * w;
         const double* f = frame + 9 * view;          // look, right, up
@@ -64,7 +76,7 @@ using namespace sphrt;
 
 static int rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const double* frame,
                      const double* row, const double* col, double* rays, const int64_t* order,
-                     int32_t* ray_id, void* stream) {
+                     int32_t* ray_id, void* stream, int64_t tv = 0, int64_t tw = 0) {
     if (n_views < 0 || h < 0 || w < 0) return fail("bad detector shape");
     if (!frame || !row || !col || !rays) return fail("null pointer");
     const int64_t n = n_views * h * w;
@@ -73,7 +85,7 @@ static int rays_cone(int64_t n_views, int64_t h, int64_t w, int circ, const doub
     StreamGuard guard(stream);
     const int64_t blocks = (n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536;
     hipLaunchKernelGGL(cone_rays_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
-                       n_views, h, w, circ, frame, row, col, rays, order, ray_id);
+                       n_views, h, w, circ, frame, row, col, rays, order, ray_id, tv, tw);
     return check_launch("cone_rays_kernel");
 }
 
@@ -93,4 +105,17 @@ extern "C" int sphrt_rays_cone_ordered(int64_t n_views, int64_t h, int64_t w, in
                                        void* stream) {
     if (!order || !ray_id) return fail("null pointer");
     return rays_cone(n_views, h, w, circ, frame, row, col, rays, order, ray_id, stream);
+}
+
+// The same rays in tiles across views (the Operator's trace order for orbits of identical cone
+// detectors, raytracer._view_tiles): the rays array is laid out (h, w / tw, n_views / tv, tv, tw,
+// 3) — a tile is one pair (tw) of pixels of a detector row seen from tv consecutive views — and
+// ray_id[i] is the geometry ray of row i (int32).  tv must divide n_views and tw divide w.
+extern "C" int sphrt_rays_cone_tiled(int64_t n_views, int64_t h, int64_t w, int circ,
+                                     const double* frame, const double* row, const double* col,
+                                     int64_t tv, int64_t tw, double* rays, int32_t* ray_id,
+                                     void* stream) {
+    if (!ray_id) return fail("null pointer");
+    if (tv < 1 || tw < 1 || n_views % tv != 0 || w % tw != 0) return fail("bad view tile");
+    return rays_cone(n_views, h, w, circ, frame, row, col, rays, nullptr, ray_id, stream, tv, tw);
 }

@@ -24,7 +24,7 @@ import os
 import torch as tr
 
 from . import _lib
-from .geometry import ViewGeom, ViewGeomCollection
+from .geometry import ConeRectGeom, ViewGeom, ViewGeomCollection
 
 DEVICE = 'cpu'
 PDEVICE = 'cpu'
@@ -274,6 +274,21 @@ class _ConeRays:
         return rays
 
 
+def _launch_tiled(cone, dev, staging, tiles):
+    """The rays of `cone` (an orbit: n_views > 1) in view tiles (sphrt_rays_cone_tiled): an array
+    (h, w / tw, n_views / tv, tv, tw, 3) and the geometry ray of every row (int32)."""
+    tv, tw = tiles
+    packed = staging.get(cone.slot, cone.host)
+    frame_d, row_d, col_d = packed.split(cone.sizes)
+    h, w, v = cone.h, cone.w, cone.n_views
+    rays = tr.empty((h, w // tw, v // tv, tv, tw, 3), dtype=tr.float64, device=dev)
+    ray_id = tr.empty(v * h * w, dtype=tr.int32, device=dev)
+    _lib.check(_lib.load().sphrt_rays_cone_tiled(
+        v, h, w, int(cone.circ), _lib.ptr(frame_d), _lib.ptr(row_d), _lib.ptr(col_d), tv, tw,
+        _lib.ptr(rays), _lib.ptr(ray_id), _lib.stream_of(dev)), 'sphrt_rays_cone_tiled')
+    return rays, ray_id
+
+
 def _device_rays(geom, dev):
     """Cone-detector ray directions generated on the device (sphrt_rays_cone), bit-identical to
     ``geom.rays``; None for other geometries (their rays are copied from the host)."""
@@ -291,6 +306,38 @@ def _geom_rays(geom, dev):
 # 43.5 / 0.157 ms, 21.3; 4: 45.6 / 46.7 / 0.161 ms, 21.1; 5: 45.8 / 47.7 / 0.164 ms, 21.2; 8: 48.0
 # / 48.3 / 0.167 ms, 21.5 us.
 _WEDGE = 3
+
+
+# Trace order of orbits (a collection of identical cone detectors, static grids): tiles of tw
+# neighbouring pixels of one detector row seen from tv consecutive views, tiles by (row, column
+# pair, view group) — a workgroup's rays then cross the volume along one family of nearby lines
+# from many directions, whose granules the neighbouring workgroups share in L2.  Forward kernel
+# (f32 / f64 us, profiles/r05_vtile_*.jsonl) C2 6.33 / 9.6 -> 5.92 / 8.45 with (50, 2), C3 204.1 /
+# 333.3 -> 195.1 / 314.1 with (64, 2), C5 (against the wedge order) 27.7 / 44.2 -> 26.8 / 37.0
+# with (64, 2); the transposed adjoints C2 6.2 / 8.6 -> 5.9 / 8.4, C3 192 / 303 -> 187 / 287, C5
+# 24.7 / 40.4 -> 24.7 / 35.3.  tv: the largest divisor of the view count in [8, 64]; tw = 2 (1
+# for an odd width).  Dynamic grids keep the per-view orders (view i <-> time slice i pairs trace
+# rows with slices by position).  SPHRT_RAY_ORDER=natural / views:G / tile:h,w (studies) keep
+# other orders, vtile:tv,1,tw forces a tile.
+_VIEW_TILE_MAX, _VIEW_TILE_MIN = 64, 8
+
+
+def _view_tiles(shape, dynamic):
+    """(tv, tw) for an orbit of `shape` (views, rows, columns), or None."""
+    mode = os.environ.get('SPHRT_RAY_ORDER', 'auto')
+    if dynamic or len(shape) != 3 or shape[0] < 2:
+        return None
+    v, h, w = shape
+    if mode.startswith('vtile:'):
+        tv, th, tw = (int(x) for x in mode[6:].split(','))
+        return (tv, tw) if th == 1 and v % tv == 0 and w % tw == 0 else None
+    if mode != 'auto':
+        return None
+    tv = next((d for d in range(min(v, _VIEW_TILE_MAX), _VIEW_TILE_MIN - 1, -1) if v % d == 0),
+              None)
+    if tv is None:
+        return None
+    return tv, (2 if w % 2 == 0 else 1)
 
 
 def _trace_order(geom, rays):
@@ -312,6 +359,9 @@ def _trace_order(geom, rays):
         return _tile_order(shape[-2], shape[-1], th, tw)
     if mode.startswith('views:') and len(shape) == 3:          # A/B studies: rows of G views
         return _view_row_order(shape[0], shape[1], shape[2], int(mode[6:]))
+    if mode.startswith('vtile:') and len(shape) == 3:          # tiles of several rows (studies)
+        return _view_tile_order(shape[0], shape[1], shape[2],
+                                *(int(v) for v in mode[6:].split(',')))
     from .geometry import ConeCircGeom
     geoms = getattr(geom, 'geoms', [geom])
     if not geoms or any(type(g) is not ConeCircGeom for g in geoms):
@@ -331,6 +381,20 @@ def _view_row_order(v, h, w, g):
     r = tr.arange(h).repeat_interleave(w).repeat(v)
     c = tr.arange(w).repeat(v * h)
     key = (((vi // g) * h + r) * g + vi % g) * w + c
+    return tr.argsort(key)
+
+
+@functools.lru_cache(maxsize=16)
+def _view_tile_order(v, h, w, tv, th, tw):
+    """Order of all (v, h, w) pixels in tiles of tv views x th rows x tw columns (studies only):
+    tiles by (row band, column band, view group), inside a tile view, row, column — a
+    workgroup's rays are one pixel patch seen from neighbouring views."""
+    vi = tr.arange(v).repeat_interleave(h * w)
+    r = tr.arange(h).repeat_interleave(w).repeat(v)
+    c = tr.arange(w).repeat(v * h)
+    ncb, nvg = -(-w // tw), -(-v // tv)
+    key = ((((r // th) * ncb + c // tw) * nvg + vi // tv) * tv + vi % tv) * (th * tw) + \
+        (r % th) * tw + c % tw
     return tr.argsort(key)
 
 
@@ -951,10 +1015,12 @@ class Operator:
         stg = _Staging()
         self._plan = _Plan(self.grid, dev, staging=stg)
         cone = _ConeRays.of(self.geom)
-        perm, s_perm = None, None
+        perm, s_perm, tiles = None, None, None
         if cone is not None:
             cone.stage(stg)
-            perm = _trace_order(self.geom, tr.empty(cone.shape + (3,), device='meta'))
+            tiles = _view_tiles(cone.shape, self.grid.dynamic) if cone.n_views > 1 else None
+            if tiles is None:
+                perm = _trace_order(self.geom, tr.empty(cone.shape + (3,), device='meta'))
             if perm is not None and perm.numel() == cone.h * cone.w:   # per view: staged too
                 s_perm = stg.add(perm)
         xs_h, st_h = _RayBatch.host_starts(self.grid, self.geom.ray_starts)
@@ -962,7 +1028,12 @@ class Operator:
         stg.upload(dev)
         self._plan.attach(stg)
         ray_id = None
-        if s_perm is not None:         # trace in wedges, generated in that order
+        xs_d, st_d = stg.get(s_xs, xs_h), stg.get(s_st, st_h)
+        if tiles is not None:          # view tiles: the starts broadcast over the tiled layout
+            rays, ray_id = _launch_tiled(cone, dev, stg, tiles)
+            tshape = (1, 1, cone.n_views // tiles[0], tiles[0], 1, 3)
+            xs_h, xs_d = xs_h.reshape(tshape), xs_d.reshape(tshape)
+        elif s_perm is not None:       # trace in wedges, generated in that order
             rays, ray_id = cone.launch(dev, stg, order=stg.get(s_perm, perm))
             perm = None
         elif cone is not None:
@@ -970,7 +1041,6 @@ class Operator:
         else:
             rays = self.geom.rays
             perm = _trace_order(self.geom, rays)
-        xs_d, st_d = stg.get(s_xs, xs_h), stg.get(s_st, st_h)
         if perm is not None and rays.dim() == 4 and perm.numel() > math.prod(rays.shape[-3:-1]):
             # an order across views (studies): starts and start voxels follow their rays
             pd = perm.to(dev, non_blocking=True)
@@ -983,7 +1053,7 @@ class Operator:
         elif perm is not None:         # trace in wedges; rows report their geometry ray
             rays, ray_id = _permute_rays(rays, perm.to(dev, non_blocking=True))
         batch = _RayBatch(self.grid, xs_h, rays, dev, staged=(xs_d, st_d))
-        self._ray_shape = batch.shape
+        self._ray_shape = cone.shape if tiles is not None else batch.shape
         n = batch.n
         stream = _lib.stream_of(dev)
         row_ptr, vox, seg_len, total, staging = _trace_csr(lib, self._plan, batch, dev, stream,
@@ -1002,13 +1072,13 @@ class Operator:
                 or os.environ.get('SPHRT_CONSTRUCT', 'native') == 'python'):
             return False
         shape = tuple(self.geom.shape)
-        perm = None
-        if len(shape) in (2, 3) and shape[-1] > _WEDGE:     # _trace_order (ConeCirc views)
-            perm = _wedge_order(shape[-2], shape[-1])
         g = self.grid
+        perm, tiles = None, _view_tiles(shape, g.dynamic)
+        if tiles is None and len(shape) in (2, 3) and shape[-1] > _WEDGE:   # _trace_order
+            perm = _wedge_order(shape[-2], shape[-1])                       # (ConeCirc views)
         c = _lib.CSR()
         res = fc.build_cone(self.geom, g.r_b, g.e_b, g.a_b, g.shape.r, g.shape.e, g.shape.a, perm,
-                            math.prod(g.shape[-3:]), ctypes.addressof(c))
+                            tiles, math.prod(g.shape[-3:]), ctypes.addressof(c))
         if res is None:
             return False
         (row_ptr, vox, len32, row_ray, empty_ray, blocks, loc, tab, runs, ray_id, bound_ptr, slen,
@@ -1323,6 +1393,9 @@ class Operator:
         del ws
         if rows is not None:
             del vox_pos, pos, v
+        geom_cols = self._tcols_geom()
+        if geom_cols:                    # columns: the rows' geometry rays instead of trace rows
+            t_ray[:total] = csr['ray_id'].index_select(0, t_ray[:total])
         nblocks = lib.sphrt_csr_blocks(total)
         vox_list = tr.empty(n_vox, dtype=tr.int32, device=dev)
         empty_vox = tr.empty(n_vox + 1, dtype=tr.int32, device=dev)
@@ -1342,7 +1415,7 @@ class Operator:
         c.empty_ray = empty_vox.data_ptr()
         c.n_cols = csr['n']
         # (columns are trace rows: detector tiles only when they are the geometry's rays)
-        shape3 = self._ray_shape3() if csr['ray_id'] is None else None
+        shape3 = self._ray_shape3() if csr['ray_id'] is None or geom_cols else None
         _set_stage(c, shape3, _stage_brick(nblocks, 'SPHRT_BRICK_T', _BRICK_RAYS)
                    if shape3 else None)
         loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
@@ -1384,11 +1457,32 @@ class Operator:
         with tr.cuda.device(self._cdev):
             return self._apply_adjoint_on(y, dshape, ddtype, ddevice, trace_order)
 
+    def _tcols_geom(self):
+        """Whether the transposed CSRs of a reordered trace (wedges, view tiles) take their
+        columns in geometry ray order — their t_ray mapped through ray_id once at transpose
+        time: the adjoint reads y as given (no gather per call) and y is brick-staged in
+        detector tiles — or in trace-row order (y gathered into trace order per call, or written
+        so by the retrieval's residual).  Measured (op.T per step, us; profiles/r05_tcols_*):
+        ConeRect orbits take geometry columns (C2 11.7 -> 7.2, C3 214.5 -> 187.2), ConeCirc
+        orbits keep trace rows (C5 41.4 against 44.2; its kernel 25.1 / 35.6 us f32 / f64 against
+        28.3-30.8 / 39.7-44.0 with geometry columns and any ray brick).  SPHRT_TCOLS=geom / trace
+        overrides."""
+        csr = self._csr
+        if csr is None or csr['ray_id'] is None:
+            return False
+        env = os.environ.get('SPHRT_TCOLS', 'auto')
+        if env != 'auto':
+            return env == 'geom'
+        geoms = getattr(self.geom, 'geoms', [self.geom])
+        return bool(geoms) and all(type(g) is ConeRectGeom for g in geoms)
+
     def _adjoint_trace_order(self):
         """The row -> geometry ray map (int32, device) when the adjoint takes its input in
-        trace order (static, transposed adjoint, a reordered trace), else None."""
+        trace order (static, transposed adjoint, a reordered trace with trace-row columns),
+        else None."""
         csr = self._csr
-        if self.grid.dynamic or self.adjoint_mode != 'transpose' or csr is None:
+        if (self.grid.dynamic or self.adjoint_mode != 'transpose' or csr is None
+                or self._tcols_geom()):
             return None
         return csr['ray_id']
 
@@ -1407,7 +1501,8 @@ class Operator:
         if self.adjoint_mode == 'transpose' and (div == 0 or paired is not None):
             cdt = ddtype if ddtype in (tr.float32, tr.float64) else tr.float32
             yv = yv.to(cdt)
-            if csr['ray_id'] is not None and not trace_order:   # its columns are trace rows
+            if csr['ray_id'] is not None and not trace_order and not self._tcols_geom():
+                # (its columns are trace rows)
                 yv = yv.view(-1, n).index_select(1, self._ray_id_long()).reshape(-1)
             if paired is not None:      # columns of the flattened (T, vol) density
                 if 'transposed' not in paired:
@@ -1467,17 +1562,16 @@ class Operator:
     def _bind_adjoint(self, y, res):
         """Register T's steady-state binding for y's shape/dtype when the general path did no
         more than one transposed-CSR forward: y contiguous on the compute device, float32/64, the
-        result left there in y's dtype, no ray permutation (a trace in geometry order), no
-        staged transpose."""
+        result left there in y's dtype.  A trace in another ray order (wedges, view tiles) reads
+        y through its ray ids (index_select in the same call); a brick-staged transpose gets its
+        stage buffer per call, as in _call_forward."""
         csr, dev = self._csr, self._cdev
         if not (type(y) is tr.Tensor and y.device == dev and res.device == dev
                 and y.dtype in (tr.float32, tr.float64) and res.dtype == y.dtype
                 and y.is_contiguous() and self.adjoint_mode == 'transpose'
-                and csr is not None and csr['ray_id'] is None and y.numel() == csr['n']):
+                and csr is not None and y.numel() == csr['n']):
             return
         tdesc = self._transposed()['desc']
-        if _stage_bytes(tdesc, 1, y.element_size()):
-            return
         fast = _lib.load_fast()
         if fast is None:
             return
@@ -1489,7 +1583,8 @@ class Operator:
         vol = math.prod(self.grid.shape[-3:])
         fast.add(self._fastc_T, tuple(y.shape), y.dtype == tr.float64, dev.index,
                  _lib.address(fn), ctypes.addressof(tdesc), 1, csr['n'], 0, vol,
-                 tuple(res.shape), 0)
+                 tuple(res.shape), _stage_bytes(tdesc, 1, y.element_size()),
+                 None if self._tcols_geom() else csr['ray_id'])
 
     # -- compatibility views -----------------------------------------------------------------------
     def _padded(self):

@@ -114,11 +114,13 @@ def test_c3_full_trace_vs_oracle(c3):
 
 def test_c3_full_forward_and_adjoint_vs_oracle(c3, gpu):
     """C3 forward (float64, float32) and transposed adjoint (float64, float32) over every ray /
-    voxel against the oracle's segments, through the product configuration: (4,2,4) brick
-    staging, run records, alternating block order (each call below flips it)."""
+    voxel against the oracle's segments, through the product configuration: the orbit traced in
+    view tiles, (4,2,4) brick staging, alternating block order (each call below flips it), the
+    transposed rows in voxel bricks (its y in trace order: the views interleaved already)."""
     grid, geom, op, ref, n_vox = c3
     desc = op._csr['desc']
-    assert tuple(desc.stage_brick) == (4, 2, 4) and desc.runs and desc.n_blocks > 256 * 6
+    assert tuple(desc.stage_brick) == (4, 2, 4) and desc.n_blocks > 256 * 6
+    assert op._csr['ray_id'] is not None
     ptr, vox, seg = _flat(ref)
     ray = np.repeat(np.arange(len(ptr) - 1), np.diff(ptr))
     g = tr.Generator().manual_seed(11)
@@ -230,7 +232,7 @@ def test_c2_full_trace_vs_oracle(c2):
     """All 250 k rays of the headline config (BASELINE configs[1]): voxel sequences exact,
     lengths 1e-12 — the one-wave path (bitmap granule tables, no brick staging)."""
     grid, geom, op, ref, _ = c2
-    assert op._csr['n'] == 50 * 50 * 100 and op._csr['ray_id'] is None
+    assert op._csr['n'] == 50 * 50 * 100 and op._csr['ray_id'] is not None   # (view tiles)
     _compare_all(ref, _gpu_views(op, 50), 5.1, 'C2')
 
 

@@ -193,6 +193,32 @@ def test_device_rays_in_trace_order(gpu):
             assert tr.equal(ray_id.cpu(), want)
 
 
+def test_device_rays_in_view_tiles(gpu):
+    """sphrt_rays_cone_tiled: the rays in the (h, w / tw, V / tv, tv, tw) view-tile layout equal
+    the geometry's rays rearranged that way, bit for bit, and every row's ray id is its geometry
+    ray (the Operator's trace order for orbits, raytracer._view_tiles)."""
+    import torch as tr
+    from sph_raytracer_amd import ConeCircGeom, ConeRectGeom
+    from sph_raytracer_amd.raytracer import _ConeRays, _Staging, _launch_tiled
+    th = tr.linspace(0, 2 * tr.pi, 6)
+    cases = [
+        sum(ConeCircGeom((30, 24), pos=(5 * tr.cos(a), 5 * tr.sin(a), 1), fov=(0, 45)) for a in th),
+        sum(ConeRectGeom((12, 20), pos=(5 * tr.cos(a), 5 * tr.sin(a), 1)) for a in th),
+    ]
+    for g in cases:
+        cone = _ConeRays.of(g)
+        v, h, w = cone.n_views, cone.h, cone.w
+        stg = _Staging()
+        cone.stage(stg)
+        stg.upload(gpu)
+        for tv, tw in ((6, 2), (3, 4), (2, 1), (1, 2)):
+            rays, ray_id = _launch_tiled(cone, gpu, stg, (tv, tw))
+            want = g.rays.reshape(v // tv, tv, h, w // tw, tw, 3).permute(2, 3, 0, 1, 4, 5)
+            assert tr.equal(rays.cpu(), want), (tv, tw)
+            idx = tr.arange(v * h * w).reshape(v // tv, tv, h, w // tw, tw).permute(2, 3, 0, 1, 4)
+            assert tr.equal(ray_id.cpu(), idx.reshape(-1).to(tr.int32))
+
+
 def _csr(op):
     c = op._csr
     return (c['row_ptr'].cpu(), c['vox'][:c['total']].cpu(), c['len'][:c['total']].cpu())
