@@ -76,6 +76,7 @@ PyObject* g_coll = nullptr;   // geometry.ViewGeomCollection
 // raytracer.py constants this sequence follows
 constexpr int64_t kSingleWaveBlocks = 256 * 6;          // _SINGLE_WAVE_BLOCKS
 constexpr int kBrick[3] = {4, 2, 4};                     // _BRICK
+constexpr int64_t kL2Bytes = int64_t(4) << 20;           // _L2_BYTES
 constexpr int64_t kTabWide = SPHRT_TAB_WIDE;
 constexpr int64_t kRunFields = SPHRT_RUN_FIELDS;
 constexpr int64_t kBlockFields = SPHRT_BLOCK_FIELDS;
@@ -725,7 +726,7 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
         c->n_segments = total;
         c->n_blocks = nblocks;
         c->n_cols = n_cols;
-        if (nblocks > kSingleWaveBlocks) {           // _stage_brick / _set_stage
+        if (nblocks > kSingleWaveBlocks && 4 * n_cols > kL2Bytes) {   // _stage_brick, _set_stage
             int64_t cols = 1;
             for (int i = 0; i < 3; ++i) cols *= (nbins[i] + kBrick[i] - 1) / kBrick[i] * kBrick[i];
             if (cols < (int64_t(1) << 31) - 1) {

@@ -702,19 +702,27 @@ def _voxel_rows_cached(shape3, brick, dev):
 _BRICK_RAYS = (8, 1, 4)
 
 
-def _stage_brick(nblocks, env_name='SPHRT_BRICK', brick=_BRICK):
+_L2_BYTES = 4 << 20     # one XCD's L2
+
+
+def _stage_brick(nblocks, env_name='SPHRT_BRICK', brick=_BRICK, n_cols=None):
     """Brick of the density staging for a trace CSR of `nblocks` workgroup blocks (sphrt.h
     stage_*), or None.  It pays when the forward runs in several waves of workgroups, whose
-    granule DMA is bound by L2 requests (C3 f32 forward 267 -> 241 us, C5 41.9 -> 35.2 us, pack
-    included); a grid that is resident at once (C2: 1473 blocks) is latency-bound and would only
-    pay the packing pass.  The environment variable `env_name` (SPHRT_BRICK for the trace CSR,
-    SPHRT_BRICK_T for the transposed one, whose columns are rays) set to `off` disables it, to
-    `b0,b1,b2` forces that brick."""
+    granule DMA is bound by L2 requests, over an array larger than one XCD's L2 (n_cols float32
+    columns; None: not checked): C3 (8.4 MB) f32 forward 267 -> 241 us in round 1, 206.7 -> 196.1
+    us with the view tiles (f64 311 -> 318); a grid that is resident at once (C2: 1473 blocks) is
+    latency-bound and would only pay the packing pass, and with the view tiles an array that fits
+    the L2 loses too (C5, 1 MB: f32 24.9 -> 26.8 us, f64 33.8 -> 36.7 us with (4,2,4) bricks;
+    profiles/r05_brick_tiles_sweep.jsonl).  The environment variable `env_name` (SPHRT_BRICK for
+    the trace CSR, SPHRT_BRICK_T for the transposed one, whose columns are rays) set to `off`
+    disables it, to `b0,b1,b2` forces that brick."""
     env = os.environ.get(env_name, 'auto')
     if env == 'off':
         return None
     if env != 'auto':
         return tuple(int(v) for v in env.split(','))
+    if n_cols is not None and 4 * n_cols <= _L2_BYTES:
+        return None
     return brick if brick is not None and nblocks > _SINGLE_WAVE_BLOCKS else None
 
 
@@ -1145,7 +1153,7 @@ class Operator:
         c.n_rays, c.n_segments, c.n_blocks = n, total, nblocks
         c.n_cols = math.prod(self.grid.shape[-3:])
         shape3 = tuple(int(v) for v in self.grid.shape[-3:])
-        _set_stage(c, shape3, _stage_brick(nblocks))
+        _set_stage(c, shape3, _stage_brick(nblocks, n_cols=c.n_cols))
         staged = staging is not None and os.environ.get('SPHRT_TABLE_STAGED', '1') != '0'
         if staged:
             free = tr.cuda.mem_get_info(dev)[0]

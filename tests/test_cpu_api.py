@@ -456,6 +456,9 @@ def test_brick_stage_fields(monkeypatch):
     from sph_raytracer_amd import raytracer as rt
     monkeypatch.delenv('SPHRT_BRICK', raising=False)
     assert rt._stage_brick(1536) is None and rt._stage_brick(1537) == rt._BRICK
+    # arrays that fit one XCD's L2 (float32 columns) keep the natural layout
+    assert rt._stage_brick(10 ** 6, n_cols=64 ** 3) is None
+    assert rt._stage_brick(10 ** 6, n_cols=128 ** 3) == rt._BRICK
     monkeypatch.delenv('SPHRT_BRICK_T', raising=False)
     assert rt._stage_brick(1536, 'SPHRT_BRICK_T', rt._BRICK_RAYS) is None
     assert rt._stage_brick(10 ** 6, 'SPHRT_BRICK_T', rt._BRICK_RAYS) == rt._BRICK_RAYS == (8, 1, 4)

@@ -262,9 +262,11 @@ def test_c5_full_trace_vs_oracle(c5):
 
 
 def test_c5_full_forward_and_adjoint_vs_oracle(c5, gpu):
-    """C5 forward (float64 half tables, brick staging, alternating block order) and adjoint (the
-    transposed CSR of a trace-ordered CSR) over every ray / voxel."""
+    """C5 forward (float64 half tables, view tiles, alternating block order; no brick staging:
+    the 64^3 density fits one XCD's L2) and adjoint (the transposed CSR of a trace-ordered CSR)
+    over every ray / voxel."""
     grid, geom, op, ref, n_vox = c5
     desc = op._csr['desc']
-    assert tuple(desc.stage_brick) == (4, 2, 4) and desc.n_blocks > 256 * 6
+    assert tuple(desc.stage_brick) == (0, 0, 0) and desc.n_blocks > 256 * 6
+    assert op._csr['ray_id'] is not None
     _static_forward_adjoint(grid, geom, op, ref, n_vox, gpu, 51, 'C5')
