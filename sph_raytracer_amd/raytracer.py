@@ -340,7 +340,7 @@ def _view_tiles(shape, dynamic):
     return tv, (2 if w % 2 == 0 else 1)
 
 
-def _trace_order(geom, rays):
+def _trace_order(geom, rays, dynamic=False):
     """Per-view order the trace visits a ConeCirc detector's pixels in, or None (geometry order).
 
     ConeCirc pixels are (radius, azimuth) with the azimuth fastest: ~36 consecutive rays (one
@@ -349,11 +349,15 @@ def _trace_order(geom, rays):
     1536 -> 1024, forward f32 33.2 -> 29.5 us, f64 52.7 -> 45.8 us, transposed adjoint f64 53.4
     -> 43.5 us (ConeRect rows are already compact: strips beat every tiling measured).  Only the order of the CSR's rows changes: every
     row reports its geometry ray (sphrt_csr_index ray_ids), outputs stay in geometry order.
-    SPHRT_RAY_ORDER=natural keeps the geometry order."""
+    SPHRT_RAY_ORDER=natural keeps the geometry order.  The study orders across views (views:,
+    vtile:) apply to static grids only (a dynamic grid pairs trace rows with time slices by
+    position)."""
     mode = os.environ.get('SPHRT_RAY_ORDER', 'auto')
     if mode == 'natural':
         return None
     shape = tuple(rays.shape[:-1])
+    if dynamic and (mode.startswith('views:') or mode.startswith('vtile:')):
+        return None
     if mode.startswith('tile:') and len(shape) in (2, 3):     # A/B studies: detector tiles
         th, tw = (int(v) for v in mode[5:].split(','))
         return _tile_order(shape[-2], shape[-1], th, tw)
@@ -1028,7 +1032,8 @@ class Operator:
             cone.stage(stg)
             tiles = _view_tiles(cone.shape, self.grid.dynamic) if cone.n_views > 1 else None
             if tiles is None:
-                perm = _trace_order(self.geom, tr.empty(cone.shape + (3,), device='meta'))
+                perm = _trace_order(self.geom, tr.empty(cone.shape + (3,), device='meta'),
+                                    self.grid.dynamic)
             if perm is not None and perm.numel() == cone.h * cone.w:   # per view: staged too
                 s_perm = stg.add(perm)
         xs_h, st_h = _RayBatch.host_starts(self.grid, self.geom.ray_starts)
@@ -1048,7 +1053,7 @@ class Operator:
             rays = cone.launch(dev, stg)
         else:
             rays = self.geom.rays
-            perm = _trace_order(self.geom, rays)
+            perm = _trace_order(self.geom, rays, self.grid.dynamic)
         if perm is not None and rays.dim() == 4 and perm.numel() > math.prod(rays.shape[-3:-1]):
             # an order across views (studies): starts and start voxels follow their rays
             pd = perm.to(dev, non_blocking=True)
