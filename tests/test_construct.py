@@ -244,3 +244,34 @@ def test_view_tiles_match_geometry_order(gpu, monkeypatch, kind):
         assert float((fa - fb).abs().max()) <= tol * float(fb.abs().max())
         ta, tb = a.T(y), b.T(y)
         assert float((ta - tb).abs().max()) <= tol * float(tb.abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('kind', ['rect', 'circ'])
+def test_transposed_columns_geometry_or_trace_order(gpu, monkeypatch, kind):
+    """A reordered trace's transposed CSR takes its columns in geometry order (ConeRect orbits:
+    y read as given, brick-staged) or in trace-row order (ConeCirc: y gathered per call); either
+    choice (SPHRT_TCOLS=geom / trace) gives the same adjoint up to summation order, through the
+    general and the steady-state paths, float64 and float32."""
+    grid = SphericalGrid(shape=(40, 36, 44))
+    geom = _orbit(kind, 16, (30, 40), fov=(45, 45) if kind == 'rect' else (0, 45))
+    g = torch.Generator(device='cpu').manual_seed(4)
+    ys = [torch.rand(tuple(geom.shape), generator=g, dtype=dt).to(gpu)
+          for dt in (torch.float64, torch.float32)]
+    out = {}
+    for mode in ('auto', 'geom', 'trace'):
+        monkeypatch.setenv('SPHRT_TCOLS', mode)
+        op = Operator(grid, geom, device=gpu)
+        assert op._csr['ray_id'] is not None
+        want_geom = mode == 'geom' or (mode == 'auto' and kind == 'rect')
+        assert op._tcols_geom() == want_geom
+        res = []
+        for y in ys:
+            a0, a1 = op.T(y), op.T(y)            # general path (binds), steady-state path
+            assert torch.equal(a0, a1)
+            res.append(a0)
+        out[mode] = res
+    for mode in ('geom', 'trace'):
+        for a, b in zip(out[mode], out['auto']):
+            tol = 1e-13 if a.dtype == torch.float64 else 1e-6
+            assert float((a - b).abs().max()) <= tol * float(b.abs().max())
