@@ -128,6 +128,9 @@ GPU_CASES = {
                                       _orbit('rect', 40, (128, 128))),
     'single_view': lambda: (SphericalGrid(shape=(30, 40, 50)),
                             ConeRectGeom((64, 48), pos=(3, 1, 0.5), fov=(40, 30))),
+    # view tiles (9, 1): an odd view count and an odd detector width
+    'odd_tiles': lambda: (SphericalGrid(shape=(24, 20, 28)), _orbit('rect', 9, (17, 41))),
+    'few_views': lambda: (SphericalGrid(shape=(24, 20, 28)), _orbit('circ', 7, (20, 30))),
 }
 
 

@@ -536,3 +536,25 @@ def test_split_adam_accepts_torch_defaults():
     assert opt.param_groups[0]['weight_decay'] == 0 and retrieval._number(0)
     assert retrieval._split_adam(opt, c) is None          # CPU tensor: torch's single-tensor Adam
     assert not retrieval._number(True) and not retrieval._number(torch.tensor(0.1))
+
+
+def test_view_tiles_rule(monkeypatch):
+    """raytracer._view_tiles: orbits of static grids in tiles of tv views (the largest divisor of
+    the view count in [8, 64]) x tw pixels of a row (2, or 1 for an odd width); none for single
+    views, too few views, dynamic grids, or SPHRT_RAY_ORDER other than auto / vtile:tv,1,tw."""
+    from sph_raytracer_amd import raytracer as rt
+    monkeypatch.delenv('SPHRT_RAY_ORDER', raising=False)
+    assert rt._view_tiles((50, 50, 100), False) == (50, 2)      # C2
+    assert rt._view_tiles((128, 128, 256), False) == (64, 2)    # C3
+    assert rt._view_tiles((64, 100, 50), False) == (64, 2)      # C5
+    assert rt._view_tiles((9, 17, 41), False) == (9, 1)
+    assert rt._view_tiles((96, 8, 8), False) == (48, 2)
+    assert rt._view_tiles((7, 20, 30), False) is None
+    assert rt._view_tiles((50, 100, 50), True) is None          # C4: dynamic
+    assert rt._view_tiles((50, 100), False) is None             # a single view
+    monkeypatch.setenv('SPHRT_RAY_ORDER', 'natural')
+    assert rt._view_tiles((50, 50, 100), False) is None
+    monkeypatch.setenv('SPHRT_RAY_ORDER', 'vtile:10,1,4')
+    assert rt._view_tiles((50, 50, 100), False) == (10, 4)
+    monkeypatch.setenv('SPHRT_RAY_ORDER', 'vtile:4,2,8')       # several rows: the study path
+    assert rt._view_tiles((50, 50, 100), False) is None
