@@ -215,14 +215,22 @@ class _Ranks:
         self.dist.all_reduce(tt, op=self.dist.ReduceOp.MAX)
         return tt.tolist()
 
+    def close(self):
+        """The closing bracket of a timed region: device sync, then the barrier (with one rank the
+        barrier is nothing, and a second idle synchronize would add ~2 µs to every region:
+        profiles/r05_region_cost.json)."""
+        torch.cuda.synchronize(self.dev)
+        if self.dist is not None:
+            self.dist.barrier()
+            torch.cuda.synchronize(self.dev)
+
     def timed(self, fn, reps):
         """Run fn() `reps` times between barrier + sync brackets -> max seconds over ranks."""
         self.barrier()
         t0 = time.perf_counter()
         for _ in range(reps):
             fn()
-        torch.cuda.synchronize(self.dev)
-        self.barrier()
+        self.close()
         return self.max_over_ranks([time.perf_counter() - t0])[0]
 
 
@@ -630,8 +638,7 @@ def main():
     for _ in range(args.steps):
         step()
     ev1.record()
-    torch.cuda.synchronize(dev)
-    barrier()
+    rk.close()
     dt = time.perf_counter() - t0
     k_ms_timed = ev0.elapsed_time(ev1) / args.steps
     gather = None
@@ -724,8 +731,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(adj_steps):
             op.T(y_adj)
-        torch.cuda.synchronize(dev)
-        barrier()
+        rk.close()
         t_adj = (time.perf_counter() - t0) / adj_steps
         if dist is not None:
             t_adj, = max_over_ranks([t_adj])
