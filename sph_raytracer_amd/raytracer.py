@@ -1255,6 +1255,15 @@ class Operator:
         sd.stage, sd.stage_bytes, sd.stage_packed = buf.data_ptr(), need, 0
         return sd, buf
 
+    def _loop_descriptor(self, dtype):
+        """A copy of the trace's forward descriptor for a loop's own launches (_forward_staged),
+        or None (no trace, a dynamic grid, or a brick-staged CSR: _stage_for_loop)."""
+        desc = self._csr['desc'] if self._csr is not None else None
+        if desc is None or self.grid.dynamic or _stage_bytes(desc, 1, 1):
+            return None
+        self._lengths(dtype)            # (the float64 lengths moved into the CSR first)
+        return _lib.CSR.from_buffer_copy(desc)
+
     def _forward_staged(self, d, out, sd):
         """Static single-channel forward of d (contiguous, on the compute device) into the flat
         out on the current stream, through a _stage_for_loop descriptor (its stage_packed says
@@ -1265,6 +1274,48 @@ class Operator:
             _lib.check(fn(sd, _lib.ptr(d), 1, math.prod(self.grid.shape[-3:]), 0, _lib.ptr(out),
                           self._csr['n'], _lib.stream_of(self._cdev)), 'sphrt_forward')
             _alternate(sd)
+
+    def _trace_position_rows(self, sd):
+        """Point a _stage_for_loop descriptor's row -> ray and empty-ray lists at trace
+        positions instead of geometry rays: its forward then writes the integral of trace
+        position j to out[j] — the transposed adjoint's column order (_adjoint_trace_order), so
+        the loop's residual streams f(d) and the measurements (pre-permuted once) instead of
+        gathering both through the ray map, and the forward's row closes store to consecutive
+        addresses.  Run records are rebuilt in trace positions (a block's rows are then one run
+        but for empty rays) or dropped (list loads).  -> the list tensors (keep them alive with
+        the descriptor), or None without a reordered trace."""
+        csr = self._csr
+        if csr is None or csr['ray_id'] is None:
+            return None
+        if 'trace_rows' not in csr:          # (once per trace)
+            n, rid = csr['n'], self._ray_id_long()
+            inv = tr.empty(n, dtype=tr.int32, device=rid.device)
+            inv[rid] = tr.arange(n, dtype=tr.int32, device=rid.device)
+            # (entries past the lists' lengths are never used; clamped so the gather stays in
+            # range)
+            rows = inv[csr['row_ray'].long().clamp_(0, n - 1)]
+            empty = inv[csr['empty_ray'].long().clamp_(0, n - 1)]
+            # run records in trace positions, where a block's rows are consecutive but for
+            # empty rays (_local_tables' rule: grids of more than one wave of workgroups)
+            runs = None
+            mode = os.environ.get('SPHRT_RUNS', 'auto')
+            if (mode == 'on' or (mode == 'auto' and csr['nblocks'] > _SINGLE_WAVE_BLOCKS)) \
+                    and n < 2 ** 31:
+                lib = _lib.load()
+                tmp = _lib.CSR.from_buffer_copy(sd)
+                tmp.row_ray, tmp.empty_ray = rows.data_ptr(), empty.data_ptr()
+                runs = tr.empty(_lib.RUN_FIELDS * csr['nblocks'], dtype=tr.int32,
+                                device=rid.device)
+                over = tr.empty(1, dtype=tr.int64, device=rid.device)
+                _lib.check(lib.sphrt_csr_runs(tmp, _lib.ptr(runs), _lib.ptr(over),
+                                              _lib.stream_of(rid.device)), 'sphrt_csr_runs')
+                if over.item():
+                    runs = None
+            csr['trace_rows'] = (rows, empty, runs)
+        rows, empty, runs = csr['trace_rows']
+        sd.row_ray, sd.empty_ray = rows.data_ptr(), empty.data_ptr()
+        sd.runs = runs.data_ptr() if runs is not None else None
+        return rows, empty, runs
 
     def _lengths(self, dtype):
         """Segment lengths as streamed by the forward kernel: the float64 trace, or (float32

@@ -198,10 +198,23 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar, 
     staged = f._stage_for_loop(coeffs.dtype) if step is not None else None
     if staged is not None and f._csr['n'] != n_meas:
         staged = None
-    yhat_buf = t.empty(n_meas, dtype=coeffs.dtype, device=coeffs.device) if staged else None
     order = f._adjoint_trace_order()
     if order is not None and order.numel() != n_meas:
         order = None
+    # the loop's own forward descriptor (a copy of the trace's): the staged one above, and with a
+    # reordered trace — whose adjoint takes its input in trace order — one that writes f(d) in
+    # that order too; the measurements are then permuted once and the residual kernel streams
+    # both (the same values in the same order: bitwise the same iterates)
+    loop_desc = staged[0] if staged is not None else None
+    y_res, res_order, keep_rows = yd, order, None
+    if order is not None:
+        sd = loop_desc if loop_desc is not None else f._loop_descriptor(coeffs.dtype)
+        keep_rows = f._trace_position_rows(sd) if sd is not None else None
+        if keep_rows is not None:
+            loop_desc = sd
+            y_res, res_order = yd.reshape(-1).index_select(0, f._ray_id_long()), None
+    yhat_buf = t.empty(n_meas, dtype=coeffs.dtype, device=coeffs.device) \
+        if loop_desc is not None else None
     # every iteration's loss as the workgroup partial sums of its fused kernel, one row per
     # iteration, summed once after the loop (no reduction launch, no host sync per iteration)
     ps, pn = lib.sphrt_loss_partials(n_meas), lib.sphrt_loss_partials(n_vox)
@@ -223,11 +236,12 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar, 
                 opt.zero_grad()
                 d = coeffs.detach()
                 stream = _lib.stream_of(d.device)
-                if staged is not None:
-                    # the forward reads the brick copy the previous Adam launch wrote (the first
-                    # one packs it)
-                    f._forward_staged(d, yhat_buf, staged[0])
-                    staged[0].stage_packed = 1
+                if loop_desc is not None:
+                    # (staged: the forward reads the brick copy the previous Adam launch wrote;
+                    # the first one packs it)
+                    f._forward_staged(d, yhat_buf, loop_desc)
+                    if staged is not None:
+                        loop_desc.stage_packed = 1
                     yhat = yhat_buf.view(yd.shape)
                 else:
                     yhat = f(d)
@@ -239,9 +253,9 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar, 
                 # (in the trace's ray order when the adjoint takes that: no permutation launch)
                 r_scaled = t.empty_like(yhat)
                 _lib.check(lib.sphrt_sq_residual_f64(
-                    _lib.ptr(yhat), _lib.ptr(yd), int(yd.dtype == t.float64), n_meas,
-                    2 * c_sq, _lib.ptr(order), _lib.ptr(r_scaled), _lib.ptr(part_sq[it]), stream),
-                    'sphrt_sq_residual_f64')
+                    _lib.ptr(yhat), _lib.ptr(y_res), int(yd.dtype == t.float64), n_meas,
+                    2 * c_sq, _lib.ptr(res_order), _lib.ptr(r_scaled), _lib.ptr(part_sq[it]),
+                    stream), 'sphrt_sq_residual_f64')
                 g = f._apply_adjoint(r_scaled, tuple(d.shape), d.dtype, d.device,
                                      trace_order=order is not None)
                 if reduce is not None:
@@ -271,9 +285,14 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar, 
     sums = part_sq[:done].sum(-1)
     if reduce is not None:
         reduce(sums)
-    losses[sq] = scaled(sums, n_norm, sq.lam).cpu().tolist()
     if neg is not None:
-        losses[neg] = scaled(part_neg[:done].sum(-1), n_vox, neg.lam).cpu().tolist()
+        sums = t.cat([sums, part_neg[:done].sum(-1)])
+    # one readback for both terms; the scaling in Python floats (the weights are Python
+    # numbers, _direct_plan) is the IEEE float64 division and product the tensor ops would do
+    host = sums.cpu().tolist()
+    losses[sq] = [scaled(v, n_norm, sq.lam) for v in host[:done]]
+    if neg is not None:
+        losses[neg] = [scaled(v, n_vox, neg.lam) for v in host[done:]]
     # the reference's bookkeeping: the coefficients once some iteration's total was < inf
     totals = [sum(v) for v in zip(*(losses[fn] for fn in loss_fns))]
     best = coeffs if any(v < float('inf') for v in totals) else None

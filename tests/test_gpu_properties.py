@@ -1173,6 +1173,11 @@ def test_gd_direct_matches_autograd(lams, meas_dtype, optim_kw, gpu, monkeypatch
         return direct(*a, **k)
 
     monkeypatch.setattr(retrieval, '_gd_direct', spy)
+    # (a wedge-ordered trace: the loop's forward writes f(d) in trace order)
+    rows = []
+    orig_rows = Operator._trace_position_rows
+    monkeypatch.setattr(Operator, '_trace_position_rows',
+                        lambda self, sd: rows.append(orig_rows(self, sd)) or rows[-1])
     runs = []
     for use_direct in (True, False):
         if not use_direct:
@@ -1182,11 +1187,36 @@ def test_gd_direct_matches_autograd(lams, meas_dtype, optim_kw, gpu, monkeypatch
                                    num_iterations=25, loss_fns=fns, progress_bar=False, **optim_kw)
         runs.append((c.detach().clone(), yh.detach().clone(), list(hist.values())))
     assert len(calls) == 1
+    assert len(rows) == 1 and rows[0] is not None
     (ca, ya, ha), (cb, yb, hb) = runs
     assert len(ha) == len(hb) and len(ha[0]) == 25 and ha[0][-1] < 0.3 * ha[0][0]
     for la, lb in zip(ha, hb):
         assert np.allclose(la, lb, rtol=1e-13, atol=0), (la, lb)
     assert tr.equal(ca, cb) and tr.equal(ya, yb)
+
+
+@pytest.mark.parametrize('kind, dtype', [('circ', tr.float64), ('circ', tr.float32),
+                                         ('rect', tr.float64)])
+@pytest.mark.parametrize('runs', ['auto', 'on'])
+def test_forward_in_trace_positions(kind, dtype, runs, gpu, monkeypatch):
+    """A loop descriptor whose row lists name trace positions (_trace_position_rows, the direct
+    gd loop's forward) writes the integral of trace position j to out[j]: bitwise op(x) gathered
+    through the trace's ray map, empty rays included."""
+    from sph_raytracer_amd import Operator
+    monkeypatch.setenv('SPHRT_RUNS', runs)           # (on: run records in trace positions)
+    grid, geom = _orbit(10, (20, 16), kind=kind, grid_shape=(16, 16, 16))
+    op = Operator(grid, geom, device=gpu)
+    if op._csr['ray_id'] is None:
+        pytest.skip('natural trace order')
+    x = tr.rand(grid.shape, dtype=dtype, device=gpu)
+    ref = op(x).reshape(-1)
+    sd = op._loop_descriptor(dtype)
+    keep = op._trace_position_rows(sd)
+    assert keep is not None and (sd.runs is None) == (keep[2] is None)
+    out = tr.full_like(ref, float('nan'))
+    op._forward_staged(x, out, sd)
+    tr.cuda.synchronize()
+    assert tr.equal(out, ref[op._ray_id_long()])
 
 
 def test_gd_direct_declines_what_it_cannot_run(gpu, monkeypatch):

@@ -26,6 +26,8 @@ def main():
     ap.add_argument('--pkg', default=None,
                     help='directory holding another revision\'s sph_raytracer_amd (A/B)')
     ap.add_argument('--no-autograd', action='store_true', help='skip the autograd comparison')
+    ap.add_argument('--reps', type=int, default=5,
+                    help='timed gd calls of each loop (the median is reported)')
     args = ap.parse_args()
     import bench            # (puts ROOT first on sys.path: --pkg goes in front of it after)
     if args.pkg:
@@ -50,15 +52,22 @@ def main():
     model = FullyDenseModel(grid)
     losses = [SquareLoss(), NegRegularizer()]
     def run():
+        # one warm-up call, then the median of `reps` whole gd calls (each the example's
+        # num_iterations, its set-up and the final forward of its return value included)
         retrieval.gd(op, y, model, num_iterations=3, loss_fns=losses, lr=1e-1, progress_bar=False)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        out = retrieval.gd(op, y, model, num_iterations=args.iters, loss_fns=losses, lr=1e-1,
-                           progress_bar=False)
-        torch.cuda.synchronize()
-        return out, time.perf_counter() - t0
+        ts = []
+        for _ in range(max(args.reps, 1)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = retrieval.gd(op, y, model, num_iterations=args.iters, loss_fns=losses, lr=1e-1,
+                               progress_bar=False)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        run.times = ts
+        return out, sorted(ts)[len(ts) // 2]
 
     (coeffs, y_hat, hist), t_gd = run()          # the autograd-free loop (retrieval._gd_direct)
+    gd_ms_all = [v * 1e3 for v in run.times]
     if args.no_autograd:
         (c_ag, hist_ag, t_ag) = (coeffs, hist, float('nan'))
     else:
@@ -71,6 +80,7 @@ def main():
                      'SquareLoss + NegRegularizer, Adam lr 0.1, float64',
            'rays': op._csr['n'], 'segments': op._csr['total'], 'iterations': args.iters,
            'operator_init_ms': t_init * 1e3, 'gd_total_ms': t_gd * 1e3,
+           'gd_total_ms_all': gd_ms_all, 'gd_timing': f'median of {len(gd_ms_all)} gd calls',
            'ms_per_iteration': t_gd / args.iters * 1e3,
            'ms_per_iteration_autograd': t_ag / args.iters * 1e3,
            'direct_iterates_equal_autograd': bool(torch.equal(coeffs, c_ag)),
