@@ -287,6 +287,9 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar, 
         reduce(sums)
     if neg is not None:
         sums = t.cat([sums, part_neg[:done].sum(-1)])
+    # the return value's forward goes out before the readback waits (best is these coefficients
+    # unless no iteration's total was finite, below)
+    y_best = f(coeffs)
     # one readback for both terms; the scaling in Python floats (the weights are Python
     # numbers, _direct_plan) is the IEEE float64 division and product the tensor ops would do
     host = sums.cpu().tolist()
@@ -296,7 +299,7 @@ def _gd_direct(f, y, coeffs, loss_fns, opt, plan, num_iterations, progress_bar, 
     # the reference's bookkeeping: the coefficients once some iteration's total was < inf
     totals = [sum(v) for v in zip(*(losses[fn] for fn in loss_fns))]
     best = coeffs if any(v < float('inf') for v in totals) else None
-    return best, f(best), losses
+    return best, (y_best if best is not None else f(best)), losses
 
 
 def _number(v):
