@@ -1195,6 +1195,40 @@ def test_gd_direct_matches_autograd(lams, meas_dtype, optim_kw, gpu, monkeypatch
     assert tr.equal(ca, cb) and tr.equal(ya, yb)
 
 
+@pytest.mark.parametrize('n', [1, 2, 7, 100001, 700000])
+@pytest.mark.parametrize('ydt', [tr.float64, tr.float32])
+@pytest.mark.parametrize('mode', ['in_order', 'order', 'unaligned'])
+def test_sq_residual_kernel(n, ydt, mode, gpu):
+    """sphrt_sq_residual_f64: r_scaled = (yhat - y) * scale elementwise as torch computes it
+    (bitwise), through a ray map or in order (aligned or not, odd lengths), and workgroup partial
+    sums of r * r within 1e-13 of torch's sum."""
+    from sph_raytracer_amd import _lib
+    lib = _lib.load()
+    g = tr.Generator(device='cpu').manual_seed(n)
+    yhat = tr.randn(n + 1, generator=g, dtype=tr.float64).to(gpu)
+    y = tr.randn(n + 1, generator=g, dtype=tr.float64).to(ydt).to(gpu)
+    order = None
+    if mode == 'unaligned':
+        yhat, y = yhat[1:], y[1:]
+    else:
+        yhat, y = yhat[:n], y[:n]
+    if mode == 'order':
+        order = tr.randperm(n, generator=g).to(tr.int32).to(gpu)
+    scale = 0.37
+    out = tr.empty(n, dtype=tr.float64, device=gpu)
+    part = tr.full((lib.sphrt_loss_partials(n),), float('nan'), dtype=tr.float64, device=gpu)
+    _lib.check(lib.sphrt_sq_residual_f64(_lib.ptr(yhat), _lib.ptr(y), int(ydt == tr.float64), n,
+                                         scale, _lib.ptr(order), _lib.ptr(out), _lib.ptr(part),
+                                         _lib.stream_of(gpu)), 'sq_residual')
+    r = yhat - y.to(tr.float64)
+    if order is not None:
+        r = r[order.long()]
+    assert tr.equal(out, r * scale)
+    assert not tr.isnan(part).any()
+    ref = float((r * r).sum())
+    assert abs(float(part.sum()) - ref) <= 1e-13 * abs(ref)
+
+
 @pytest.mark.parametrize('kind, dtype', [('circ', tr.float64), ('circ', tr.float32),
                                          ('rect', tr.float64)])
 @pytest.mark.parametrize('runs', ['auto', 'on'])
