@@ -19,11 +19,13 @@ its forward + dynamic gradient), ``--config c5`` times the static_retrieval.py g
 C2 run reports both legs too (``strong``), each checked against one GPU over the whole orbit.
 
 One JSON line on rank 0: value = rays/s over all ranks; roofline of the forward kernel
-(algorithmic bytes per launch / its mean launch duration from HIP events around the timed steps
-on the launch stream; the graph-replayed kernel alone beside it); cpu_baseline = the reference's forward (torch CPU on the reference's padded trace,
+(algorithmic bytes per launch, and the bytes it must stream, over its mean launch duration from
+HIP events bound to each launch's dispatch, K launches after the timed steps; the timed steps'
+span / K and the graph-replayed kernel beside it); cpu_baseline = the reference's forward (torch CPU on the reference's padded trace,
 oracle/ref_forward.py) on a bounded sample, timed on this host.
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -401,28 +403,113 @@ def _public(leg):
     return {k: v for k, v in leg.items() if not k.startswith('_')}
 
 
-def roofline(op, x, config, k_ms, k_method):
-    """The forward kernel's roofline: ALGORITHMIC bytes per launch (s_y + 4 +
-    S*(4 + s_len + s_rho) per ray; f32 path s_len = s_rho = 4) over its mean launch duration
-    `k_ms` (HIP events, kernel_time_ms), next to the HBM traffic of the newest committed
-    rocprofv3 --pmc record of this kernel and config (profiles/rNN_forward_<config>_pmc.json)."""
-    kname = op._forward_kernel_name(x)
-    traffic, traffic_src = None, None
+def kernel_dispatch_ms(op, x, reps):
+    """Mean duration of the forward kernel over `reps` back-to-back launches on the launch stream,
+    each launch's own dispatch bracketed by a pair of HIP events (sphrt_time_next_forward:
+    hipExtLaunchKernelGGL binds the events to the kernel's start and end) — the kernel's duration
+    as rocprofv3's kernel trace reports it, whatever the host's issue rate (a timed region's span
+    / K also counts the gaps between launches, and under the profiler the host can fall behind
+    the GPU).  -> (mean ms, median ms)."""
+    from sph_raytracer_amd import _lib
+    lib = _lib.load()
+    n_chan, div, _ = op._layout(x.shape)
+    out = torch.empty(op._csr['n'] * (n_chan if div == 0 else 1), dtype=x.dtype, device=x.device)
+    op._lengths(x.dtype)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for a, b in evs:            # (torch creates the HIP events on their first record)
+        a.record()
+        b.record()
+    torch.cuda.synchronize(x.device)
+    try:
+        for a, b in evs:
+            _lib.check(lib.sphrt_time_next_forward(ctypes.c_void_p(a.cuda_event),
+                                                   ctypes.c_void_p(b.cuda_event)),
+                       'sphrt_time_next_forward')
+            op._launch_forward(x, out, n_chan, div)
+    finally:
+        lib.sphrt_time_next_forward(None, None)
+    torch.cuda.synchronize(x.device)
+    d = sorted(a.elapsed_time(b) for a, b in evs)
+    return sum(d) / len(d), d[len(d) // 2]
+
+
+def must_move_bytes(op, x):
+    """Bytes the forward kernel must stream from HBM per launch, beside
+    SURVEY §8(d)'s algorithmic count: per segment its 2-byte granule slot (`loc`; 4-byte `vox`
+    for the per-segment gather modes) and its length in the density's precision; the granule
+    table entries its workgroups read (sum of n_tab over blocks, the tables' entry width); the
+    row metadata (48-byte block records, plus 128-byte run records or 4 B of row / empty-ray list
+    per ray); the outputs; the density once per resident copy (the distinct granules the tables
+    name, at most the whole array).  Density re-reads served by L2/MALL are not counted: this is
+    the floor a kernel could reach at full HBM bandwidth."""
+    n_chan, div, _ = op._layout(x.shape)
+    desc, k_chan, cs, k_div = op._launch_args(x, n_chan, div)
+    es = x.element_size()
+    csr = op._csr
+    n, total = csr['n'], csr['total']
+    blocks = csr['blocks']
+    if div > 0:
+        rec = op._paired(x.shape[0], div)
+        if rec is not None:
+            blocks = rec['keep'][1]
+    table = bool(desc.loc) and bool(desc.tab) and desc.tab_stride > 0 and k_div == 0
+    n_tab = int(blocks.view(-1, 6)[:, 5].sum()) if table else 0
+    seg = total * ((2 if table else 4) + es)
+    tabs = n_tab * int(desc.tab_bytes)
+    meta = desc.n_blocks * 48 + (desc.n_blocks * 128 if desc.runs else 4 * n)
+    outs = n * es * (k_chan if k_div == 0 else 1)
+    cols = desc.stage_cols if desc.stage_shape[0] > 0 else desc.n_cols
+    dens = k_chan * es * (min(cols, 4 * n_tab) if table else cols)
+    return {'bytes': seg + tabs + meta + outs + dens, 'segments': seg, 'tables': tabs,
+            'metadata': meta, 'outputs': outs, 'density_once': dens}
+
+
+def _pmc_traffic(op, x, config, kname):
+    """HBM traffic per launch of the newest committed rocprofv3 --pmc record of this kernel and
+    config (profiles/rNN_forward_<config>_pmc.json), when it was taken on the same CSR: records
+    carry their ray and segment counts (round 6 on); a record without them is taken to be the
+    single-GPU config, so a shard (a strong-scaled rank) of another size gets none."""
     for tag in ('r06', 'r05', 'r04', 'r03', 'r02', 'r01'):
         pmc = os.path.join(ROOT, 'profiles', f'{tag}_forward_{config}_pmc.json')
         if not os.path.exists(pmc):
             continue
-        rec_pmc = json.load(open(pmc))
-        if rec_pmc.get('kernel') == kname and rec_pmc.get('config') == config:
-            traffic, traffic_src = rec_pmc['traffic_bytes_per_launch'], os.path.relpath(pmc, ROOT)
-            break
+        rec = json.load(open(pmc))
+        if rec.get('kernel') != kname or rec.get('config') != config:
+            continue
+        if 'segments' in rec:
+            same = rec['segments'] == op._csr['total'] and rec.get('rays') == op._csr['n']
+        else:
+            full = CONFIGS[config]
+            same = op._csr['n'] == math.prod(full[2]) * full[1]
+        if not same:
+            return None, f'{os.path.relpath(pmc, ROOT)} was taken on another CSR (not this shard)'
+        return rec['traffic_bytes_per_launch'], os.path.relpath(pmc, ROOT)
+    return None, None
+
+
+def roofline(op, x, config, k_ms, k_method):
+    """The forward kernel's roofline.  achieved = ALGORITHMIC bytes per launch (SURVEY §8(d):
+    s_y + 4 + S*(4 + s_len + s_rho) per ray; f32 path s_len = s_rho = 4) over its mean launch
+    duration `k_ms`; `must_move` = the same over the bytes the kernel must stream (must_move_bytes);
+    `traffic` = HBM bytes per launch of the committed PMC record of this kernel on this CSR.
+    SURVEY's basis counts every density gather as HBM although the volume is L2-resident, so it
+    can exceed the peak where gathers repeat (C5: the view tiles); must_move cannot."""
+    kname = op._forward_kernel_name(x)
+    traffic, traffic_src = _pmc_traffic(op, x, config, kname)
     es = x.element_size()
-    alg_bytes = op._csr['n'] * (es + 4) + op._csr['total'] * (4 + es + es)
+    n_chan, div, _ = op._layout(x.shape)
+    n_out = n_chan if div == 0 else 1
+    alg_bytes = op._csr['n'] * n_out * (es + 4) + op._csr['total'] * n_out * (4 + es + es)
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    mm = must_move_bytes(op, x)
+    mm_gbs = mm['bytes'] / (k_ms * 1e-3) / 1e9
+    mm.update({'achieved': mm_gbs, 'frac': mm_gbs / HBM_PEAK_GBS})
     return {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
             'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
             'achieved_basis': 'algorithmic bytes (SURVEY 8(d): s_y + 4 + S*(4 + s_len + '
                               's_rho) per ray; density gathers counted as HBM)',
+            'must_move': mm,
             'traffic_gbs': traffic / (k_ms * 1e-3) / 1e9 if traffic else None,
             'traffic_frac': traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
             'traffic_source': traffic_src, 'kernel': kname,
@@ -460,7 +547,9 @@ def strong_main(args, rk):
         ms, dtype = leg['ms_per_iteration'], torch.float64
     peak_gb = torch.cuda.max_memory_allocated(rk.dev) / 1e9
     op, x = leg['_op'], leg['_x']
-    k_ms, k_method = kernel_time_ms(op, x, reps=50)
+    k_ms, k_med = kernel_dispatch_ms(op, x, reps=max(args.steps, 50))
+    k_method = ('HIP events bound to each launch\'s dispatch (sphrt_time_next_forward), mean '
+                f'over {max(args.steps, 50)} back-to-back launches on the launch stream')
     rec = {
         'metric': METRIC,
         'value': leg['rays_per_s'],
@@ -483,6 +572,7 @@ def strong_main(args, rk):
         'strong': _public(leg),
         'roofline': roofline(op, x, args.config, k_ms, k_method),
     }
+    rec['roofline']['kernel_ms_median'] = k_med
     rec['roofline']['scope'] = 'this rank\'s local forward kernel'
     if rk.rank == 0 and rk.world == 1 and not args.no_cpu_baseline:
         try:
@@ -641,6 +731,9 @@ def main():
     rk.close()
     dt = time.perf_counter() - t0
     k_ms_timed = ev0.elapsed_time(ev1) / args.steps
+    # the roofline's denominator: the forward kernel's own duration over K more launches, each
+    # dispatch bracketed by its HIP event pair (what rocprofv3's kernel trace reports)
+    k_ms_disp, k_med_disp = kernel_dispatch_ms(op, x, args.steps)
     gather = None
     if dist is not None:
         dt, t_cold = max_over_ranks([dt, t_cold])
@@ -696,7 +789,8 @@ def main():
     k_ms_graph, _ = kernel_time_ms(op, x, reps=k_reps)
     # launch order of the forward kernel in this process, for tools/rocprof_legs.py (splits a
     # rocprofv3 kernel trace of this command into these legs)
-    log('legs ' + json.dumps([['first', 1], ['warmup', args.warmup], ['steps', args.steps]] +
+    log('legs ' + json.dumps([['first', 1], ['warmup', args.warmup], ['steps', args.steps],
+                              ['dispatch', args.steps]] +
                              ([['final_gather_fwd', 1]] if dist is not None else []) +
                              [['cold', 3], ['pcie', 3 + reps_h], ['graph', 1 + 4 * k_reps]] +
                              [['adjoint', 3 + adj_steps]]))
@@ -742,8 +836,14 @@ def main():
                    'what': 'op.T(y), y = torch.rand(geom.shape): the transposed CSR (built by the '
                            'first of 3 untimed calls) through the same table kernel; per-step '
                            'wall time incl. launch; bytes as SURVEY 8(d) with voxels as rows'}
-    roof = roofline(op, x, args.config, k_ms_timed,
-                    'HIP events on the launch stream around the timed steps (span / K)')
+    roof = roofline(op, x, args.config, k_ms_disp,
+                    f'HIP events bound to each launch\'s dispatch (sphrt_time_next_forward), mean '
+                    f'over {args.steps} back-to-back launches on the launch stream, right after '
+                    f'the timed steps')
+    roof['kernel_ms_median'] = k_med_disp
+    # the timed steps' span / K on the launch stream (kernel + the gaps between launches)
+    roof['kernel_ms_timed_span'] = k_ms_timed
+    roof['frac_timed_span'] = roof['bytes_per_launch'] / (k_ms_timed * 1e-3) / 1e9 / HBM_PEAK_GBS
     # the same kernel back to back in a HIP graph (no host issue between launches), for reference
     roof['kernel_ms_graph_replay'] = k_ms_graph
     roof['frac_graph_replay'] = roof['bytes_per_launch'] / (k_ms_graph * 1e-3) / 1e9 / HBM_PEAK_GBS

@@ -349,6 +349,14 @@ int sphrt_forward_f64(const sphrt_csr *csr, const double *density, int64_t n_cha
                       int64_t chan_stride, int64_t ray_chan_div, double *out,
                       int64_t out_chan_stride, void *stream);
 
+/* Kernel timing for measurement (bench.py's roofline; no reference counterpart): the next
+ * sphrt_forward_f32/f64 call on this host thread launches its main forward kernel with these two
+ * HIP events (hipEvent_t, created with timing) bound to the dispatch itself, so that
+ * hipEventElapsedTime(start, stop) is that kernel's own duration — what a kernel trace reports —
+ * whatever the host's issue rate.  Consumed by that one launch; the brick pack and the fallback
+ * launch are not bracketed.  Either event may be NULL. */
+int sphrt_time_next_forward(void *start_event, void *stop_event);
+
 /* ---- adjoint / back-projection (replaces Operator.T, raytracer.py:715-748, and the autograd
  * backward of raytracer.py:710) ------------------------------------------------------------ */
 /* acc[c*chan_stride + vox[s]] += y[c*y_chan_stride + i] * len[s], float64 atomics into a zeroed

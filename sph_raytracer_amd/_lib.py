@@ -101,6 +101,7 @@ _SIGNATURES = [
                                   c_vp]),
     ('sphrt_forward_f64', c_int, [ctypes.POINTER(CSR), c_vp, c_i64, c_i64, c_i64, c_vp, c_i64,
                                   c_vp]),
+    ('sphrt_time_next_forward', c_int, [c_vp, c_vp]),
     ('sphrt_adjoint_accumulate', c_int, [ctypes.POINTER(CSR), c_vp, c_int, c_i64, c_i64, c_i64,
                                          c_vp, c_i64, c_vp]),
     ('sphrt_transpose_workspace_bytes', ctypes.c_size_t, [c_i64, c_i64]),

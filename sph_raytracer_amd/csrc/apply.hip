@@ -14,6 +14,7 @@
 // gathers the density (a 0.5-8 MB volume, L2/MALL resident), reduces runs between head bits in
 // float64, and a block-level segmented scan stitches rows that cross thread chunks.  Balanced
 // whatever the row lengths, ~3 dependent global round trips per workgroup, deterministic order.
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 
 #include <stdlib.h>
@@ -2017,6 +2018,29 @@ static int fwd_chunk(const sphrt_csr* c, size_t elem) {
     return (c->order & 1) ? ~k : k;   // (block_of: reversed)
 }
 
+// Dispatch timing (sphrt_time_next_forward): the next forward launch on this thread brackets its
+// main kernel with these HIP events, recorded by the dispatch itself (hipExtLaunchKernelGGL): the
+// kernel's own start and end, as a kernel trace reports them, independent of how fast the host
+// issues.  The stage pack and the fallback launch are not bracketed.  Consumed by one launch.
+static thread_local hipEvent_t t_fwd_start = nullptr, t_fwd_stop = nullptr;
+
+extern "C" int sphrt_time_next_forward(void* start_event, void* stop_event) {
+    t_fwd_start = (hipEvent_t)start_event;
+    t_fwd_stop = (hipEvent_t)stop_event;
+    return 0;
+}
+
+#define FWD_LAUNCH(KERNEL, G, B, LDS, ST, ...)                                                   \
+    do {                                                                                          \
+        if (t_fwd_start || t_fwd_stop) {                                                          \
+            hipEvent_t e0_ = t_fwd_start, e1_ = t_fwd_stop;                                       \
+            t_fwd_start = t_fwd_stop = nullptr;                                                   \
+            hipExtLaunchKernelGGL(KERNEL, G, B, (uint32_t)(LDS), ST, e0_, e1_, 0u, __VA_ARGS__);   \
+        } else {                                                                                  \
+            hipLaunchKernelGGL(KERNEL, G, B, LDS, ST, __VA_ARGS__);                               \
+        }                                                                                         \
+    } while (0)
+
 template <typename T, typename L>
 static int launch_forward(const sphrt_csr* c, const L* len, const T* density, int64_t n_chan,
                           int64_t chan_stride, int64_t div, T* out, int64_t ocs, void* stream) {
@@ -2033,8 +2057,8 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
     const T* td = sm.on ? (const T*)c->stage : density;      // what the table kernel gathers
     const int64_t tcs = sm.on ? c->stage_cols : chan_stride;
     if (div > 0) {
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdDynamic, int32_t, false, P>), grid, block, 0, st,
-                           FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, nullptr);
+        FWD_LAUNCH((forward_kernel<T, L, kFwdDynamic, int32_t, false, P>), grid, block, 0, st,
+                   FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, (const int32_t*)nullptr);
     } else if (use_tables(c, td, n_chan, tcs, div)) {
         if (sm.on && (!c->stage || (int64_t)sizeof(T) * n_chan * c->stage_cols > c->stage_bytes))
             return fail("brick stage buffer missing or too small for this call");
@@ -2058,8 +2082,8 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
                                : edma ? imax64(c->tab_stride, kGranEarly * kThreads)
                                       : c->tab_stride) + 1) * 4 * sizeof(T);   // + zero granule
 #define FWD_TABLE(TabT, E, R, H)                                                            \
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdTable, TabT, E, P, R, H>), grid, block, lds, \
-                           st, FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
+        FWD_LAUNCH((forward_kernel<T, L, kFwdTable, TabT, E, P, R, H>), grid, block, lds, st, \
+                   FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
 #define FWD_TABLE_R(TabT, E, H)                                                             \
         do {                                                                                      \
             if (c->runs) FWD_TABLE(TabT, E, true, H);                                       \
@@ -2090,8 +2114,8 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
                                nullptr);
         }
     } else {
-        hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0, st,
-                           FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, nullptr);
+        FWD_LAUNCH((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0, st,
+                   FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, (const int32_t*)nullptr);
     }
 #undef FWD_ARGS
     return check_launch(sizeof(T) == 4 ? "forward_kernel<f32>" : "forward_kernel<f64>");

@@ -20,6 +20,7 @@ import ctypes
 import functools
 import math
 import os
+import weakref
 
 import torch as tr
 
@@ -216,14 +217,31 @@ class _Plan:
             self.handle = None
 
 
+def _broadcast_shapes(*shapes):
+    """torch.broadcast_shapes in plain Python: the torch function imports torch._refs (and with
+    it sympy) on its first call, ~0.8 s that the first dynamic Operator's first forward paid
+    (tools/first_construct.py).  Same result and the same error type."""
+    nd = max((len(s) for s in shapes), default=0)
+    out = [1] * nd
+    for s in shapes:
+        for i, v in enumerate(s, nd - len(s)):
+            v = int(v)
+            if v != 1:
+                if out[i] not in (1, v):
+                    raise RuntimeError(f'Shape mismatch: objects cannot be broadcast to a single '
+                                       f'shape.  Mismatch is between {tuple(shapes)}')
+                out[i] = v
+    return tuple(out)
+
+
 def _broadcast_pair(xs, rays):
     """Reference broadcasting rule (raytracer.py:76-80) -> (ray shape, xs, rays) un-expanded."""
     xs = tr.asarray(xs, dtype=tr.float64)
     rays = tr.asarray(rays, dtype=tr.float64)
     if xs.numel() > rays.numel():
-        shape = tuple(tr.broadcast_shapes(rays.shape, xs.shape))
+        shape = _broadcast_shapes(rays.shape, xs.shape)
     else:
-        shape = tuple(tr.broadcast_shapes(xs.shape, rays.shape))
+        shape = _broadcast_shapes(xs.shape, rays.shape)
     return shape[:-1], xs, rays
 
 
@@ -536,7 +554,7 @@ def _layout_for(grid, ray_shape, shape):
         T = shape[0]
         if len(R) > 3:
             raise NotImplementedError('dynamic grids need a detector of rank <= 3')
-        out_shape = tuple(tr.broadcast_shapes((T, 1, 1, 1), R + (1,))[:-1])
+        out_shape = _broadcast_shapes((T, 1, 1, 1), R + (1,))[:-1]
         if len(R) == 3 and R[0] == T and T > 1:
             return 1, R[1] * R[2], out_shape        # view i sees time slice i
         if len(R) == 3 and R[0] != 1 and T != 1:
@@ -671,18 +689,34 @@ _TROWS = (4, 2, 4)
 
 
 def _voxel_rows(shape3, n_cols, dev, nblocks):
-    """(vpos, vperm) int32 on `dev`: row position of every voxel (column) of a static
+    """A _VoxelRows (vpos, vperm: int32 on `dev`): row position of every voxel (column) of a static
     transposed CSR and the voxel of every row position, or None (linear order)."""
     env = os.environ.get('SPHRT_TROWS', 'auto')
     brick = None if env == 'off' else tuple(int(v) for v in env.split(',')) if env != 'auto' \
         else _TROWS if nblocks > _SINGLE_WAVE_BLOCKS else None
     if brick is None or n_cols != math.prod(shape3) or n_cols >= 2 ** 31:
         return None
-    return _voxel_rows_cached(shape3, brick, str(dev))
+    key = (shape3, brick, str(dev))
+    rows = _VOXEL_ROWS.get(key)
+    if rows is None:
+        rows = _VoxelRows(*_voxel_rows_make(shape3, brick, dev))
+        _VOXEL_ROWS[key] = rows
+    return rows
 
 
-@functools.lru_cache(maxsize=8)
-def _voxel_rows_cached(shape3, brick, dev):
+class _VoxelRows:
+    """The row maps of one grid shape and device, shared by the transposed CSRs that hold them
+    (each keeps a reference in its record) and released with the last of them (ADVICE r05:
+    a module-level cache of device tensors outlived every Operator)."""
+
+    def __init__(self, vpos, vperm):
+        self.vpos, self.vperm = vpos, vperm
+
+
+_VOXEL_ROWS = weakref.WeakValueDictionary()
+
+
+def _voxel_rows_make(shape3, brick, dev):
     nr, ne, na = shape3
     br, be, ba = brick
     idx = tr.arange(nr * ne * na, device=dev, dtype=tr.int64)
@@ -920,14 +954,27 @@ class _TraceRecord(dict):
             self._move_len()
         return dict.__getitem__(self, k)
 
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+
+    def lengths64(self):
+        """The float64 segment lengths (moved out of the trace staging on the first call)."""
+        return self['len']
+
     def _move_len(self):
         row_ptr, bound_ptr, slen, dev = dict.pop(self, 'len_staging')
         total, n = dict.__getitem__(self, 'total'), dict.__getitem__(self, 'n')
         seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
         with tr.cuda.device(dev):
+            stream = tr.cuda.current_stream(dev)
             _lib.check(_lib.load().sphrt_trace_compact(
                 n, _lib.ptr(bound_ptr), None, _lib.ptr(slen), _lib.ptr(row_ptr), None,
-                _lib.ptr(seg_len), _lib.stream_of(dev)), 'sphrt_trace_compact(len)')
+                _lib.ptr(seg_len), ctypes.c_void_p(stream.cuda_stream)), 'sphrt_trace_compact(len)')
+            # the staging was allocated on the construction stream: if this first float64 use
+            # runs on another stream, the allocator must not hand the staging back to the
+            # construction stream before the compaction has read it (ADVICE r05)
+            for t in (bound_ptr, slen, row_ptr):
+                t.record_stream(stream)
         dict.__getitem__(self, 'desc').len = seg_len.data_ptr()
         dict.__setitem__(self, 'len', seg_len)
 
@@ -1344,6 +1391,8 @@ class Operator:
         lib = _lib.load()
         self._lengths(d.dtype)
         desc, n_chan, cs, div = self._launch_args(d, n_chan, div)
+        if d.dtype == tr.float64 and not desc.len:
+            raise RuntimeError('float64 forward without the float64 segment lengths')
         fn = lib.sphrt_forward_f32 if d.dtype == tr.float32 else lib.sphrt_forward_f64
         _call_forward(fn, desc, d, n_chan, cs, div, out, self._csr['n'], self._cdev)
         _alternate(desc)
@@ -1352,9 +1401,23 @@ class Operator:
         """The forward kernel instantiation a launch on `d` runs (sphrt_forward_*'s choice, for
         reports): 0 = granule tables staged in LDS, 1 = per-segment gathers, 2 = time slices;
         the last flag: float64 half tables."""
-        t = 'float, float' if d.dtype == tr.float32 else 'double, double'
         n_chan, div, _ = self._layout(d.shape)
         c, n_chan, _, div = self._launch_args(d, n_chan, div)
+        return self._kernel_name_for(c, d, n_chan, div)
+
+    def _adjoint_kernel_name(self, d):
+        """The instantiation the adjoint of a density like `d` runs (the transposed CSR's
+        forward; a dynamic grid's time-paired gradient), after the first adjoint built it."""
+        n_chan, div, _ = self._layout(d.shape)
+        if div > 0:
+            c = self._paired(d.shape[0], div)['transposed']['desc']
+        else:
+            c = self._transposed()['desc']
+        return self._kernel_name_for(c, d, 1, 0)
+
+    @staticmethod
+    def _kernel_name_for(c, d, n_chan, div):
+        t = 'float, float' if d.dtype == tr.float32 else 'double, double'
         es = d.element_size()
         aligned = d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0)
         table = (c.loc and div == 0 and 0 < c.tab_stride and (c.tab_stride + 1) * 4 * es <= 64 * 1024
@@ -1441,7 +1504,7 @@ class Operator:
         rows = _voxel_rows(tuple(int(v) for v in self.grid.shape[-3:]), n_cols, dev,
                            csr['nblocks'])
         if rows is not None:             # the columns renumbered in row order for the sort
-            vpos, vperm = rows
+            vpos = rows.vpos
             v = vox[:total]
             pos = vpos.index_select(0, v & 0x7fffffff)
             vox_pos = tr.where(v < 0, pos | _HEAD32, pos)
@@ -1467,7 +1530,7 @@ class Operator:
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n_vox), dtype=tr.uint8, device=dev)
         _lib.check(lib.sphrt_csr_index(_lib.ptr(col_ptr), n_vox, _lib.ptr(t_ray),
                                        _lib.ptr(vox_list), _lib.ptr(empty_vox), _lib.ptr(blocks),
-                                       nblocks, _lib.ptr(rows[1]) if rows is not None else None,
+                                       nblocks, _lib.ptr(rows.vperm) if rows is not None else None,
                                        _lib.ptr(iws), stream),
                    'sphrt_csr_index(T)')
         t_len32 = tr.empty(t_len.shape, dtype=tr.float32, device=dev)   # (filled with the tables)
@@ -1484,7 +1547,7 @@ class Operator:
                    if shape3 else None)
         loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
         return dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, empty_vox, blocks,
-                                  loc, tab, runs))
+                                  loc, tab, runs, rows))
 
     def _paired(self, T, div):
         """The trace with time-paired columns (ray r reads slice r // div: column

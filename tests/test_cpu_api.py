@@ -248,6 +248,35 @@ def test_density_layouts():
         _layout_for(static, (64, 64), (2, 3, 5))
 
 
+def test_layout_and_broadcast_import_nothing_heavy():
+    """The shape rules import no sympy: torch.broadcast_shapes does (torch._refs) on its first
+    call, which cost the first dynamic Operator's first forward ~0.8 s.
+    The plain-Python broadcast equals torch's, errors included."""
+    import subprocess
+    import sys
+    code = ('import sys; sys.path.insert(0, %r); import torch; '
+            'from sph_raytracer_amd import SphericalGrid; '
+            'from sph_raytracer_amd.raytracer import _layout_for, _broadcast_pair; '
+            'dyn = SphericalGrid((10, 2, 3, 4)); _layout_for(dyn, (10, 8, 6), (10, 2, 3, 4)); '
+            '_layout_for(dyn, (4,), (10, 2, 3, 4)); '
+            '_broadcast_pair(torch.zeros(3), torch.ones(5, 4, 3)); '
+            'print("sympy" in sys.modules)' % os.path.dirname(os.path.dirname(__file__)))
+    out = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, check=True)
+    assert out.stdout.strip().splitlines()[-1] == 'False'
+    from sph_raytracer_amd.raytracer import _broadcast_shapes
+    rng = np.random.default_rng(0)
+    for _ in range(500):
+        a = tuple(int(v) for v in rng.integers(1, 4, rng.integers(0, 5)))
+        b = tuple(int(v) for v in rng.integers(1, 4, rng.integers(0, 5)))
+        try:
+            want = tuple(tr.broadcast_shapes(a, b))
+        except RuntimeError:
+            with pytest.raises(RuntimeError):
+                _broadcast_shapes(a, b)
+            continue
+        assert _broadcast_shapes(a, b) == want
+
+
 def test_no_cpu_fallback():
     """Without a GPU the product path fails loudly instead of computing on the CPU."""
     if tr.cuda.is_available():

@@ -45,6 +45,9 @@ def main():
     ap.add_argument('--config', default='c2')
     ap.add_argument('--only', action='store_true')
     ap.add_argument('--dtype', default='f32', choices=['f32', 'f64'], help='--only: forward dtype')
+    ap.add_argument('--adjoint', action='store_true',
+                    help='--only: the adjoint instead (op.T, or the time-paired gradient of a '
+                         'dynamic grid): the transposed CSR\'s forward kernel')
     args = ap.parse_args()
     import bench
     from sph_raytracer_amd import Operator, _lib
@@ -60,6 +63,14 @@ def main():
     o64 = torch.empty(o32.shape, dtype=torch.float64, device=dev)
     if args.only:
         xo, oo = (x32, o32) if args.dtype == 'f32' else (x64, o64)
+        if args.adjoint:
+            yo = torch.rand(tuple(geom.shape), dtype=xo.dtype, device=dev)
+            op._apply_adjoint(yo, tuple(xo.shape), xo.dtype, dev)     # builds the transpose
+            torch.cuda.synchronize()
+            for _ in range(args.reps):
+                op._apply_adjoint(yo, tuple(xo.shape), xo.dtype, dev)
+            torch.cuda.synchronize()
+            return
         for _ in range(args.reps):
             op._launch_forward(xo, oo, n_chan, div)
         torch.cuda.synchronize()
