@@ -335,8 +335,8 @@ _WEDGE = 3
 # with (64, 2); the transposed adjoints C2 6.2 / 8.6 -> 5.9 / 8.4, C3 192 / 303 -> 187 / 287, C5
 # 24.7 / 40.4 -> 24.7 / 35.3.  tv: the largest divisor of the view count in [8, 64]; tw = 2 (1
 # for an odd width).  Dynamic grids keep the per-view orders (view i <-> time slice i pairs trace
-# rows with slices by position).  SPHRT_RAY_ORDER=natural / views:G / tile:h,w (studies) keep
-# other orders, vtile:tv,1,tw forces a tile.
+# rows with slices by position).  SPHRT_RAY_ORDER=natural keeps the geometry order, vtile:tv,1,tw
+# forces a tile.
 _VIEW_TILE_MAX, _VIEW_TILE_MIN = 64, 8
 
 
@@ -365,25 +365,14 @@ def _trace_order(geom, rays, dynamic=False):
     workgroup block at C5) sweep most of a ring, whose rays part around the view axis.  Wedges of
     _WEDGE azimuth columns, radius-major inside, keep a block's rays together: C5 table stride
     1536 -> 1024, forward f32 33.2 -> 29.5 us, f64 52.7 -> 45.8 us, transposed adjoint f64 53.4
-    -> 43.5 us (ConeRect rows are already compact: strips beat every tiling measured).  Only the order of the CSR's rows changes: every
-    row reports its geometry ray (sphrt_csr_index ray_ids), outputs stay in geometry order.
-    SPHRT_RAY_ORDER=natural keeps the geometry order.  The study orders across views (views:,
-    vtile:) apply to static grids only (a dynamic grid pairs trace rows with time slices by
-    position)."""
-    mode = os.environ.get('SPHRT_RAY_ORDER', 'auto')
-    if mode == 'natural':
+    -> 43.5 us (ConeRect rows are already compact: strips beat every tiling measured).  Only the
+    order of the CSR's rows changes: every row reports its geometry ray (sphrt_csr_index ray_ids),
+    outputs stay in geometry order.  SPHRT_RAY_ORDER=natural keeps the geometry order.  (The
+    orders across views measured in rounds 2-5 — rows of G views, detector tiles, tiles of
+    several rows — live in tools/build_src_variant.py's history and the A/B records; only the
+    view tiles, _view_tiles, were kept.)"""
+    if os.environ.get('SPHRT_RAY_ORDER', 'auto') == 'natural':
         return None
-    shape = tuple(rays.shape[:-1])
-    if dynamic and (mode.startswith('views:') or mode.startswith('vtile:')):
-        return None
-    if mode.startswith('tile:') and len(shape) in (2, 3):     # A/B studies: detector tiles
-        th, tw = (int(v) for v in mode[5:].split(','))
-        return _tile_order(shape[-2], shape[-1], th, tw)
-    if mode.startswith('views:') and len(shape) == 3:          # A/B studies: rows of G views
-        return _view_row_order(shape[0], shape[1], shape[2], int(mode[6:]))
-    if mode.startswith('vtile:') and len(shape) == 3:          # tiles of several rows (studies)
-        return _view_tile_order(shape[0], shape[1], shape[2],
-                                *(int(v) for v in mode[6:].split(',')))
     from .geometry import ConeCircGeom
     geoms = getattr(geom, 'geoms', [geom])
     if not geoms or any(type(g) is not ConeCircGeom for g in geoms):
@@ -392,41 +381,6 @@ def _trace_order(geom, rays, dynamic=False):
     if len(shape) not in (2, 3) or shape[-1] <= _WEDGE:
         return None
     return _wedge_order(shape[-2], shape[-1])
-
-
-@functools.lru_cache(maxsize=16)
-def _view_row_order(v, h, w, g):
-    """Order of all (v, h, w) pixels: groups of g consecutive views, inside a group row by row
-    and, inside a row, view by view (studies only: adjacent orbit views cross nearly the same
-    voxels along a row, so a group's rows reuse each other's density lines)."""
-    vi = tr.arange(v).repeat_interleave(h * w)
-    r = tr.arange(h).repeat_interleave(w).repeat(v)
-    c = tr.arange(w).repeat(v * h)
-    key = (((vi // g) * h + r) * g + vi % g) * w + c
-    return tr.argsort(key)
-
-
-@functools.lru_cache(maxsize=16)
-def _view_tile_order(v, h, w, tv, th, tw):
-    """Order of all (v, h, w) pixels in tiles of tv views x th rows x tw columns (studies only):
-    tiles by (row band, column band, view group), inside a tile view, row, column — a
-    workgroup's rays are one pixel patch seen from neighbouring views."""
-    vi = tr.arange(v).repeat_interleave(h * w)
-    r = tr.arange(h).repeat_interleave(w).repeat(v)
-    c = tr.arange(w).repeat(v * h)
-    ncb, nvg = -(-w // tw), -(-v // tv)
-    key = ((((r // th) * ncb + c // tw) * nvg + vi // tv) * tv + vi % tv) * (th * tw) + \
-        (r % th) * tw + c % tw
-    return tr.argsort(key)
-
-
-@functools.lru_cache(maxsize=16)
-def _tile_order(h, w, th, tw):
-    """Pixel order of an (h, w) detector in row-major tiles of th x tw pixels (studies only)."""
-    r = tr.arange(h).repeat_interleave(w)
-    a = tr.arange(w).repeat(h)
-    key = (((r // th) * (-(-w // tw)) + a // tw) * th + r % th) * tw + a % tw
-    return tr.argsort(key)
 
 
 @functools.lru_cache(maxsize=16)
@@ -1027,8 +981,9 @@ class Operator:
         self._fast = {}     # (shape, dtype, device) -> bound forward launch (steady-state calls)
         self._fastc = None  # the same bindings inside the CPython entry (csrc/fastpath.cpp)
         self._fastc_T = None  # the adjoint's steady-state bindings (T), same entry
-        # 'transpose': deterministic voxel-major adjoint (default); 'atomic': float64 atomics
-        # (used anyway when views are paired with time slices)
+        # 'transpose': deterministic voxel-major adjoint (default; a view <-> time pairing
+        # transposes its time-paired CSR); 'atomic': float64 atomics (a cross-check, and the
+        # fallback when T * vol does not fit 32-bit columns)
         self.adjoint_mode = 'transpose'
         if _compute:
             self._trace()
@@ -1101,16 +1056,7 @@ class Operator:
         else:
             rays = self.geom.rays
             perm = _trace_order(self.geom, rays, self.grid.dynamic)
-        if perm is not None and rays.dim() == 4 and perm.numel() > math.prod(rays.shape[-3:-1]):
-            # an order across views (studies): starts and start voxels follow their rays
-            pd = perm.to(dev, non_blocking=True)
-            full = tuple(rays.shape[:-1])
-            rays = rays.reshape(-1, 3).index_select(0, pd).reshape(rays.shape)
-            xs_d = xs_d.expand(full + (3,)).reshape(-1, 3).index_select(0, pd).reshape(full + (3,))
-            st_d = st_d.expand(full + (4,)).reshape(-1, 4).index_select(0, pd).reshape(full + (4,))
-            xs_h = xs_d
-            ray_id = pd.to(tr.int32)
-        elif perm is not None:         # trace in wedges; rows report their geometry ray
+        if perm is not None:           # trace in wedges; rows report their geometry ray
             rays, ray_id = _permute_rays(rays, perm.to(dev, non_blocking=True))
         batch = _RayBatch(self.grid, xs_h, rays, dev, staged=(xs_d, st_d))
         self._ray_shape = cone.shape if tiles is not None else batch.shape
