@@ -144,6 +144,15 @@ int sphrt_trace_fill(const sphrt_plan *plan, const sphrt_rays *rays, const int64
 int sphrt_trace_reference(const sphrt_plan *plan, const sphrt_rays *rays, int flags,
                           int32_t *counts, const int64_t *row_ptr, int32_t *vox, double *len,
                           void *workspace, size_t workspace_size, void *stream);
+/* The reference-mode trace in one pass, as sphrt_trace_emit: every ray's segments into its slot
+ * [bound_ptr[i], bound_ptr[i+1]) of (svox, slen) and its exact count into counts; rays whose
+ * count exceeds their slot write only the count and are counted in *n_over (device int64).  A
+ * slot of K (sphrt_plan_candidates) segments always suffices: the walk keeps at most one segment
+ * per list entry.  Compact with sphrt_trace_compact after scanning the counts. */
+int sphrt_trace_reference_emit(const sphrt_plan *plan, const sphrt_rays *rays, int flags,
+                               const int64_t *bound_ptr, int32_t *counts, int32_t *svox,
+                               double *slen, int64_t *n_over, void *workspace,
+                               size_t workspace_size, void *stream);
 
 /* One-pass trace (the same CSR as count + fill, tracing every ray once instead of twice):
  *  1. sphrt_trace_bound: screens the rays and writes an upper bound of every ray's segment count
@@ -259,7 +268,11 @@ typedef struct sphrt_csr {
      * resident wave of blocks, so a CSR (or a forward / adjoint pair) that outgrows the
      * memory-side cache starts each launch on the lines the previous launch left cached instead
      * of the ones it evicted first (C3 forward f32 233 -> 213 us; C5 retrieval 0.138 -> 0.133
-     * ms/iteration). */
+     * ms/iteration).  Bit 2 set (not a hint: a layout): dense output ranges — the rows are in
+     * output order (row_ray increasing) and each block record's fields 0 / 1 hold the output range
+     * [lo, hi) that block writes, its rows and the empty rows up to the next block's first row;
+     * the block zeroes the range itself and empty_ray is not read.  One channel, no
+     * ray_chan_div, runs NULL. */
     int64_t order;
     /* 1: `stage` already holds this call's density in the brick layout (pad columns zero), e.g.
      * written by sphrt_adam_neg_f64 after an earlier forward packed the same buffer; the forward
@@ -375,6 +388,11 @@ int sphrt_csr_transpose(const sphrt_csr *csr, int64_t n_vox, int64_t *col_ptr, i
                         double *t_len, void *workspace, size_t workspace_size, void *stream);
 /* dst[i] = (float)src[i] — rounding the float64 accumulator to a float32 result. */
 int sphrt_f64_to_f32(const double *src, float *dst, int64_t n, void *stream);
+/* dst[i] = src[idx[i]], i < n (idx int32): the adjoint's input in trace order when the transposed
+ * CSR's columns are trace rows (idx = the trace's ray ids), one launch instead of an
+ * index_select. */
+int sphrt_gather_f32(const float *src, const int32_t *idx, int64_t n, float *dst, void *stream);
+int sphrt_gather_f64(const double *src, const int32_t *idx, int64_t n, double *dst, void *stream);
 
 /* ---- retrieval loss tails (csrc/loss.hip; retrieval._gd_direct) ------------------------------
  * SquareLoss: r = yhat - y (y float32 or float64, promoted), r_scaled = r * scale, and the

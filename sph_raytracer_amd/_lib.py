@@ -67,6 +67,8 @@ _SIGNATURES = [
     ('sphrt_solve_f32', c_int, [c_vp, ctypes.POINTER(RayBatch), c_int, c_vp, c_vp, c_vp, c_vp]),
     ('sphrt_trace_reference', c_int, [c_vp, ctypes.POINTER(RayBatch), c_int, c_vp, c_vp, c_vp,
                                       c_vp, c_vp, ctypes.c_size_t, c_vp]),
+    ('sphrt_trace_reference_emit', c_int, [c_vp, ctypes.POINTER(RayBatch), c_int, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp]),
     ('sphrt_trace_workspace_bytes', ctypes.c_size_t, [c_vp, c_i64]),
     ('sphrt_trace_count', c_int, [c_vp, ctypes.POINTER(RayBatch), c_vp, c_vp, ctypes.c_size_t,
                                   c_vp]),
@@ -108,6 +110,8 @@ _SIGNATURES = [
     ('sphrt_csr_transpose', c_int, [ctypes.POINTER(CSR), c_i64, c_vp, c_vp, c_vp, c_vp,
                                     ctypes.c_size_t, c_vp]),
     ('sphrt_f64_to_f32', c_int, [c_vp, c_vp, c_i64, c_vp]),
+    ('sphrt_gather_f32', c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    ('sphrt_gather_f64', c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     ('sphrt_loss_partials', c_i64, [c_i64]),
     ('sphrt_sq_residual_f64', c_int, [c_vp, c_vp, c_int, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp]),
     ('sphrt_neg_reg_f64', c_int, [c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp]),

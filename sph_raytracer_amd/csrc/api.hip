@@ -114,6 +114,26 @@ __global__ __launch_bounds__(256) void f64_to_f32_kernel(const double* src, floa
         dst[i] = (float)src[i];
 }
 
+// dst[i] = src[idx[i]]: 4 consecutive outputs per thread (one 16-byte index load, 4 gathers,
+// their stores), one pass, no grid-stride loop (the ~1 MB gathers this serves fit one wave of
+// workgroups).
+template <typename T>
+__global__ __launch_bounds__(256) void gather_kernel(const T* __restrict__ src,
+                                                     const int32_t* __restrict__ idx, int64_t n,
+                                                     T* __restrict__ dst) {
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i0 + 4 <= n && ((uintptr_t)(idx + i0) & 15) == 0) {
+        const int4 q = *reinterpret_cast<const int4*>(idx + i0);
+        const T a = src[q.x], b = src[q.y], c = src[q.z], d = src[q.w];
+        dst[i0] = a;
+        dst[i0 + 1] = b;
+        dst[i0 + 2] = c;
+        dst[i0 + 3] = d;
+    } else {
+        for (int64_t i = i0; i < n && i < i0 + 4; ++i) dst[i] = src[idx[i]];
+    }
+}
+
 static unsigned grid_for(int64_t n, int64_t per_block, int64_t cap) {
     int64_t g = (n + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -304,4 +324,25 @@ extern "C" int sphrt_f64_to_f32(const double* src, float* dst, int64_t n, void* 
     hipLaunchKernelGGL(f64_to_f32_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
                        (hipStream_t)stream, src, dst, n);
     return check_launch("f64_to_f32");
+}
+
+template <typename T>
+static int gather(const T* src, const int32_t* idx, int64_t n, T* dst, void* stream) {
+    if (n < 0) return fail("negative gather length");
+    if (n == 0) return 0;
+    if (!src || !idx || !dst) return fail("null gather argument");
+    StreamGuard guard(stream);
+    const int64_t blocks = (n + 1023) / 1024;
+    if (blocks > INT32_MAX) return fail("gather too large");
+    hipLaunchKernelGGL(gather_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                       src, idx, n, dst);
+    return check_launch("gather_kernel");
+}
+extern "C" int sphrt_gather_f32(const float* src, const int32_t* idx, int64_t n, float* dst,
+                                void* stream) {
+    return gather(src, idx, n, dst, stream);
+}
+extern "C" int sphrt_gather_f64(const double* src, const int32_t* idx, int64_t n, double* dst,
+                                void* stream) {
+    return gather(src, idx, n, dst, stream);
 }

@@ -1285,9 +1285,10 @@ using AccumOf = typename std::conditional<sizeof(T) == 4, float, double>::type;
 // Every segment reads its density in the phase that holds its granule (the other phase reads
 // the zero granule) and keeps that value: the sums are unchanged, bit for bit.
 constexpr int kHalfTab = kGranEarly * kThreads;   // = the early DMA rounds' entries (768)
+constexpr int kOutStage = 2048;                   // dense output range staged in LDS (elements)
 
 template <typename T, typename L, int MODE, typename TabT = int32_t, bool EDMA = false,
-          int P = kPer, bool RUNS = false, bool HALF = false>
+          int P = kPer, bool RUNS = false, bool HALF = false, bool DENSE = false>
 __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_kernel(
     const int64_t* __restrict__ blocks, const int32_t* __restrict__ vox,
     const uint16_t* __restrict__ loc, const TabT* __restrict__ tab, const L* __restrict__ len,
@@ -1341,11 +1342,47 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     // RUNS has no early exit for blocks without rows (below): an empty pass range instead, so
     // no pass runs (a pass over an empty window would still close "the last row" at its end)
     if (RUNS && s0 >= s1) s1 = base0;
-    if (MODE == kFwdGather && fallback_only && n_tab >= 0) return;
+    // fallback_only: the per-segment gather launch for the blocks a table launch skipped.
+    // DENSE: dense output ranges (sphrt_csr.order bit 2, below) — instantiations of their own,
+    // so that the other launches carry none of its code (with it as a run-time switch the
+    // forwards measured C2 f32 5.9 -> 6.0 us, C5 f32 24.8 -> 26.7 us on one box)
+    static_assert(!DENSE || (!RUNS && MODE != kFwdDynamic), "dense ranges: no runs, no slices");
+    const bool fb_only = fallback_only != 0;
+    constexpr bool dense = DENSE;
+    if (MODE == kFwdGather && fb_only && n_tab >= 0) return;
     // Empty rays integrate to zero: this workgroup's share of the list is fetched now and
     // written at the very end, off the critical path.
     const int64_t e_lo = m[0];
-    const int e_n = (fallback_only || RUNS) ? 0 : (int)(m[1] - e_lo);
+    const int e_n = (fb_only || RUNS || dense) ? 0 : (int)(m[1] - e_lo);
+    // Dense output ranges: the rows are in output order and block fields 0 / 1 hold the output
+    // range [lo, hi) this workgroup owns (its rows and the empty rows up to the next workgroup's
+    // first row): it zeroes the range with contiguous vector stores before any row closes, so
+    // every output line is written by one workgroup (no empty-ray list, no partial lines from
+    // several XCDs).  The closes of the same workgroup follow after a vmcnt(0) and the count
+    // scan's barrier; a block left to the fallback launch zeroes its range here and the later
+    // launch writes its rows.
+    // Table launches stage a dense range of up to kOutStage outputs in LDS behind the granule
+    // image: zeroed, written by the closes, flushed with contiguous stores at the end — each
+    // output line is then written once (zeros and values together).  Larger ranges, and the
+    // fallback launch, zero the range in global memory first.
+    const bool ostaged = MODE == kFwdTable && dense && m[1] - m[0] <= kOutStage;
+    T* ost = dens + ((HALF ? kHalfTab : EDMA ? imax64(tab_stride, kGranEarly * kThreads)
+                                           : tab_stride) + 1) * 4;
+    if (ostaged)
+        for (int j = tid; j < (int)(m[1] - m[0]); j += THR) ost[j] = (T)0;
+    auto put = [&](T* oc, int64_t r, T val) {
+        if (ostaged) ost[r - m[0]] = val;
+        else oc[r] = val;
+    };
+    auto zero_range = [&]() {
+        const int64_t lo = m[0], hi = m[1];
+        constexpr int E = 16 / (int)sizeof(T);             // elements per 16-byte store
+        const int64_t a = imin64((lo + E - 1) / E * E, hi), b = imax64(hi / E * E, a);
+        if (tid < a - lo) out[lo + tid] = (T)0;
+        if (tid < hi - b) out[b + tid] = (T)0;
+        uint4* ov = reinterpret_cast<uint4*>(out);
+        for (int64_t q = a / E + tid; q < b / E; q += THR) ov[q] = make_uint4(0u, 0u, 0u, 0u);
+    };
     // (unconditional load: empty_ray holds n_rays + 1 entries; a predicated load would make
     // the wait-count model drain every load before the granule DMA)
     constexpr int kEmptyLoads = RUNS ? 0 : 1;
@@ -1384,7 +1421,8 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     // exit path, the compiler sank the table-entry and chunk loads below the block record's
     // arrival, serialising one more round trip in front of every workgroup.
     if (!RUNS && s0 >= s1) {
-        zero_empty();
+        if (dense) zero_range();
+        else zero_empty();
         return;
     }
     const int32_t g_full = (int32_t)imin64(n_cols >> 2, INT32_MAX);   // whole granules
@@ -1417,6 +1455,10 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     if (local && EDMA && !HALF)   // rounds past the early ones (tables of more than 768 granules)
         stage_granules_late<T, TabT, THR>(density, tab_b, kEarlyRounds<T, THR>, (int)n_tab, g_full,
                                           dens);
+    if (dense && !ostaged) {      // (uniform) zeros before any close of this workgroup
+        zero_range();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     int64_t rbase = 0;                            // rows started in earlier passes
 #pragma clang loop unroll(disable)   // (also no peeling: one copy of the pass body)
     for (int64_t c = 0; c < nc; ++c) {
@@ -1581,15 +1623,15 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
                 if (base == base0 && first >= 0 && first < P) cmask &= ~(1u << first);
                 if (base + kPass >= s1 && end > 0 && end <= P) cmask |= 1u << P;
             }
-            if ((cmask >> h1) & 1) oc[r_prev] = (T)(run0 + (Stitch)qa);
-            if (h2 != h1 && ((cmask >> h2) & 1)) oc[r_first] = (T)v1;
-            if (h3 != h2 && ((cmask >> h3) & 1)) oc[r_second] = (T)v2;
+            if ((cmask >> h1) & 1) put(oc, r_prev, (T)(run0 + (Stitch)qa));
+            if (h2 != h1 && ((cmask >> h2) & 1)) put(oc, r_first, (T)v1);
+            if (h3 != h2 && ((cmask >> h3) & 1)) put(oc, r_second, (T)v2);
             if (hcount > 2) {                         // rare: closes of the fourth and later runs
                 A q = (A)0;
                 int rank = 0;
 #pragma unroll
                 for (int k = 0; k <= P; ++k) {
-                    if (k > h3 && ((cmask >> k) & 1)) oc[row_of(rank - 1)] = (T)q;
+                    if (k > h3 && ((cmask >> k) & 1)) put(oc, row_of(rank - 1), (T)q);
                     if (k < P) {
                         const bool h = (hmask >> k) & 1;
                         rank += h;
@@ -1600,6 +1642,12 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
             carry = tot_has ? tot_sum : carry + tot_sum;
             rbase += pass_heads;
         }
+    }
+    if (ostaged) {                // the staged range out with contiguous stores
+        lds_barrier();
+        const int64_t lo = m[0], hi = m[1];
+        for (int j = tid; j < (int)(hi - lo); j += THR) out[lo + j] = ost[j];
+        return;
     }
     zero_empty();
 }
@@ -1991,7 +2039,12 @@ template <typename T>
 static bool use_tables(const sphrt_csr* c, const T* density, int64_t n_chan, int64_t chan_stride,
                        int64_t div) {
     if (!c->loc || !c->tab || c->n_cols <= 0 || div > 0) return false;
-    if (c->tab_stride < 1 || (size_t)(c->tab_stride + 1) * 4 * sizeof(T) > kTableLdsMax) return false;
+    // (+ the staged output range of dense output ranges, which the granule image leaves room for)
+    const size_t extra = (c->order & 4) ? (size_t)kOutStage * sizeof(T) : 0;
+    if (c->tab_stride < 1 ||
+        (size_t)(imax64(c->tab_stride, kGranEarly * kThreads) + 1) * 4 * sizeof(T) + extra >
+            kTableLdsMax)
+        return false;
     if ((uintptr_t)density % (4 * sizeof(T)) != 0) return false;
     if (n_chan > 1 && chan_stride % 4 != 0) return false;
     return true;
@@ -2054,6 +2107,9 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
 #define FWD_ARGS(TabT, D, CS, COLS) c->blocks, c->vox, c->loc, (const TabT*)c->tab, len,    \
                        c->row_ray, c->empty_ray, D, n_chan, CS, div, out, ocs, c->n_rays,          \
                        c->n_segments, COLS, c->tab_stride, chunk
+    if ((c->order & 4) && (n_chan != 1 || div > 0 || c->runs))
+        return fail("dense output ranges need one channel, no time slices and no run records");
+    const bool dense = (c->order & 4) != 0;        // (instantiations with DENSE)
     const T* td = sm.on ? (const T*)c->stage : density;      // what the table kernel gathers
     const int64_t tcs = sm.on ? c->stage_cols : chan_stride;
     if (div > 0) {
@@ -2081,13 +2137,15 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
         size_t lds = (size_t)((half ? kHalfTab
                                : edma ? imax64(c->tab_stride, kGranEarly * kThreads)
                                       : c->tab_stride) + 1) * 4 * sizeof(T);   // + zero granule
-#define FWD_TABLE(TabT, E, R, H)                                                            \
-        FWD_LAUNCH((forward_kernel<T, L, kFwdTable, TabT, E, P, R, H>), grid, block, lds, st, \
+        if (dense) lds += (size_t)kOutStage * sizeof(T);       // the staged output range
+#define FWD_TABLE(TabT, E, R, H, D)                                                         \
+        FWD_LAUNCH((forward_kernel<T, L, kFwdTable, TabT, E, P, R, H, D>), grid, block, lds, st, \
                    FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
 #define FWD_TABLE_R(TabT, E, H)                                                             \
         do {                                                                                      \
-            if (c->runs) FWD_TABLE(TabT, E, true, H);                                       \
-            else FWD_TABLE(TabT, E, false, H);                                              \
+            if (dense) FWD_TABLE(TabT, E, false, H, true);                                  \
+            else if (c->runs) FWD_TABLE(TabT, E, true, H, false);                           \
+            else FWD_TABLE(TabT, E, false, H, false);                                       \
         } while (0)
 #define FWD_TABLE_E(TabT)                                                                   \
         do {                                                                                      \
@@ -2109,13 +2167,24 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
 #undef FWD_TABLE
         if (c->n_fallback > 0) {   // (natural vox, natural density)
             if (int e = check_launch("forward_kernel<table>")) return e;
-            hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0,
-                               st, FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 1,
-                               nullptr);
+            if (dense)
+                hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P, false, false,
+                                                   true>), grid, block, 0, st,
+                                   FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 1, nullptr);
+            else
+                hipLaunchKernelGGL((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block,
+                                   0, st, FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 1,
+                                   nullptr);
         }
     } else {
-        FWD_LAUNCH((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0, st,
-                   FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0, (const int32_t*)nullptr);
+        if (dense)
+            FWD_LAUNCH((forward_kernel<T, L, kFwdGather, int32_t, false, P, false, false, true>), grid,
+                       block, 0, st, FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0,
+                       (const int32_t*)nullptr);
+        else
+            FWD_LAUNCH((forward_kernel<T, L, kFwdGather, int32_t, false, P>), grid, block, 0, st,
+                       FWD_ARGS(int32_t, density, chan_stride, c->n_cols), 0,
+                       (const int32_t*)nullptr);
     }
 #undef FWD_ARGS
     return check_launch(sizeof(T) == 4 ? "forward_kernel<f32>" : "forward_kernel<f64>");

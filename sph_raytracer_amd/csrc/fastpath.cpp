@@ -26,6 +26,7 @@ namespace {
 using ForwardFn = int (*)(const void* csr, const void* density, int64_t n_chan, int64_t chan_stride,
                           int64_t div, void* out, int64_t ocs, void* stream);
 using LastErrorFn = const char* (*)();
+using GatherFn = int (*)(const void* src, const int32_t* idx, int64_t n, void* dst, void* stream);
 
 struct Binding {
     std::vector<int64_t> in_sizes;   // density shape this binding serves
@@ -38,6 +39,7 @@ struct Binding {
     int64_t stage_bytes;             // > 0: brick-staged CSR, a stage buffer of this size per call
     at::Tensor perm;                 // defined: the input is read as input.view(-1)[perm] (the
                                      // adjoint of a trace in another ray order: y in trace order)
+    GatherFn gather = nullptr;       // sphrt_gather_f32/_f64 for perm (else index_select)
 };
 
 struct Bindings {
@@ -79,10 +81,10 @@ PyObject* py_new(PyObject*, PyObject* arg) {
 }
 
 // add(capsule, in_sizes, is_f64, device, fn_address, csr_address, n_chan, n_vox, div, n, out_shape,
-//     stage_bytes[, perm])
+//     stage_bytes[, perm[, gather_address]])
 PyObject* py_add(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-    if (nargs != 12 && nargs != 13) {
-        PyErr_SetString(PyExc_TypeError, "add() takes 12 or 13 arguments");
+    if (nargs < 12 || nargs > 14) {
+        PyErr_SetString(PyExc_TypeError, "add() takes 12 to 14 arguments");
         return nullptr;
     }
     auto* b = static_cast<Bindings*>(PyCapsule_GetPointer(args[0], kCapsule));
@@ -100,12 +102,20 @@ PyObject* py_add(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
     if (PyErr_Occurred() || !int_tuple(args[10], x.out_shape)) return nullptr;
     x.stage_bytes = PyLong_AsLongLong(args[11]);
     if (PyErr_Occurred()) return nullptr;
-    if (nargs == 13 && args[12] != Py_None) {
+    if (nargs >= 13 && args[12] != Py_None) {
         if (!THPVariable_Check(args[12])) {
             PyErr_SetString(PyExc_TypeError, "perm: a device index tensor or None");
             return nullptr;
         }
         x.perm = THPVariable_Unpack(args[12]);
+        if (nargs == 14 && args[13] != Py_None) {
+            x.gather = reinterpret_cast<GatherFn>(PyLong_AsVoidPtr(args[13]));
+            if (PyErr_Occurred()) return nullptr;
+            if (x.perm.scalar_type() != at::kInt) {
+                PyErr_SetString(PyExc_TypeError, "perm: int32 for the gather entry point");
+                return nullptr;
+            }
+        }
     }
     if (!x.fn || !x.csr) {
         PyErr_SetString(PyExc_ValueError, "null forward entry point or CSR");
@@ -145,7 +155,19 @@ PyObject* py_forward(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
         if (x.dtype != dt || x.device != dev || !sizes.equals(x.in_sizes)) continue;
         at::Tensor out = at::empty(x.out_shape, d.options());
         void* stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
-        const at::Tensor src = x.perm.defined() ? d.reshape({-1}).index_select(0, x.perm) : d;
+        at::Tensor src = d;
+        if (x.perm.defined() && x.gather && d.numel() == x.perm.numel()) {
+            src = at::empty({d.numel()}, d.options());
+            if (x.gather(d.const_data_ptr(), x.perm.const_data_ptr<int32_t>(), d.numel(),
+                         src.mutable_data_ptr(), stream) != 0) {
+                const std::string msg = std::string("sphrt_gather: ") +
+                                        (b->last_error ? b->last_error() : "failed");
+                PyErr_SetString(PyExc_RuntimeError, msg.c_str());
+                return nullptr;
+            }
+        } else if (x.perm.defined()) {
+            src = d.reshape({-1}).index_select(0, x.perm);
+        }
         const void* csr = x.csr;
         sphrt_csr staged;
         at::Tensor stage;      // this call's brick stage (caching allocator, current stream)

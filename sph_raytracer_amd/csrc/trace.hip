@@ -1700,8 +1700,8 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
     const uint64_t below = lanemask_lt(lane);
     const int r_lim = 2 * G.nbr, e_lim = 2 * G.nbr + 2 * G.nbe;
     const int64_t count = exact_count<ALL>(R, o);
-    for (int64_t q = blockIdx.x; q < count; q += gridDim.x) {
-        const int64_t ray = exact_ray<ALL>(o, q);
+    // one ray: its candidate list, the emulated introsort, the walk (uniform over the workgroup)
+    auto trace_ray = [&](const int64_t ray) {
         double x[3], d[3];
         int s[3];
         load_ray(R, ray, x, d, s);
@@ -1725,9 +1725,7 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
                 exact_walk<MODE, T, F, INV>(G, o, ray, s, v);
             }
             __syncthreads();
-            continue;
-        }
-        if (wid == 0) {
+            return;
         }
         // ---- partition phase (uniform control flow per wave) ----
         // the top levels, breadth-first: range w of level l splits into ranges w and w + 2^l
@@ -1786,8 +1784,6 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
             }
         }
         __syncthreads();
-        if (wid == 0) {
-        }
         // ---- final insertion sort = stable sort inside each leaf, as ranks ----
         for (int p = tid; p < K; p += 64 * W) {
             const uint32_t code = leaf[p];
@@ -1805,8 +1801,45 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
         // (the pre-sort list and the left-stop list are free now: compacted segments go there)
         if (wid == 0) exact_walk_wave<MODE, T, F, INV>(G, o, ray, s, ts, ps, lpos, tk, lane);
         __syncthreads();
-        if (wid == 0) {
+    };
+    if constexpr (ALL && !INV && W == 1) {
+        // The reference-mode trace of every ray, screened 64 rays at a time (one per lane): a
+        // ray that starts outside every shell (start region r < 0) and crosses no sphere (every
+        // sphere_solve distance +inf, in the trace's precision) keeps r < 0 for every segment
+        // before its first infinite entry, and every segment from there on is infinite or NaN:
+        // all masked (raytracer.py:155-173), no segment.  Only the others take the exact path.
+        // (invalid=True keeps those segments: no screen.)
+        for (int64_t q0 = (int64_t)blockIdx.x * 64; q0 < count; q0 += (int64_t)gridDim.x * 64) {
+            const int64_t my = q0 + lane;
+            bool need = false;
+            if (my < count) {
+                double x[3], d[3];
+                int s[3];
+                load_ray(R, my, x, d, s);
+                need = s[0] >= 0;
+                if (!need) {
+                    const RayGeoT<F> g = exact_geo<F>(x, d);
+                    for (int j = 0; j < G.nbr && !need; ++j) {
+                        F ti, to;
+                        int ri, ro, ni, no;
+                        sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
+                        need = __builtin_isfinite(ti) || __builtin_isfinite(to);
+                    }
+                }
+                if (!need) {
+                    if (MODE == MODE_COUNT) o.counts[my] = 0;
+                    if (MODE == MODE_EMIT) (void)emit_slot(o, my, 0, true);
+                }
+            }
+            uint64_t m = __ballot(need);
+            while (m) {
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                trace_ray(q0 + l);
+            }
         }
+    } else {
+        for (int64_t q = blockIdx.x; q < count; q += gridDim.x) trace_ray(exact_ray<ALL>(o, q));
     }
 }
 
@@ -2123,8 +2156,10 @@ extern "C" int sphrt_solve_f32(const sphrt_plan* plan, const sphrt_rays* rays, i
 // emulated libstdc++ introsort, the forward fill and diff over the whole list — with the solves
 // and the length differences in the trace's precision and, for invalid=True, no masking.  These
 // options are outside every fast path (whose pruning — the outer-sphere span, the start-voxel
-// rules, the wedge — relies on float64 distances and on the masks); they cost one exact-path pass
-// per ray (count, then fill).
+// rules, the wedge — relies on float64 distances and on the masks).  One pass
+// (sphrt_trace_reference_emit: every ray into a slot of K segments, then a compaction) or two
+// (count, then fill); without invalid=True the rays that cannot keep a segment are screened out
+// (exact_wave_kernel), which at C2 is ~82 % of them.
 template <int MODE, typename F, bool INV>
 static int launch_reference(const GridDev& G, const RaysDev& R, TraceOut<double> o,
                             void* workspace, size_t workspace_size, hipStream_t st) {
@@ -2147,6 +2182,34 @@ static int launch_reference(const GridDev& G, const RaysDev& R, TraceOut<double>
                            dim3(64), 0, st, G, R, o, scratch);
     }
     return check_launch("exact_kernel (reference mode)");
+}
+
+extern "C" int sphrt_trace_reference_emit(const sphrt_plan* plan, const sphrt_rays* rays,
+                                          int flags, const int64_t* bound_ptr, int32_t* counts,
+                                          int32_t* svox, double* slen, int64_t* n_over,
+                                          void* workspace, size_t workspace_size, void* stream) {
+    GridDev G;
+    RaysDev R;
+    if (int e = resolve(plan, rays, G, R, stream)) return e;
+    DeviceGuard guard(plan->device);
+    if (flags & ~(SPHRT_TRACE_F32 | SPHRT_TRACE_INVALID | SPHRT_TRACE_FRESH_RAYS))
+        return fail("unknown trace flags %d", flags);
+    if (!bound_ptr || !counts || !svox || !slen || !n_over) return fail("null emit argument");
+    R.fresh = (flags & SPHRT_TRACE_FRESH_RAYS) != 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(n_over, 0, sizeof(int64_t), st) != hipSuccess) return fail("memset failed");
+    TraceOut<double> o{};
+    o.row_ptr = bound_ptr;
+    o.counts = counts;
+    o.vox = svox;
+    o.len = slen;
+    o.n_over = (unsigned long long*)n_over;
+    const bool f32 = (flags & SPHRT_TRACE_F32) != 0, inv = (flags & SPHRT_TRACE_INVALID) != 0;
+    if (f32)
+        return inv ? launch_reference<MODE_EMIT, float, true>(G, R, o, workspace, workspace_size, st)
+                   : launch_reference<MODE_EMIT, float, false>(G, R, o, workspace, workspace_size, st);
+    return inv ? launch_reference<MODE_EMIT, double, true>(G, R, o, workspace, workspace_size, st)
+               : launch_reference<MODE_EMIT, double, false>(G, R, o, workspace, workspace_size, st);
 }
 
 extern "C" int sphrt_trace_reference(const sphrt_plan* plan, const sphrt_rays* rays, int flags,

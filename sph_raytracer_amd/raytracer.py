@@ -769,6 +769,42 @@ def _call_forward(fn, desc, d, n_chan, cs, div, out, ocs, dev):
     del stage
 
 
+def _dense_ranges(desc, blocks, row_list, n_out):
+    """Dense output ranges (sphrt_csr.order bit 2) for a CSR whose rows are in output order:
+    block b owns outputs [first row of b, first row of the next block with rows) — the first
+    block from 0, the last to n_out — written into its record's fields 0 / 1 (the empty-list
+    share, unused in this mode), and zeroes that range itself before its row closes.  Every
+    output line is then written by one workgroup: the time-paired transposed adjoint of C4
+    (6.25 M voxel-slice rows, ~70 % of them empty) wrote 47 MB per launch for a 25 MB result
+    through the empty-ray list, its zeros and closes landing in the same lines from different
+    XCDs (profiles/r06_adjoint_c4_pmc.json).  Run records are dropped (their empty ranges
+    describe the list)."""
+    b = blocks.view(-1, _lib.BLOCK_FIELDS)
+    n_rows = max(int(row_list.numel()), 1)
+    has = b[:, 2] < b[:, 3]
+    k0 = b[:, 4].clamp(0, n_rows - 1)
+    first = tr.where(has, row_list[k0].long(), tr.full_like(k0, n_out))
+    first = first.flip(0).cummin(0).values.flip(0)     # rowless blocks: the next block's first
+    lo = first.clone()
+    lo[0] = 0
+    hi = tr.cat((first[1:], first.new_full((1,), n_out)))
+    b[:, 0], b[:, 1] = lo, hi
+    desc.order |= 4
+    desc.runs = None
+
+
+def _gather(src, idx, n, dev):
+    """src[idx] (contiguous float32 / float64 src, int32 idx of n entries) on the current stream
+    of `dev` through sphrt_gather_* — the adjoint's input in trace order (one launch of 4
+    gathers per thread; torch's index_select took 7.5 us for C4's 250,000 rays)."""
+    out = tr.empty(n, dtype=src.dtype, device=dev)
+    lib = _lib.load()
+    fn = lib.sphrt_gather_f32 if src.dtype == tr.float32 else lib.sphrt_gather_f64
+    _lib.check(fn(_lib.ptr(src), _lib.ptr(idx), n, _lib.ptr(out), _lib.stream_of(dev)),
+               'sphrt_gather')
+    return out
+
+
 def _clear_stage(desc):
     for i in range(3):
         desc.stage_shape[i] = desc.stage_brick[i] = 0
@@ -981,6 +1017,7 @@ class Operator:
         self._fast = {}     # (shape, dtype, device) -> bound forward launch (steady-state calls)
         self._fastc = None  # the same bindings inside the CPython entry (csrc/fastpath.cpp)
         self._fastc_T = None  # the adjoint's steady-state bindings (T), same entry
+        self._fastc_A = None  # the time-paired adjoint's (dynamic gradient), same entry
         # 'transpose': deterministic voxel-major adjoint (default; a view <-> time pairing
         # transposes its time-paired CSR); 'atomic': float64 atomics (a cross-check, and the
         # fallback when T * vol does not fit 32-bit columns)
@@ -1121,13 +1158,36 @@ class Operator:
         row_ptr = tr.empty(n + 1, dtype=tr.int64, device=dev)
         tws = _workspace(lib, self._plan, n, dev)
         h, d = self._plan.handle, batch.desc
-        _lib.check(lib.sphrt_trace_reference(h, d, flags, _lib.ptr(counts), None, None, None,
-                                             _lib.ptr(tws), tws.numel(), stream),
-                   'sphrt_trace_reference(count)')
         ws = tr.empty(lib.sphrt_scan_workspace_bytes(n), dtype=tr.uint8, device=dev)
-        _lib.check(lib.sphrt_scan_counts(_lib.ptr(counts), n, _lib.ptr(row_ptr), _lib.ptr(ws),
-                                         stream), 'sphrt_scan_counts')
-        total = int(row_ptr[n].item())
+        K = int(self._plan.K)
+        # one pass into slots of K segments (the walk keeps at most one per list entry), then a
+        # compaction — when the staging fits comfortably; else count, then fill
+        if 0 < n and n * K * 12 <= 0.4 * tr.cuda.mem_get_info(dev)[0]:
+            bound_ptr = tr.arange(n + 1, dtype=tr.int64, device=dev) * K
+            svox = tr.empty(n * K, dtype=tr.int32, device=dev)
+            slen = tr.empty(n * K, dtype=tr.float64, device=dev)
+            over = tr.empty(1, dtype=tr.int64, device=dev)
+            _lib.check(lib.sphrt_trace_reference_emit(
+                h, d, flags, _lib.ptr(bound_ptr), _lib.ptr(counts), _lib.ptr(svox),
+                _lib.ptr(slen), _lib.ptr(over), _lib.ptr(tws), tws.numel(), stream),
+                'sphrt_trace_reference_emit')
+            _lib.check(lib.sphrt_scan_counts(_lib.ptr(counts), n, _lib.ptr(row_ptr),
+                                             _lib.ptr(ws), stream), 'sphrt_scan_counts')
+            total, n_over = tr.stack((row_ptr[n], over[0])).tolist()
+            if n_over == 0:
+                vox, seg_len = _compact_staging(lib, n, row_ptr, total, (bound_ptr, svox, slen),
+                                                dev, stream)
+                del tws, counts, ws, svox, slen, bound_ptr
+                self._index(lib, dev, batch, row_ptr, vox, seg_len, total, None)
+                return
+            del svox, slen, bound_ptr
+        else:
+            _lib.check(lib.sphrt_trace_reference(h, d, flags, _lib.ptr(counts), None, None, None,
+                                                 _lib.ptr(tws), tws.numel(), stream),
+                       'sphrt_trace_reference(count)')
+            _lib.check(lib.sphrt_scan_counts(_lib.ptr(counts), n, _lib.ptr(row_ptr),
+                                             _lib.ptr(ws), stream), 'sphrt_scan_counts')
+            total = int(row_ptr[n].item())
         vox = tr.empty(_seg_alloc(total), dtype=tr.int32, device=dev)
         seg_len = tr.empty(_seg_alloc(total), dtype=tr.float64, device=dev)
         if n > 0:
@@ -1365,8 +1425,11 @@ class Operator:
     def _kernel_name_for(c, d, n_chan, div):
         t = 'float, float' if d.dtype == tr.float32 else 'double, double'
         es = d.element_size()
+        dense = 'true' if c.order & 4 else 'false'     # (dense output ranges, sphrt.h order)
         aligned = d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0)
-        table = (c.loc and div == 0 and 0 < c.tab_stride and (c.tab_stride + 1) * 4 * es <= 64 * 1024
+        extra = 2048 * es if c.order & 4 else 0          # (apply.hip kOutStage)
+        table = (c.loc and div == 0 and 0 < c.tab_stride
+                 and (max(c.tab_stride, 768) + 1) * 4 * es + extra <= 64 * 1024
                  and (c.stage_shape[0] > 0 or aligned))
         if table:   # early granule DMA whenever the table columns are whole granules
             cols = c.stage_cols if c.stage_shape[0] > 0 else c.n_cols
@@ -1376,8 +1439,9 @@ class Operator:
             # float64 half tables (apply.hip kHalfTab = 768 granules per phase)
             half = (es == 8 and edma == 'true' and (c.tab_stride + 1) * 32 > 40 * 1024
                     and c.tab_stride <= 1536 and os.environ.get('SPHRT_FWD_HALF', '1') != '0')
-            return f'forward_kernel<{t}, 0, {tabt}, {edma}, 8, {runs}, {"true" if half else "false"}>'
-        return f'forward_kernel<{t}, {2 if div else 1}, int, false, 8, false, false>'
+            return (f'forward_kernel<{t}, 0, {tabt}, {edma}, 8, {runs}, '
+                    f'{"true" if half else "false"}, {dense}>')
+        return f'forward_kernel<{t}, {2 if div else 1}, int, false, 8, false, false, {dense}>'
 
     def _apply_forward(self, density):
         with tr.cuda.device(self._cdev):      # launches and allocations on the operator's GPU
@@ -1435,11 +1499,12 @@ class Operator:
         shape = [1] * max(0, 3 - len(shape)) + shape
         return (math.prod(shape[:-2]), shape[-2], shape[-1])
 
-    def _transpose_of(self, src, n_cols, vox):
+    def _transpose_of(self, src, n_cols, vox, dense=False):
         """Transpose of the CSR `src` (columns < n_cols; `vox` its column tensor) with its own
         index and granule tables; its columns (rays) are brick-staged in detector tiles for
         multi-wave grids.  Its rows (voxels) are ordered brick by brick (_voxel_rows) and report
-        their voxel through the index's row ids."""
+        their voxel through the index's row ids.  dense (rows in linear order): every workgroup
+        owns a contiguous output range and zeroes it itself (_dense_ranges)."""
         csr = self._csr
         lib, dev = _lib.load(), self._cdev
         stream = _lib.stream_of(dev)
@@ -1492,6 +1557,9 @@ class Operator:
         _set_stage(c, shape3, _stage_brick(nblocks, 'SPHRT_BRICK_T', _BRICK_RAYS)
                    if shape3 else None)
         loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
+        if dense and rows is None:
+            _dense_ranges(c, blocks, vox_list, n_vox)
+            runs = None
         return dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, empty_vox, blocks,
                                   loc, tab, runs, rows))
 
@@ -1527,8 +1595,50 @@ class Operator:
         return csr[key]
 
     def _apply_adjoint(self, y, dshape, ddtype, ddevice, trace_order=False):
+        fa = self._fastc_A
+        if fa is not None and not trace_order and y.dtype == ddtype and ddevice == self._cdev:
+            # steady state of the time-paired adjoint in one C call (y gathered into trace
+            # order and the transposed forward, csrc/fastpath.cpp): the autograd backward of a
+            # dynamic forward and Operator.T(y, time_slices=True) land here
+            out = self._fastfn(fa, y)
+            if out is not None:
+                return out
         with tr.cuda.device(self._cdev):
-            return self._apply_adjoint_on(y, dshape, ddtype, ddevice, trace_order)
+            res = self._apply_adjoint_on(y, dshape, ddtype, ddevice, trace_order)
+            if not trace_order:
+                self._bind_paired_adjoint(y, dshape, res)
+            return res
+
+    def _bind_paired_adjoint(self, y, dshape, res):
+        """Register the steady-state binding of the time-paired adjoint for y's shape / dtype
+        when the general path ran just the gather and the transposed forward: y contiguous on
+        the compute device, float32 / float64, the result there in y's dtype."""
+        csr, dev = self._csr, self._cdev
+        if not (self.grid.dynamic and type(y) is tr.Tensor and y.device == dev
+                and res.device == dev and y.dtype in (tr.float32, tr.float64)
+                and res.dtype == y.dtype and y.is_contiguous()
+                and self.adjoint_mode == 'transpose' and csr is not None
+                and y.numel() == csr['n']):
+            return
+        n_chan, div, _ = self._layout(dshape)
+        paired = csr.get(('paired', dshape[0], div)) if div > 0 else None
+        if paired is None or 'transposed' not in paired:
+            return
+        fast = _lib.load_fast()
+        if fast is None:
+            return
+        tdesc = paired['transposed']['desc']
+        lib = _lib.load()
+        fn = lib.sphrt_forward_f32 if y.dtype == tr.float32 else lib.sphrt_forward_f64
+        gfn = lib.sphrt_gather_f32 if y.dtype == tr.float32 else lib.sphrt_gather_f64
+        if self._fastc_A is None:
+            self._fastfn = fast.forward
+            self._fastc_A = fast.new(_lib.address(lib.sphrt_last_error))
+        perm = csr['ray_id'] if csr['ray_id'] is not None and not self._tcols_geom() else None
+        fast.add(self._fastc_A, tuple(y.shape), y.dtype == tr.float64, dev.index,
+                 _lib.address(fn), ctypes.addressof(tdesc), 1, csr['n'], 0, tdesc.n_rays,
+                 tuple(dshape), _stage_bytes(tdesc, 1, y.element_size()), perm,
+                 _lib.address(gfn))
 
     def _tcols_geom(self):
         """Whether the transposed CSRs of a reordered trace (wedges, view tiles) take their
@@ -1575,13 +1685,14 @@ class Operator:
             cdt = ddtype if ddtype in (tr.float32, tr.float64) else tr.float32
             yv = yv.to(cdt)
             if csr['ray_id'] is not None and not trace_order and not self._tcols_geom():
-                # (its columns are trace rows)
-                yv = yv.view(-1, n).index_select(1, self._ray_id_long()).reshape(-1)
+                # (its columns are trace rows: y gathered into trace order)
+                yv = _gather(yv, csr['ray_id'], n, dev) if yv.numel() == n else \
+                    yv.view(-1, n).index_select(1, self._ray_id_long()).reshape(-1)
             if paired is not None:      # columns of the flattened (T, vol) density
                 if 'transposed' not in paired:
                     paired['transposed'] = self._transpose_of(paired['desc'],
                                                               paired['desc'].n_cols,
-                                                              paired['keep'][0])
+                                                              paired['keep'][0], dense=True)
                 tdesc, n_chan, vol = paired['transposed']['desc'], 1, paired['desc'].n_cols
             else:
                 tdesc = self._transposed()['desc']
@@ -1654,10 +1765,11 @@ class Operator:
             self._fastfn = fast.forward
             self._fastc_T = fast.new(_lib.address(lib.sphrt_last_error))
         vol = math.prod(self.grid.shape[-3:])
+        gfn = lib.sphrt_gather_f32 if y.dtype == tr.float32 else lib.sphrt_gather_f64
         fast.add(self._fastc_T, tuple(y.shape), y.dtype == tr.float64, dev.index,
                  _lib.address(fn), ctypes.addressof(tdesc), 1, csr['n'], 0, vol,
                  tuple(res.shape), _stage_bytes(tdesc, 1, y.element_size()),
-                 None if self._tcols_geom() else csr['ray_id'])
+                 None if self._tcols_geom() else csr['ray_id'], _lib.address(gfn))
 
     # -- compatibility views -----------------------------------------------------------------------
     def _padded(self):

@@ -587,3 +587,36 @@ def test_view_tiles_rule(monkeypatch):
     assert rt._view_tiles((50, 50, 100), False) == (10, 4)
     monkeypatch.setenv('SPHRT_RAY_ORDER', 'vtile:4,2,8')       # several rows: the study path
     assert rt._view_tiles((50, 50, 100), False) is None
+
+
+def test_dense_ranges_partition_the_output():
+    """_dense_ranges (sphrt_csr.order bit 2): block b's output range starts at its first row's
+    output (0 for the first block), ends where the next block with rows starts (n_out for the
+    last), rowless blocks get empty ranges — a partition of [0, n_out) in block order, each
+    block's rows inside its own range."""
+    from sph_raytracer_amd import _lib
+    from sph_raytracer_amd.raytracer import _dense_ranges
+    rng = np.random.default_rng(3)
+    n_out = 500
+    rows = np.sort(rng.choice(n_out, 180, replace=False)).astype(np.int32)   # non-empty outputs
+    # blocks over the rows: k0 per block, some blocks without rows (s0 == s1)
+    k0 = [0, 0, 17, 60, 60, 61, 120, 179]
+    has = [False, True, True, False, True, True, True, True]
+    nb = len(k0)
+    blocks = tr.zeros((nb, _lib.BLOCK_FIELDS), dtype=tr.int64)
+    blocks[:, 4] = tr.tensor(k0)
+    blocks[:, 2] = tr.arange(nb) * 10
+    blocks[:, 3] = blocks[:, 2] + tr.tensor([10 if h else 0 for h in has])
+    desc = _lib.CSR()
+    _dense_ranges(desc, blocks.view(-1), tr.from_numpy(rows), n_out)
+    lo, hi = blocks[:, 0].tolist(), blocks[:, 1].tolist()
+    assert desc.order & 4 and not desc.runs
+    assert lo[0] == 0 and hi[-1] == n_out
+    assert all(hi[b] == lo[b + 1] for b in range(nb - 1))
+    assert all(lo[b] <= hi[b] for b in range(nb))
+    k1 = k0[1:] + [len(rows)]
+    for b in range(nb):
+        if not has[b]:
+            assert lo[b] == hi[b] or b == 0
+        for k in range(k0[b], k1[b] if has[b] else k0[b]):
+            assert lo[b] <= rows[k] < hi[b]

@@ -226,3 +226,35 @@ def test_parallel_geom_operator(gpu):
     got = op.T(tr.from_numpy(case['y0']).to(gpu)).cpu().numpy()
     ref = case['adj64_0']
     assert float(np.abs(got - ref).max() / np.abs(ref).max()) <= 1e-10
+
+
+@pytest.mark.parametrize('mode', ['float32', 'invalid'])
+def test_reference_mode_orbit_sample(mode, gpu):
+    """The reference-mode trace at an orbit's size class (3 views of the C2 orbit: 15,000 rays,
+    50^3 grid): one pass into slots of K segments plus the compaction (sphrt_trace_reference_emit)
+    and, for float32, the screen that skips rays starting outside every shell and crossing no
+    sphere (~80 % of them: no kept segment) — the CSR bit for bit the oracle's restatement of the
+    same options (IEEE sqrt), misses included."""
+    import math
+    from sph_raytracer_amd import ConeRectGeom, Operator, SphericalGrid
+    from sph_raytracer_amd.raytracer import find_starts
+    f32 = mode == 'float32'
+    grid = SphericalGrid(shape=(50, 50, 50))
+    thetas = tr.linspace(0, 2 * math.pi, 50)[[0, 17, 33]]
+    geom = sum(ConeRectGeom((50, 100), pos=(5 * tr.cos(t), 5 * tr.sin(t), 1), fov=(45, 45))
+               for t in thetas)
+    kw = dict(ftype=tr.float32) if f32 else dict(invalid=True)
+    op = Operator(grid, geom, device=gpu, **kw)
+    ptr, vox, seg = (t.cpu().numpy() for t in op.segments())
+    ora = _oracle()
+    g = ora.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy(),
+                                 ftype='float32' if f32 else 'float64')
+    xs = geom.ray_starts.broadcast_to(geom.rays.shape)
+    starts = find_starts(grid, xs, ftype=tr.float32 if f32 else tr.float64).numpy()
+    optr, ovox, oseg = ora.trace_segments(g, xs.numpy(), geom.rays.numpy(), starts,
+                                          invalid=not f32)
+    assert np.array_equal(ptr, optr), f'{mode}: segment counts differ from the oracle'
+    assert np.array_equal(vox, ovox), f'{mode}: voxels differ from the oracle'
+    assert _same_bits(seg, oseg), f'{mode}: lengths differ from the oracle'
+    empty = float((np.diff(ptr) == 0).mean())
+    assert (empty > 0.5) if f32 else (empty == 0.0), empty

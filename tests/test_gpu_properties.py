@@ -452,7 +452,7 @@ def test_half_tables_float64(gpu, monkeypatch):
     gen = tr.Generator().manual_seed(5)
     x = tr.rand((2,) + tuple(grid.shape), dtype=tr.float64, generator=gen)
     xg = x.to(gpu)
-    assert op._forward_kernel_name(xg[0]).endswith('true, true>')
+    assert op._forward_kernel_name(xg[0]).endswith('true, true, false>')   # (half, not dense)
     y = op(xg[0])
     rp, vx, ln = (t.cpu().numpy() for t in op.segments())
     nv = math.prod(grid.shape)
@@ -633,6 +633,11 @@ def test_dynamic_operator_T_time_slices(gpu, dt):
     xg = x.clone().requires_grad_(True)
     (op(xg) * y).sum().backward()
     assert tr.equal(got, xg.grad)
+    # the steady-state binding (csrc/fastpath.cpp: gather into trace order + transposed forward)
+    # serves the later calls: the same bits
+    assert op._fastc_A is not None
+    assert tr.equal(op.T(y, time_slices=True), got)
+    assert tr.equal(op._apply_adjoint(y, tuple(grid.shape), dt, gpu), got)
     # one geometry seen at every time step: slice t = the static adjoint of image t
     single = geom.geoms[0]
     op1 = Operator(grid, single, device=gpu)
