@@ -77,6 +77,11 @@ PyObject* g_coll = nullptr;   // geometry.ViewGeomCollection
 constexpr int64_t kSingleWaveBlocks = 256 * 6;          // _SINGLE_WAVE_BLOCKS
 constexpr int kBrick[3] = {4, 2, 4};                     // _BRICK
 constexpr int64_t kL2Bytes = int64_t(4) << 20;           // _L2_BYTES
+constexpr double kGateWideTables = 0.3;                   // _GATE_WIDE_TABLES
+constexpr double kGateStaged = 0.5;                       // _GATE_STAGED
+constexpr double kStagedSegBytes = 18.0;                  // _STAGED_SEG_BYTES
+constexpr double kGateTraceStaging = 0.4;                 // _GATE_TRACE_STAGING
+constexpr double kStagingSlotBytes = 12.0;                // _STAGING_SLOT_BYTES
 constexpr int64_t kTabWide = SPHRT_TAB_WIDE;
 constexpr int64_t kRunFields = SPHRT_RUN_FIELDS;
 constexpr int64_t kBlockFields = SPHRT_BLOCK_FIELDS;
@@ -693,7 +698,7 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
         const int64_t cap = hv[0];
         size_t free_b = 0, total_b = 0;
         hip_ok(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
-        if ((double)cap * 12 > 0.4 * (double)free_b)   // staging too large: two-pass trace
+        if ((double)cap * kStagingSlotBytes > kGateTraceStaging * (double)free_b)   // two-pass trace
             Py_RETURN_NONE;
         at::Tensor svox = at::empty({std::max<int64_t>(cap, 1)}, on_dev.dtype(at::kInt));
         at::Tensor slen = at::empty({std::max<int64_t>(cap, 1)}, on_dev.dtype(at::kDouble));
@@ -741,8 +746,8 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
         const int64_t cols = c->stage_shape[0] > 0 ? c->stage_cols : c->n_cols;   // _tables_one_pass
         c->tab_bytes = (cols + 3) / 4 <= 65536 ? 2 : 4;
         const double wide_bytes = (double)nblocks * kTabWide * (double)c->tab_bytes;
-        const double need = 18.0 * (double)seg_alloc(total) + wide_bytes;          // _staged_fits
-        if (!(wide_bytes <= 0.3 * (double)free_b) || !(need <= 0.5 * (double)free_b))
+        const double need = kStagedSegBytes * (double)seg_alloc(total) + wide_bytes;  // _staged_fits
+        if (!(wide_bytes <= kGateWideTables * (double)free_b) || !(need <= kGateStaged * (double)free_b))
             Py_RETURN_NONE;                          // compaction first: the Python path
         at::Tensor vox = at::empty({seg_alloc(total)}, on_dev.dtype(at::kInt));
         at::Tensor row_ray = at::empty({std::max<int64_t>(n, 1)}, on_dev.dtype(at::kInt));

@@ -1672,6 +1672,98 @@ __device__ __forceinline__ void exact_heap_range(const SoaList& v, double* tk, u
     wave_sync();
 }
 
+// Reference mode without invalid=True, lists of <= 64 M candidates: the whole list in
+// concatenation order (tk / pk) sorted by (distance, candidate) in registers — composite keys as in
+// the fast path, with the distance's bits mapped to an order-preserving unsigned (negative and
+// infinite distances included) — into ts / ps.  That is the emulated introsort's order up to the
+// order inside groups of equal distances, which the walk reads only where two entries of a group
+// set one region row to different values (the segments inside a group are empty, the group's
+// state after it is the same in any order) or, from the first infinite distance on, not at all
+// (infinite and NaN segments are masked).  False: a NaN distance, two distances the composite
+// keys do not separate, or a group that matters — the caller runs the emulated introsort.  (C2
+// ftype=float32: ~45 k rays reach the exact path after the miss screen; each sorts 256
+// candidates.)  float32 distances never collide in the keys (their low 29 bits are zero).
+__device__ __forceinline__ uint64_t order_bits(double t) {
+    const uint64_t b = (uint64_t)__double_as_longlong(t + 0.0);      // -0 -> +0
+    return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+template <int M>
+__device__ bool network_sort(const GridDev& G, const double* tk, const uint32_t* pk, double* ts,
+                             uint32_t* ps, int K, int lane, const int* s) {
+    const int cbits = 32 - __builtin_clz((unsigned)(K - 1));
+    const uint64_t cmask = (1ull << cbits) - 1ull;
+    uint64_t k[M];
+    bool nan = false;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int e = lane * M + i;
+        k[i] = ~0ull;
+        if (e < K) {
+            const double t = tk[e];
+            nan |= __builtin_isnan(t);
+            k[i] = (order_bits(t) & ~cmask) | (uint64_t)e;
+        }
+    }
+    if (__ballot(nan) != 0) return false;
+    sort_stages<M, 2>(k, lane);
+    double t[M];
+    uint32_t p[M];
+    uint64_t kb[M];
+    int cand[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        cand[i] = (int)(k[i] & cmask);
+        const bool in = lane * M + i < K;
+        t[i] = in ? tk[cand[i]] : kInf;
+        p[i] = in ? pk[cand[i]] : 0u;
+        kb[i] = order_bits(t[i]);
+    }
+    // (distance, candidate) strictly ascending, across the lanes too
+    bool bad = false;
+#pragma unroll
+    for (int i = 1; i < M; ++i)
+        bad |= lane * M + i < K &&
+               (kb[i] < kb[i - 1] || (kb[i] == kb[i - 1] && cand[i] < cand[i - 1]));
+    const uint64_t pk_prev = (uint64_t)__shfl_up((long long)kb[M - 1], 1);
+    const int pc_prev = __shfl_up(cand[M - 1], 1);
+    bad |= lane > 0 && lane * M < K &&
+           (kb[0] < pk_prev || (kb[0] == pk_prev && cand[0] < pc_prev));
+    if (__ballot(bad) != 0) return false;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+        const int e = lane * M + i;
+        if (e < K) {
+            ts[e] = t[i];
+            ps[e] = p[i];
+        }
+    }
+    wave_sync();
+    const int r_lim = 2 * G.nbr, e_lim = 2 * G.nbr + 2 * G.nbe;
+    bool amb = false;
+    for (int e = lane; e + 1 < K; e += 64) {
+        const double te = ts[e];
+        if (!(te >= 0.0 && te < kInf) || ts[e + 1] != te) continue;
+        for (int j = e + 1; j < K && ts[j] == te; ++j)
+            amb |= entries_conflict(ps[e], ps[j], K, r_lim, e_lim, s);
+    }
+    return __ballot(amb) == 0;
+}
+template <bool INV>
+__device__ __forceinline__ bool reference_network(const GridDev& G, const double* tk,
+                                                  const uint32_t* pk, double* ts, uint32_t* ps,
+                                                  int lane, const int* s) {
+    if constexpr (INV) {
+        return false;       // (every list with two infinite distances is a group that matters)
+    } else {
+        const int K = G.K;
+        if (K <= 64) return network_sort<1>(G, tk, pk, ts, ps, K, lane, s);
+        if (K <= 128) return network_sort<2>(G, tk, pk, ts, ps, K, lane, s);
+        if (K <= 256) return network_sort<4>(G, tk, pk, ts, ps, K, lane, s);
+        if (K <= 512) return network_sort<8>(G, tk, pk, ts, ps, K, lane, s);
+        return false;
+    }
+}
+
 // W waves per ray.  The candidates and the leaf ranks are spread over all 64 W lanes; the
 // partitions run breadth-first for log2(W) levels (wave w partitions range w of the level, so
 // the two halves of a partition proceed in parallel), then each wave finishes one of the W
@@ -1718,6 +1810,14 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
             top[2] = 2 * (31 - __builtin_clz((unsigned)max(K, 1)));
         }
         __syncthreads();
+        if constexpr (ALL && W == 1 && !INV) {      // reference mode: the register sort first
+            if (reference_network<INV>(G, tk, pk, ts, ps, lane, s)) {
+                exact_walk_wave<MODE, T, F, INV>(G, o, ray, s, ts, ps, lpos, tk, lane);
+                __syncthreads();
+                return;
+            }
+            __syncthreads();
+        }
         for (int p = tid; p < K; p += 64 * W) nan |= __builtin_isnan(tk[p]) ? 1 : 0;
         if (__syncthreads_or(nan)) {
             if (tid == 0) {

@@ -535,6 +535,15 @@ def _seg_alloc(total):
     return max((total + 15) // 16 * 16, 16)
 
 
+# memory gates of the construction (fractions of the free device memory), shared with the native
+# construction (csrc/construct.cpp kGate*, pinned by tests/test_cpu_api.py)
+_GATE_WIDE_TABLES = 0.3     # one-pass tables: the wide tables' bytes
+_GATE_STAGED = 0.5          # staged table build: final CSR + wide tables
+_STAGED_SEG_BYTES = 18      # its CSR bytes per segment (vox 4 + len 8 + len32 4 + loc 2)
+_GATE_TRACE_STAGING = 0.4   # one-pass trace: its staging
+_STAGING_SLOT_BYTES = 12    # per bound slot (vox 4 + len 8)
+
+
 def _tables_one_pass(desc, nblocks, dev, free=None):
     """Whether _local_tables builds in one pass (wide tables fit comfortably in free memory and
     SPHRT_TABLES is not 'twopass'); decides desc.tab_bytes (16-bit entries when every granule
@@ -543,7 +552,8 @@ def _tables_one_pass(desc, nblocks, dev, free=None):
     desc.tab_bytes = 2 if (cols + 3) // 4 <= 65536 else 4
     wide_bytes = nblocks * _lib.TAB_WIDE * desc.tab_bytes
     return (os.environ.get('SPHRT_TABLES', 'onepass') != 'twopass' and
-            wide_bytes <= 0.3 * (tr.cuda.mem_get_info(dev)[0] if free is None else free))
+            wide_bytes <= _GATE_WIDE_TABLES * (tr.cuda.mem_get_info(dev)[0] if free is None
+                                               else free))
 
 
 def _staged_fits(desc, nblocks, total, free):
@@ -553,8 +563,8 @@ def _staged_fits(desc, nblocks, total, free):
     compaction path's staging + 12 B per segment (the staging is freed before the tables).  Taken
     only when the CSR and the wide tables fit in half the free memory; otherwise the staging is
     compacted first (C3 peak 3.04 -> 4.60 GB with the staged build)."""
-    need = 18 * _seg_alloc(total) + nblocks * _lib.TAB_WIDE * desc.tab_bytes
-    return need <= 0.5 * free
+    need = _STAGED_SEG_BYTES * _seg_alloc(total) + nblocks * _lib.TAB_WIDE * desc.tab_bytes
+    return need <= _GATE_STAGED * free
 
 
 def _local_tables(lib, desc, blocks, nblocks, total, dev, stream, staged=None):
@@ -778,7 +788,9 @@ def _dense_ranges(desc, blocks, row_list, n_out):
     (6.25 M voxel-slice rows, ~70 % of them empty) wrote 47 MB per launch for a 25 MB result
     through the empty-ray list, its zeros and closes landing in the same lines from different
     XCDs (profiles/r06_adjoint_c4_pmc.json).  Run records are dropped (their empty ranges
-    describe the list)."""
+    describe the list).  (Closing the rows by block-relative index and expanding them through an
+    occupancy bitmap instead of reading row_ray — 17 MB less per C4 launch — measured the same:
+    26.56 against 26.42 us, profiles/r06_dense_ab_c4.json.)"""
     b = blocks.view(-1, _lib.BLOCK_FIELDS)
     n_rows = max(int(row_list.numel()), 1)
     has = b[:, 2] < b[:, 3]
@@ -855,7 +867,7 @@ def _trace_csr(lib, plan, batch, dev, stream, keep_staging=False):
             _bound_hook(counts[:n])
         scan(counts, bound_ptr)          # (counts holds the bounds until the emit pass)
         cap = int(bound_ptr[n].item())   # host sync 1
-        if cap * 12 <= 0.4 * tr.cuda.mem_get_info(dev)[0]:
+        if cap * _STAGING_SLOT_BYTES <= _GATE_TRACE_STAGING * tr.cuda.mem_get_info(dev)[0]:
             svox = tr.empty(max(cap, 1), dtype=tr.int32, device=dev)
             slen = tr.empty(max(cap, 1), dtype=tr.float64, device=dev)
             over = tr.empty(1, dtype=tr.int64, device=dev)
@@ -1162,7 +1174,7 @@ class Operator:
         K = int(self._plan.K)
         # one pass into slots of K segments (the walk keeps at most one per list entry), then a
         # compaction — when the staging fits comfortably; else count, then fill
-        if 0 < n and n * K * 12 <= 0.4 * tr.cuda.mem_get_info(dev)[0]:
+        if 0 < n and n * K * _STAGING_SLOT_BYTES <= _GATE_TRACE_STAGING * tr.cuda.mem_get_info(dev)[0]:
             bound_ptr = tr.arange(n + 1, dtype=tr.int64, device=dev) * K
             svox = tr.empty(n * K, dtype=tr.int32, device=dev)
             slen = tr.empty(n * K, dtype=tr.float64, device=dev)
@@ -1552,8 +1564,10 @@ class Operator:
         c.row_ray, c.blocks = vox_list.data_ptr(), blocks.data_ptr()
         c.empty_ray = empty_vox.data_ptr()
         c.n_cols = csr['n']
-        # (columns are trace rows: detector tiles only when they are the geometry's rays)
-        shape3 = self._ray_shape3() if csr['ray_id'] is None or geom_cols else None
+        # (columns are trace rows: detector tiles only when they are the geometry's rays; none
+        # for the dense time-paired transpose: a pack launch per call for no kernel gain)
+        shape3 = (self._ray_shape3() if (csr['ray_id'] is None or geom_cols) and not dense
+                  else None)
         _set_stage(c, shape3, _stage_brick(nblocks, 'SPHRT_BRICK_T', _BRICK_RAYS)
                    if shape3 else None)
         loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
@@ -1648,14 +1662,18 @@ class Operator:
         so by the retrieval's residual).  Measured (op.T per step, us; profiles/r05_tcols_*):
         ConeRect orbits take geometry columns (C2 11.7 -> 7.2, C3 214.5 -> 187.2), ConeCirc
         orbits keep trace rows (C5 41.4 against 44.2; its kernel 25.1 / 35.6 us f32 / f64 against
-        28.3-30.8 / 39.7-44.0 with geometry columns and any ray brick).  SPHRT_TCOLS=geom / trace
-        overrides."""
+        28.3-30.8 / 39.7-44.0 with geometry columns and any ray brick).  Dynamic grids (the
+        time-paired transpose, whose columns are never brick-staged) take geometry columns: C4's
+        adjoint call 29.0 -> 25.9 us, the per-call gather of y gone and the kernel unchanged (25.9
+        / 25.7 us; profiles/r06_adjstats_c4*.json).  SPHRT_TCOLS=geom / trace overrides."""
         csr = self._csr
         if csr is None or csr['ray_id'] is None:
             return False
         env = os.environ.get('SPHRT_TCOLS', 'auto')
         if env != 'auto':
             return env == 'geom'
+        if self.grid.dynamic:
+            return True
         geoms = getattr(self.geom, 'geoms', [self.geom])
         return bool(geoms) and all(type(g) is ConeRectGeom for g in geoms)
 

@@ -620,3 +620,24 @@ def test_dense_ranges_partition_the_output():
             assert lo[b] == hi[b] or b == 0
         for k in range(k0[b], k1[b] if has[b] else k0[b]):
             assert lo[b] <= rows[k] < hi[b]
+
+
+def test_native_construction_constants_match_python():
+    """The native cone construction (csrc/construct.cpp) repeats the Python construction's brick,
+    L2 and memory-gate rules: every `constexpr` there that names its Python twin in
+    its comment (`// _NAME`) equals that twin."""
+    from sph_raytracer_amd import raytracer as rt
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            'sph_raytracer_amd', 'csrc', 'construct.cpp')).read()
+    pat = re.compile(r'constexpr\s+\w+\s+(k\w+)(\[3\])?\s*=\s*([^;]+);\s*//\s*(_[A-Z0-9_]+)')
+    seen = set()
+    for cname, arr, val, pyname in pat.findall(src):
+        py = getattr(rt, pyname)
+        if arr:
+            cval = tuple(int(v) for v in val.strip('{} ').split(','))
+        else:
+            cval = eval(val.replace('int64_t', ''), {})
+        assert cval == py, (cname, cval, pyname, py)
+        seen.add(pyname)
+    assert {'_BRICK', '_L2_BYTES', '_SINGLE_WAVE_BLOCKS', '_GATE_WIDE_TABLES', '_GATE_STAGED',
+            '_STAGED_SEG_BYTES', '_GATE_TRACE_STAGING', '_STAGING_SLOT_BYTES'} <= seen

@@ -810,6 +810,33 @@ def test_staged_forward_on_concurrent_streams(gpu, monkeypatch):
             assert tr.equal(outs[0], ref[0]) and tr.equal(outs[1], ref[1])
 
 
+def test_first_float64_use_on_side_stream(gpu):
+    """The float64 segment lengths stay in the trace staging until the first float64 use, which
+    compacts them on the current stream: an operator whose first float64 forward and
+    adjoint run on a side stream — with allocations on the construction stream right after —
+    matches one whose first float64 use ran on the default stream, bitwise."""
+    from sph_raytracer_amd import Operator
+    grid, geom = _orbit(5, (24, 30), grid_shape=(20, 17, 22))
+    g = tr.Generator(device=gpu).manual_seed(11)
+    x = tr.rand(grid.shape, dtype=tr.float64, device=gpu, generator=g)
+    y = tr.rand(tuple(geom.shape), dtype=tr.float64, device=gpu, generator=g)
+    ref_op = Operator(grid, geom, device=gpu)
+    ref_f, ref_a = ref_op(x), ref_op.T(y)
+    for _ in range(3):
+        op = Operator(grid, geom, device=gpu)
+        op(x.float())                            # float32 first: the lengths stay staged
+        s = tr.cuda.Stream(device=gpu)
+        s.wait_stream(tr.cuda.current_stream(gpu))
+        with tr.cuda.stream(s):
+            f = op(x)
+            a = op.T(y)
+        junk = [tr.full((1 << 20,), 7.0, dtype=tr.float64, device=gpu) for _ in range(8)]
+        tr.cuda.current_stream(gpu).wait_stream(s)
+        tr.cuda.synchronize(gpu)
+        del junk
+        assert tr.equal(f, ref_f) and tr.equal(a, ref_a)
+
+
 def test_operator_device_argument(gpu):
     """Operator(device='cuda:k') traces and computes on GPU k whatever device is current (ADVICE
     r1): the compute device follows `device`; with two GPUs an operator built on cuda:1 while
