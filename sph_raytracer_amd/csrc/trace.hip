@@ -1490,14 +1490,15 @@ __device__ void exact_walk_wave(const GridDev& G, const TraceOut<T>& o, int64_t 
 
 // Large K (the wave list does not fit kExactLdsMax): lane 0 sorts the ray's list serially in the
 // wave's slice of workspace.
-// ALL: every ray of R (the reference-mode trace, sphrt_trace_reference), not the deferred list.
+// ALL: the reference-mode trace (sphrt_trace_reference): every ray of R, or with a ray list
+// (o.deferred set: the rays ref_screen_kernel kept) those; else the fast path's deferred list.
 template <bool ALL, typename T>
 __device__ __forceinline__ int64_t exact_count(const RaysDev& R, const TraceOut<T>& o) {
-    return ALL ? R.n : (int64_t)*o.n_deferred;
+    return ALL && !o.deferred ? R.n : (int64_t)*o.n_deferred;
 }
 template <bool ALL, typename T>
 __device__ __forceinline__ int64_t exact_ray(const TraceOut<T>& o, int64_t q) {
-    return ALL ? q : o.deferred[q];
+    return ALL && !o.deferred ? q : o.deferred[q];
 }
 template <typename F>
 __device__ __forceinline__ RayGeoT<F> exact_geo(const double* x, const double* d) {
@@ -1902,45 +1903,7 @@ __global__ __launch_bounds__(64 * W) void exact_wave_kernel(GridDev G, RaysDev R
         if (wid == 0) exact_walk_wave<MODE, T, F, INV>(G, o, ray, s, ts, ps, lpos, tk, lane);
         __syncthreads();
     };
-    if constexpr (ALL && !INV && W == 1) {
-        // The reference-mode trace of every ray, screened 64 rays at a time (one per lane): a
-        // ray that starts outside every shell (start region r < 0) and crosses no sphere (every
-        // sphere_solve distance +inf, in the trace's precision) keeps r < 0 for every segment
-        // before its first infinite entry, and every segment from there on is infinite or NaN:
-        // all masked (raytracer.py:155-173), no segment.  Only the others take the exact path.
-        // (invalid=True keeps those segments: no screen.)
-        for (int64_t q0 = (int64_t)blockIdx.x * 64; q0 < count; q0 += (int64_t)gridDim.x * 64) {
-            const int64_t my = q0 + lane;
-            bool need = false;
-            if (my < count) {
-                double x[3], d[3];
-                int s[3];
-                load_ray(R, my, x, d, s);
-                need = s[0] >= 0;
-                if (!need) {
-                    const RayGeoT<F> g = exact_geo<F>(x, d);
-                    for (int j = 0; j < G.nbr && !need; ++j) {
-                        F ti, to;
-                        int ri, ro, ni, no;
-                        sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
-                        need = __builtin_isfinite(ti) || __builtin_isfinite(to);
-                    }
-                }
-                if (!need) {
-                    if (MODE == MODE_COUNT) o.counts[my] = 0;
-                    if (MODE == MODE_EMIT) (void)emit_slot(o, my, 0, true);
-                }
-            }
-            uint64_t m = __ballot(need);
-            while (m) {
-                const int l = __builtin_ctzll(m);
-                m &= m - 1;
-                trace_ray(q0 + l);
-            }
-        }
-    } else {
-        for (int64_t q = blockIdx.x; q < count; q += gridDim.x) trace_ray(exact_ray<ALL>(o, q));
-    }
+    for (int64_t q = blockIdx.x; q < count; q += gridDim.x) trace_ray(exact_ray<ALL>(o, q));
 }
 
 // ---- one-pass trace: staging slots -> tight CSR ---------------------------------------------
@@ -2260,6 +2223,45 @@ extern "C" int sphrt_solve_f32(const sphrt_plan* plan, const sphrt_rays* rays, i
 // (sphrt_trace_reference_emit: every ray into a slot of K segments, then a compaction) or two
 // (count, then fill); without invalid=True the rays that cannot keep a segment are screened out
 // (exact_wave_kernel), which at C2 is ~82 % of them.
+// The reference-mode screen (without invalid=True), one ray per lane: a ray that starts outside
+// every shell (start region r < 0) and crosses no sphere (every sphere_solve distance +inf, in the
+// trace's precision) keeps r < 0 for every segment before its first infinite entry, and every
+// segment from there on is infinite or NaN: all masked (raytracer.py:155-173), no segment.  The
+// others are listed (o.deferred, one atomic per wave) for the exact path, one wave each over the
+// whole chip.  (invalid=True keeps those segments: no screen.)  In the exact path's kernel the
+// screen took a wave per 64 rays and that wave then traced their ~12 hit rays one after another:
+// C2 ftype=float32 exact kernel 628 us.
+template <int MODE, typename F>
+__global__ __launch_bounds__(256) void ref_screen_kernel(GridDev G, RaysDev R, TraceOut<double> o) {
+    const int64_t my = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    bool need = false;
+    if (my < R.n) {
+        double x[3], d[3];
+        int s[3];
+        load_ray(R, my, x, d, s);
+        need = s[0] >= 0;
+        if (!need) {
+            const RayGeoT<F> g = exact_geo<F>(x, d);
+            for (int j = G.nbr - 1; j >= 0 && !need; --j) {   // (outer shells first: hits stop early)
+                F ti, to;
+                int ri, ro, ni, no;
+                sphere_solve(G, g, j, ti, ri, to, ro, ni, no);
+                need = __builtin_isfinite(ti) || __builtin_isfinite(to);
+            }
+        }
+        if (!need) {
+            if (MODE == MODE_COUNT) o.counts[my] = 0;
+            if (MODE == MODE_EMIT) (void)emit_slot(o, my, 0, true);
+        }
+    }
+    const uint64_t m = __ballot(need);
+    unsigned long long base = 0;
+    if (lane == 0 && m) base = atomicAdd(o.n_deferred, (unsigned long long)__popcll(m));
+    base = (unsigned long long)__shfl((long long)base, 0);
+    if (need) o.deferred[base + __popcll(m & lanemask_lt(lane))] = my;
+}
+
 template <int MODE, typename F, bool INV>
 static int launch_reference(const GridDev& G, const RaysDev& R, TraceOut<double> o,
                             void* workspace, size_t workspace_size, hipStream_t st) {
@@ -2272,6 +2274,12 @@ static int launch_reference(const GridDev& G, const RaysDev& R, TraceOut<double>
     o.n_deferred = (unsigned long long*)ws;
     o.n_heap = (unsigned long long*)(ws + 128);
     if (hipMemsetAsync(ws, 0, kWsHead, st) != hipSuccess) return fail("memset failed");
+    if (!INV) {
+        o.deferred = (int64_t*)(ws + kWsHead);
+        hipLaunchKernelGGL((ref_screen_kernel<MODE, F>), dim3((unsigned)((R.n + 255) / 256)),
+                           dim3(256), 0, st, G, R, o);
+        if (int e = check_launch("ref_screen_kernel")) return e;
+    }
     if (exact_in_lds(G)) {
         const int64_t blocks = R.n < 4 * kExactBlocks ? R.n : 4 * kExactBlocks;
         hipLaunchKernelGGL((exact_wave_kernel<MODE, double, F, INV, true>), dim3((unsigned)blocks),
