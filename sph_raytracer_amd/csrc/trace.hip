@@ -1970,6 +1970,16 @@ __global__ __launch_bounds__(256) void compact_kernel(int64_t n, const int64_t* 
     }
 }
 
+// Grids whose K-entry list does not fit a wave's LDS: every screened hit ray goes to the exact
+// path (the deferred list; its serial kernel keeps each list in the workspace).
+template <typename T>
+__global__ __launch_bounds__(256) void defer_hits_kernel(TraceOut<T> o) {
+    const int64_t n = (int64_t)*o.n_hits;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        o.deferred[i] = o.hits[i].ray;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *o.n_deferred = (unsigned long long)n;
+}
+
 // ---- host launchers ----------------------------------------------------------------------
 static int trace_cap(const GridDev& G) { return ((G.K + 63) / 64) * 64; }
 constexpr int kExactBlocks = 4096;   // one workgroup per deferred ray, 16 per CU
@@ -2019,12 +2029,13 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
                     workspace_bytes(G, R.n));
     const int cap = trace_cap(G);
     // one LDS list of K entries per wave: 4 waves per workgroup, fewer for large K (a workgroup
-    // may hold all 160 KiB of a CU's LDS), K <= 13653 with one wave
+    // may hold all 160 KiB of a CU's LDS), K <= 13653 with one wave; larger K (e.g. ~6800+
+    // shells) sends every hit ray through the exact path, its list in the workspace
     const size_t per_wave = (size_t)cap * (sizeof(uint64_t) + sizeof(uint32_t));
     int waves = kWavesPerBlock;
     while (waves > 1 && (size_t)waves * per_wave > kLdsBytes) waves >>= 1;
     const size_t lds = (size_t)waves * per_wave;
-    if (lds > kLdsBytes) return fail("grid too large for the per-wave LDS list (K=%d > 13653)", G.K);
+    const bool wave_list = lds <= kLdsBytes;
     unsigned char* ws = (unsigned char*)workspace;
     o.n_deferred = (unsigned long long*)ws;
     o.n_hits = (unsigned*)(ws + 64);
@@ -2047,11 +2058,16 @@ static int launch_trace(const GridDev& G, const RaysDev& R, TraceOut<T> o, void*
     }
     if constexpr (MODE == MODE_BOUND) return 0;
     if (!(steps & kTrace)) return 0;
-    // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
-    const int64_t grid = kTraceGrid * kWavesPerBlock / waves;
-    hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds, st, G,
-                       o, cap);
-    if (int e = check_launch("trace_kernel")) return e;
+    if (wave_list) {
+        // enough waves to fill the chip several times over; each drains hits[w], hits[w + W], ...
+        const int64_t grid = kTraceGrid * kWavesPerBlock / waves;
+        hipLaunchKernelGGL((trace_kernel<MODE, T>), dim3((unsigned)grid), dim3(64 * waves), lds,
+                           st, G, o, cap);
+        if (int e = check_launch("trace_kernel")) return e;
+    } else {
+        hipLaunchKernelGGL((defer_hits_kernel<T>), dim3(256), dim3(256), 0, st, o);
+        if (int e = check_launch("defer_hits_kernel")) return e;
+    }
     if (exact_multi_wave(G))
         hipLaunchKernelGGL((exact_wave_kernel<MODE, T, double, false, false, kExactWaves>),
                            dim3(kExactBlocks), dim3(64 * kExactWaves),

@@ -270,3 +270,25 @@ def test_c5_full_forward_and_adjoint_vs_oracle(c5, gpu):
     assert tuple(desc.stage_brick) == (0, 0, 0) and desc.n_blocks > 256 * 6
     assert op._csr['ray_id'] is not None
     _static_forward_adjoint(grid, geom, op, ref, n_vox, gpu, 51, 'C5')
+
+
+def test_large_k_trace_vs_oracle(gpu):
+    """A grid whose candidate list (K = 2 (nr + 1) + 2 (ne + 1) + (na + 1) + 1 = 14 017) outgrows one
+    wave's LDS list (K <= 13 653): every hit ray goes through the exact path with its list in the
+    workspace (the reference materialises any K, raytracer.py:92-173).  Segments of every ray
+    against the oracle, the forward against the oracle's line integrals."""
+    from sph_raytracer_amd import ConeRectGeom, Operator, SphericalGrid
+    grid = SphericalGrid(shape=(7000, 3, 5))
+    geom = sum(ConeRectGeom((6, 8), pos=(3 * tr.cos(th), 3 * tr.sin(th), 0.5), fov=(40, 40))
+               for th in tr.linspace(0, 2 * tr.pi, 3))
+    op = Operator(grid, geom, device=gpu)
+    assert op._csr['total'] > 0
+    ref, n_vox = _oracle_trace(grid, geom)
+    _compare_all(ref, _gpu_views(op, 3), 5.1, 'large K')
+    g = tr.Generator().manual_seed(7)
+    x = tr.rand(tuple(grid.shape), dtype=tr.float64, generator=g)
+    ptr, vox, seg = _flat(ref)
+    xv = x.numpy().reshape(-1)
+    want = np.array([float(np.sum(xv[vox[a:b]] * seg[a:b])) for a, b in zip(ptr[:-1], ptr[1:])])
+    got = op(x.to(gpu)).cpu().numpy().reshape(-1)
+    assert np.allclose(got, want, rtol=1e-10, atol=1e-12)
