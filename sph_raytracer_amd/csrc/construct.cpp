@@ -1,4 +1,5 @@
-// construct.cpp — the float64 Operator construction over cone-beam detectors in one C++ call.
+// construct.cpp — the float64 Operator construction in one C++ call (cone-beam detectors:
+// build_cone; any other geometry from its host starts and directions: build_rays).
 //
 // Host code only (no kernels): part of the CPython entry _sphrt_fast.so (csrc/fastpath.cpp); the
 // device work is libsphrt.so's C ABI (include/sphrt.h), resolved from the library the Python
@@ -298,6 +299,8 @@ bool sorted_finite(const at::Tensor& b) {
     return b.numel() >= 2;
 }
 
+bool grid_prelude(PyObject* const* grid_b, const int64_t* nbins, Prelude& P);
+
 // geom + grid boundaries -> the trace's host values; false (no error set): not this sequence
 bool prelude(PyObject* geom, PyObject* const* grid_b, const int64_t* nbins, Prelude& P) {
     std::vector<PyObject*> views;
@@ -392,8 +395,12 @@ bool prelude(PyObject* geom, PyObject* const* grid_b, const int64_t* nbins, Prel
         xs = vs[0].pos.unsqueeze(0).unsqueeze(0);
     }
     P.xs = xs.to(at::kDouble).contiguous();
+    return grid_prelude(grid_b, nbins, P);
+}
 
-    // _Plan: boundaries in float64 (the fast trace's dtype), trig tables with torch CPU
+// _Plan and _RayBatch.host_starts for starts P.xs: boundaries in float64 (the fast trace's
+// dtype), trig tables with torch CPU, start voxels; false: not this sequence
+bool grid_prelude(PyObject* const* grid_b, const int64_t* nbins, Prelude& P) {
     at::Tensor b[3];
     for (int k = 0; k < 3; ++k) {
         if (!THPVariable_Check(grid_b[k])) return false;
@@ -457,6 +464,24 @@ PyObject* wrap(at::Tensor t) {
     return THPVariable_Wrap(std::move(t));
 }
 
+struct PlanGuard {
+    sphrt_plan* p = nullptr;
+    ~PlanGuard() {
+        if (p) g_lib.plan_destroy(p);
+    }
+};
+
+// What the common part of a construction starts from: the plan (owned by the guard), the ray
+// batch over the staged starts and the device rays, and what the Operator keeps of them.
+struct Batch {
+    sphrt_rays rd{};
+    int64_t n = 0;
+    at::Tensor rays;                // device rays (released once traced)
+    at::Tensor ray_id;              // the geometry ray of each trace row, or undefined
+    at::Tensor xs_keep;             // the staged starts (kept: debug_los)
+    std::vector<int64_t> rshape;    // the Operator's ray shape
+};
+
 bool prelude_args(PyObject* const* args, int64_t* nbins) {
     for (int k = 0; k < 3; ++k) {
         nbins[k] = PyLong_AsLongLong(args[4 + k]);
@@ -466,6 +491,9 @@ bool prelude_args(PyObject* const* args, int64_t* nbins) {
 }
 
 }  // namespace
+
+PyObject* build_tail(PlanGuard& guard, Batch& B, const int64_t* nbins, int64_t n_cols,
+                     sphrt_csr* c, hipStream_t stream, const at::TensorOptions& on_dev);
 
 // bind(lib_path, ConeRectGeom, ConeCircGeom, ViewGeomCollection)
 PyObject* construct_bind(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
@@ -579,12 +607,7 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
     const int64_t n_cols = PyLong_AsLongLong(args[9]);
     auto* c = static_cast<sphrt_csr*>(PyLong_AsVoidPtr(args[10]));
     if (PyErr_Occurred()) return nullptr;
-    struct PlanGuard {
-        sphrt_plan* p = nullptr;
-        ~PlanGuard() {
-            if (p) g_lib.plan_destroy(p);
-        }
-    } guard;
+    PlanGuard guard;
     try {
         Prelude P;
         if (!prelude(args[0], args + 1, nbins, P)) {
@@ -658,15 +681,17 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
                   "sphrt_rays_cone");
         }
         // _RayBatch over the staged starts (broadcast against the rays, raytracer.py:76-80)
-        const at::Tensor xs_keep = staged.narrow(0, S.offs[s_xs], nbytes(P.xs))
-                                       .view(at::kDouble).view(P.xs.sizes());
+        Batch B;
+        B.xs_keep = staged.narrow(0, S.offs[s_xs], nbytes(P.xs)).view(at::kDouble).view(P.xs.sizes());
+        const at::Tensor& xs_keep = B.xs_keep;
         // tiles: the view starts (V, 1, 1, 3) as (1, 1, V / tv, tv, 1, 3) over the tile layout
         const at::Tensor xs_b = tiled ? xs_keep.reshape({1, 1, P.n_views / tv, tv, 1, 3}) : xs_keep;
         if ((int64_t)bshape.size() > SPHRT_MAX_DIMS) Py_RETURN_NONE;
-        sphrt_rays rd{};
+        sphrt_rays& rd = B.rd;
         rd.ndim = (int32_t)bshape.size();
-        const auto xs_str = xs_b.expand(full).strides();
-        const auto ry_str = rays.strides();
+        // (the strides copied out: an IntArrayRef of a temporary's strides dangles)
+        const std::vector<int64_t> xs_str = xs_b.expand(full).strides().vec();
+        const std::vector<int64_t> ry_str = rays.strides().vec();
         for (size_t i = 0; i < bshape.size(); ++i) {
             rd.shape[i] = bshape[i];
             rd.xs_stride[i] = xs_str[i];
@@ -676,147 +701,249 @@ PyObject* construct_build_cone(PyObject*, PyObject* const* args, Py_ssize_t narg
         rd.rays = rays.const_data_ptr<double>();
         rd.start = (const int32_t*)dptr(s_st);
 
-        // _trace_csr, one pass: bound -> scan -> [sync] -> emit -> scan -> [sync]
-        at::Tensor counts = at::empty({std::max<int64_t>(n, 1)}, on_dev.dtype(at::kInt));
-        at::Tensor row_ptr = at::empty({n + 1}, on_dev.dtype(at::kLong));
-        at::Tensor ws = at::empty({(int64_t)g_lib.scan_workspace_bytes(n)}, on_dev.dtype(at::kByte));
-        at::Tensor tws = at::empty({(int64_t)g_lib.trace_workspace_bytes(plan, n)},
-                                   on_dev.dtype(at::kByte));
-        at::Tensor bound_ptr = at::empty({n + 1}, on_dev.dtype(at::kLong));
-        check(g_lib.trace_bound(plan, &rd, counts.data_ptr<int32_t>(), tws.data_ptr(),
-                                (size_t)tws.numel(), stream), "sphrt_trace_bound");
-        check(g_lib.scan_counts(counts.data_ptr<int32_t>(), n, bound_ptr.data_ptr<int64_t>(),
-                                ws.data_ptr(), stream), "sphrt_scan_counts");
-        at::Tensor pin = at::empty({4}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
-        int64_t* hv = pin.mutable_data_ptr<int64_t>();
-        auto hip_ok = [](hipError_t e, const char* what) {
-            if (e != hipSuccess) throw LibError{std::string(what) + ": " + hipGetErrorString(e)};
-        };
-        hip_ok(hipMemcpyAsync(hv, bound_ptr.data_ptr<int64_t>() + n, 8, hipMemcpyDeviceToHost,
-                              stream), "hipMemcpyAsync");
-        hip_ok(hipStreamSynchronize(stream), "hipStreamSynchronize");
-        const int64_t cap = hv[0];
-        size_t free_b = 0, total_b = 0;
-        hip_ok(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
-        if ((double)cap * kStagingSlotBytes > kGateTraceStaging * (double)free_b)   // two-pass trace
-            Py_RETURN_NONE;
-        at::Tensor svox = at::empty({std::max<int64_t>(cap, 1)}, on_dev.dtype(at::kInt));
-        at::Tensor slen = at::empty({std::max<int64_t>(cap, 1)}, on_dev.dtype(at::kDouble));
-        at::Tensor over = at::empty({1}, on_dev.dtype(at::kLong));
-        check(g_lib.trace_emit(plan, &rd, bound_ptr.data_ptr<int64_t>(), counts.data_ptr<int32_t>(),
-                               svox.data_ptr<int32_t>(), slen.data_ptr<double>(),
-                               over.data_ptr<int64_t>(), tws.data_ptr(), (size_t)tws.numel(),
-                               stream), "sphrt_trace_emit");
-        check(g_lib.scan_counts(counts.data_ptr<int32_t>(), n, row_ptr.data_ptr<int64_t>(),
-                                ws.data_ptr(), stream), "sphrt_scan_counts");
-        hip_ok(hipMemcpyAsync(hv, row_ptr.data_ptr<int64_t>() + n, 8, hipMemcpyDeviceToHost,
-                              stream), "hipMemcpyAsync");
-        hip_ok(hipMemcpyAsync(hv + 1, over.data_ptr<int64_t>(), 8, hipMemcpyDeviceToHost, stream),
-               "hipMemcpyAsync");
-        hip_ok(hipStreamSynchronize(stream), "hipStreamSynchronize");
-        const int64_t total = hv[0], n_over = hv[1];
-        g_lib.plan_destroy(guard.p);    // (the trace has run: the plan is not needed again)
-        guard.p = nullptr;
-        if (n_over != 0) Py_RETURN_NONE;   // a ray over its bound: the Python path's fill pass
-        tws.reset();
-        counts.reset();
-        over.reset();
-        ws.reset();
-        rays.reset();                   // trace input only
+        B.n = n;
+        B.rays = rays;
+        rays.reset();
+        B.ray_id = ray_id;
+        B.rshape = rshape;
+        return build_tail(guard, B, nbins, n_cols, c, stream, on_dev);
+    } catch (const LibError& e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what.c_str());
+    } catch (const std::exception& e) {
+        PyErr_SetString(PyExc_RuntimeError, e.what());
+    }
+    return nullptr;
+}
 
-        // Operator._index, staged: blocks, brick staging, table width, memory gates
-        const int64_t nblocks = g_lib.csr_blocks(total);
-        *c = sphrt_csr{};
-        c->n_rays = n;
-        c->n_segments = total;
-        c->n_blocks = nblocks;
-        c->n_cols = n_cols;
-        if (nblocks > kSingleWaveBlocks && 4 * n_cols > kL2Bytes) {   // _stage_brick, _set_stage
-            int64_t cols = 1;
-            for (int i = 0; i < 3; ++i) cols *= (nbins[i] + kBrick[i] - 1) / kBrick[i] * kBrick[i];
-            if (cols < (int64_t(1) << 31) - 1) {
-                for (int i = 0; i < 3; ++i) {
-                    c->stage_shape[i] = (int32_t)nbins[i];
-                    c->stage_brick[i] = kBrick[i];
-                }
-                c->stage_cols = cols;
+
+// _trace_csr's one-pass trace and _index's staged table build over a ray batch (the device
+// sequence both constructions share).  Throws LibError; None: a branch the Python path handles.
+PyObject* build_tail(PlanGuard& guard, Batch& B, const int64_t* nbins, int64_t n_cols,
+                     sphrt_csr* c, hipStream_t stream, const at::TensorOptions& on_dev) {
+    const int64_t n = B.n;
+    // _trace_csr, one pass: bound -> scan -> [sync] -> emit -> scan -> [sync]
+    at::Tensor counts = at::empty({std::max<int64_t>(n, 1)}, on_dev.dtype(at::kInt));
+    at::Tensor row_ptr = at::empty({n + 1}, on_dev.dtype(at::kLong));
+    at::Tensor ws = at::empty({(int64_t)g_lib.scan_workspace_bytes(n)}, on_dev.dtype(at::kByte));
+    at::Tensor tws = at::empty({(int64_t)g_lib.trace_workspace_bytes(guard.p, n)},
+                               on_dev.dtype(at::kByte));
+    at::Tensor bound_ptr = at::empty({n + 1}, on_dev.dtype(at::kLong));
+    check(g_lib.trace_bound(guard.p, &B.rd, counts.data_ptr<int32_t>(), tws.data_ptr(),
+                            (size_t)tws.numel(), stream), "sphrt_trace_bound");
+    check(g_lib.scan_counts(counts.data_ptr<int32_t>(), n, bound_ptr.data_ptr<int64_t>(),
+                            ws.data_ptr(), stream), "sphrt_scan_counts");
+    at::Tensor pin = at::empty({4}, at::TensorOptions().dtype(at::kLong).pinned_memory(true));
+    int64_t* hv = pin.mutable_data_ptr<int64_t>();
+    auto hip_ok = [](hipError_t e, const char* what) {
+        if (e != hipSuccess) throw LibError{std::string(what) + ": " + hipGetErrorString(e)};
+    };
+    hip_ok(hipMemcpyAsync(hv, bound_ptr.data_ptr<int64_t>() + n, 8, hipMemcpyDeviceToHost,
+                          stream), "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    const int64_t cap = hv[0];
+    size_t free_b = 0, total_b = 0;
+    hip_ok(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
+    if ((double)cap * kStagingSlotBytes > kGateTraceStaging * (double)free_b)   // two-pass trace
+        Py_RETURN_NONE;
+    at::Tensor svox = at::empty({std::max<int64_t>(cap, 1)}, on_dev.dtype(at::kInt));
+    at::Tensor slen = at::empty({std::max<int64_t>(cap, 1)}, on_dev.dtype(at::kDouble));
+    at::Tensor over = at::empty({1}, on_dev.dtype(at::kLong));
+    check(g_lib.trace_emit(guard.p, &B.rd, bound_ptr.data_ptr<int64_t>(), counts.data_ptr<int32_t>(),
+                           svox.data_ptr<int32_t>(), slen.data_ptr<double>(),
+                           over.data_ptr<int64_t>(), tws.data_ptr(), (size_t)tws.numel(),
+                           stream), "sphrt_trace_emit");
+    check(g_lib.scan_counts(counts.data_ptr<int32_t>(), n, row_ptr.data_ptr<int64_t>(),
+                            ws.data_ptr(), stream), "sphrt_scan_counts");
+    hip_ok(hipMemcpyAsync(hv, row_ptr.data_ptr<int64_t>() + n, 8, hipMemcpyDeviceToHost,
+                          stream), "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(hv + 1, over.data_ptr<int64_t>(), 8, hipMemcpyDeviceToHost, stream),
+           "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    const int64_t total = hv[0], n_over = hv[1];
+    g_lib.plan_destroy(guard.p);    // (the trace has run: the plan is not needed again)
+    guard.p = nullptr;
+    if (n_over != 0) Py_RETURN_NONE;   // a ray over its bound: the Python path's fill pass
+    tws.reset();
+    counts.reset();
+    over.reset();
+    ws.reset();
+    B.rays.reset();                 // trace input only
+
+    // Operator._index, staged: blocks, brick staging, table width, memory gates
+    const int64_t nblocks = g_lib.csr_blocks(total);
+    *c = sphrt_csr{};
+    c->n_rays = n;
+    c->n_segments = total;
+    c->n_blocks = nblocks;
+    c->n_cols = n_cols;
+    if (nblocks > kSingleWaveBlocks && 4 * n_cols > kL2Bytes) {   // _stage_brick, _set_stage
+        int64_t cols = 1;
+        for (int i = 0; i < 3; ++i) cols *= (nbins[i] + kBrick[i] - 1) / kBrick[i] * kBrick[i];
+        if (cols < (int64_t(1) << 31) - 1) {
+            for (int i = 0; i < 3; ++i) {
+                c->stage_shape[i] = (int32_t)nbins[i];
+                c->stage_brick[i] = kBrick[i];
             }
+            c->stage_cols = cols;
         }
-        hip_ok(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
-        const int64_t cols = c->stage_shape[0] > 0 ? c->stage_cols : c->n_cols;   // _tables_one_pass
-        c->tab_bytes = (cols + 3) / 4 <= 65536 ? 2 : 4;
-        const double wide_bytes = (double)nblocks * kTabWide * (double)c->tab_bytes;
-        const double need = kStagedSegBytes * (double)seg_alloc(total) + wide_bytes;  // _staged_fits
-        if (!(wide_bytes <= kGateWideTables * (double)free_b) || !(need <= kGateStaged * (double)free_b))
-            Py_RETURN_NONE;                          // compaction first: the Python path
-        at::Tensor vox = at::empty({seg_alloc(total)}, on_dev.dtype(at::kInt));
-        at::Tensor row_ray = at::empty({std::max<int64_t>(n, 1)}, on_dev.dtype(at::kInt));
-        at::Tensor empty_ray = at::empty({n + 1}, on_dev.dtype(at::kInt));
-        at::Tensor blocks = at::empty({kBlockFields * nblocks}, on_dev.dtype(at::kLong));
-        at::Tensor nz_row = at::empty({std::max<int64_t>(n, 1)}, on_dev.dtype(at::kInt));
-        {
-            at::Tensor iws = at::empty({(int64_t)g_lib.csr_index_workspace_bytes(n)},
-                                       on_dev.dtype(at::kByte));
-            check(g_lib.csr_index_staged(row_ptr.data_ptr<int64_t>(), n, row_ray.data_ptr<int32_t>(),
-                                         empty_ray.data_ptr<int32_t>(), blocks.data_ptr<int64_t>(),
-                                         nblocks,
-                                         ray_id.defined() ? ray_id.data_ptr<int32_t>() : nullptr,
-                                         nz_row.data_ptr<int32_t>(), iws.data_ptr(), stream),
-                  "sphrt_csr_index_staged");
-        }
-        at::Tensor len32 = at::empty({seg_alloc(total)}, on_dev.dtype(at::kFloat));
-        c->row_ptr = row_ptr.data_ptr<int64_t>();
-        c->vox = vox.data_ptr<int32_t>();
-        c->len = nullptr;
-        c->len32 = len32.data_ptr<float>();
-        c->row_ray = row_ray.data_ptr<int32_t>();
-        c->blocks = blocks.data_ptr<int64_t>();
-        c->empty_ray = empty_ray.data_ptr<int32_t>();
+    }
+    hip_ok(hipMemGetInfo(&free_b, &total_b), "hipMemGetInfo");
+    const int64_t cols = c->stage_shape[0] > 0 ? c->stage_cols : c->n_cols;   // _tables_one_pass
+    c->tab_bytes = (cols + 3) / 4 <= 65536 ? 2 : 4;
+    const double wide_bytes = (double)nblocks * kTabWide * (double)c->tab_bytes;
+    const double need = kStagedSegBytes * (double)seg_alloc(total) + wide_bytes;  // _staged_fits
+    if (!(wide_bytes <= kGateWideTables * (double)free_b) || !(need <= kGateStaged * (double)free_b))
+        Py_RETURN_NONE;                          // compaction first: the Python path
+    at::Tensor vox = at::empty({seg_alloc(total)}, on_dev.dtype(at::kInt));
+    at::Tensor row_ray = at::empty({std::max<int64_t>(n, 1)}, on_dev.dtype(at::kInt));
+    at::Tensor empty_ray = at::empty({n + 1}, on_dev.dtype(at::kInt));
+    at::Tensor blocks = at::empty({kBlockFields * nblocks}, on_dev.dtype(at::kLong));
+    at::Tensor nz_row = at::empty({std::max<int64_t>(n, 1)}, on_dev.dtype(at::kInt));
+    {
+        at::Tensor iws = at::empty({(int64_t)g_lib.csr_index_workspace_bytes(n)},
+                                   on_dev.dtype(at::kByte));
+        check(g_lib.csr_index_staged(row_ptr.data_ptr<int64_t>(), n, row_ray.data_ptr<int32_t>(),
+                                     empty_ray.data_ptr<int32_t>(), blocks.data_ptr<int64_t>(),
+                                     nblocks,
+                                     B.ray_id.defined() ? B.ray_id.data_ptr<int32_t>() : nullptr,
+                                     nz_row.data_ptr<int32_t>(), iws.data_ptr(), stream),
+              "sphrt_csr_index_staged");
+    }
+    at::Tensor len32 = at::empty({seg_alloc(total)}, on_dev.dtype(at::kFloat));
+    c->row_ptr = row_ptr.data_ptr<int64_t>();
+    c->vox = vox.data_ptr<int32_t>();
+    c->len = nullptr;
+    c->len32 = len32.data_ptr<float>();
+    c->row_ray = row_ray.data_ptr<int32_t>();
+    c->blocks = blocks.data_ptr<int64_t>();
+    c->empty_ray = empty_ray.data_ptr<int32_t>();
 
-        // _local_tables, staged: run records, one-pass tables moved out of the staging, pack
-        at::Tensor stats = at::empty({3}, on_dev.dtype(at::kLong));
-        at::Tensor runs;
-        if (nblocks > kSingleWaveBlocks && n < (int64_t(1) << 31)) {
-            runs = at::empty({kRunFields * nblocks}, on_dev.dtype(at::kInt));
-            check(g_lib.csr_runs(c, runs.data_ptr<int32_t>(), stats.data_ptr<int64_t>() + 2, stream),
-                  "sphrt_csr_runs");
-        } else {
-            stats.narrow(0, 2, 1).fill_(1);
-        }
-        at::Tensor loc = at::empty({seg_alloc(total)}, on_dev.dtype(at::kShort));
-        const at::ScalarType tdt = c->tab_bytes == 2 ? at::kShort : at::kInt;
-        at::Tensor wide = at::empty({nblocks * kTabWide}, on_dev.dtype(tdt));
-        check(g_lib.csr_local_build_staged(c, blocks.data_ptr<int64_t>(),
-                                           (uint16_t*)loc.data_ptr(), wide.data_ptr(),
-                                           stats.data_ptr<int64_t>(), bound_ptr.data_ptr<int64_t>(),
-                                           nz_row.data_ptr<int32_t>(), svox.data_ptr<int32_t>(),
-                                           slen.data_ptr<double>(), stream),
-              "sphrt_csr_local_build_staged");
-        hip_ok(hipMemcpyAsync(hv, stats.data_ptr<int64_t>(), 24, hipMemcpyDeviceToHost, stream),
-               "hipMemcpyAsync");
-        hip_ok(hipStreamSynchronize(stream), "hipStreamSynchronize");
-        const int64_t n_fallback = hv[0], max_tab = hv[1], runs_over = hv[2];
-        if (runs_over) runs.reset();
-        const int64_t stride = std::max<int64_t>(64, (max_tab + 63) / 64 * 64);
-        at::Tensor tab = at::empty({nblocks * stride + 3 * 256}, on_dev.dtype(tdt));
-        check(g_lib.csr_local_pack(c, blocks.data_ptr<int64_t>(), wide.data_ptr(), tab.data_ptr(),
-                                   stride, stream), "sphrt_csr_local_pack");
-        wide.reset();
-        svox.reset();
-        nz_row.reset();
-        c->n_fallback = n_fallback;
-        c->tab_stride = stride;
-        c->loc = (uint16_t*)loc.data_ptr();
-        c->tab = tab.data_ptr();
-        c->runs = runs.defined() ? runs.data_ptr<int32_t>() : nullptr;
+    // _local_tables, staged: run records, one-pass tables moved out of the staging, pack
+    at::Tensor stats = at::empty({3}, on_dev.dtype(at::kLong));
+    at::Tensor runs;
+    if (nblocks > kSingleWaveBlocks && n < (int64_t(1) << 31)) {
+        runs = at::empty({kRunFields * nblocks}, on_dev.dtype(at::kInt));
+        check(g_lib.csr_runs(c, runs.data_ptr<int32_t>(), stats.data_ptr<int64_t>() + 2, stream),
+              "sphrt_csr_runs");
+    } else {
+        stats.narrow(0, 2, 1).fill_(1);
+    }
+    at::Tensor loc = at::empty({seg_alloc(total)}, on_dev.dtype(at::kShort));
+    const at::ScalarType tdt = c->tab_bytes == 2 ? at::kShort : at::kInt;
+    at::Tensor wide = at::empty({nblocks * kTabWide}, on_dev.dtype(tdt));
+    check(g_lib.csr_local_build_staged(c, blocks.data_ptr<int64_t>(),
+                                       (uint16_t*)loc.data_ptr(), wide.data_ptr(),
+                                       stats.data_ptr<int64_t>(), bound_ptr.data_ptr<int64_t>(),
+                                       nz_row.data_ptr<int32_t>(), svox.data_ptr<int32_t>(),
+                                       slen.data_ptr<double>(), stream),
+          "sphrt_csr_local_build_staged");
+    hip_ok(hipMemcpyAsync(hv, stats.data_ptr<int64_t>(), 24, hipMemcpyDeviceToHost, stream),
+           "hipMemcpyAsync");
+    hip_ok(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    const int64_t n_fallback = hv[0], max_tab = hv[1], runs_over = hv[2];
+    if (runs_over) runs.reset();
+    const int64_t stride = std::max<int64_t>(64, (max_tab + 63) / 64 * 64);
+    at::Tensor tab = at::empty({nblocks * stride + 3 * 256}, on_dev.dtype(tdt));
+    check(g_lib.csr_local_pack(c, blocks.data_ptr<int64_t>(), wide.data_ptr(), tab.data_ptr(),
+                               stride, stream), "sphrt_csr_local_pack");
+    wide.reset();
+    svox.reset();
+    nz_row.reset();
+    c->n_fallback = n_fallback;
+    c->tab_stride = stride;
+    c->loc = (uint16_t*)loc.data_ptr();
+    c->tab = tab.data_ptr();
+    c->runs = runs.defined() ? runs.data_ptr<int32_t>() : nullptr;
 
-        PyObject* shape_t = PyTuple_New((Py_ssize_t)rshape.size());
-        for (size_t i = 0; i < rshape.size(); ++i)
-            PyTuple_SET_ITEM(shape_t, i, PyLong_FromLongLong(rshape[i]));
-        return Py_BuildValue("(NNNNNNNNNNNNNLLN)", wrap(row_ptr), wrap(vox), wrap(len32),
-                             wrap(row_ray), wrap(empty_ray), wrap(blocks), wrap(loc), wrap(tab),
-                             wrap(runs), wrap(ray_id), wrap(bound_ptr), wrap(slen),
-                             wrap(xs_keep), (long long)total, (long long)nblocks, shape_t);
+    PyObject* shape_t = PyTuple_New((Py_ssize_t)B.rshape.size());
+    for (size_t i = 0; i < B.rshape.size(); ++i)
+        PyTuple_SET_ITEM(shape_t, i, PyLong_FromLongLong(B.rshape[i]));
+    return Py_BuildValue("(NNNNNNNNNNNNNLLN)", wrap(row_ptr), wrap(vox), wrap(len32),
+                         wrap(row_ray), wrap(empty_ray), wrap(blocks), wrap(loc), wrap(tab),
+                         wrap(runs), wrap(B.ray_id), wrap(bound_ptr), wrap(slen),
+                         wrap(B.xs_keep), (long long)total, (long long)nblocks, shape_t);
+}
+
+// build_rays(xs, rays, r_b, e_b, a_b, nr, ne, na, n_cols, csr_address) -> as build_cone | None:
+// the same construction for any other geometry (ParallelGeom, an arbitrary ViewGeom, their
+// collections) from its float64 host starts and directions (geom.ray_starts / geom.rays,
+// broadcast against each other, raytracer.py:76-80): the starts, their voxels, the rays and the
+// plan tables in one host-to-device copy, then build_cone's device sequence.  Geometry order
+// (the trace orders are for cone detectors): no ray ids.
+PyObject* construct_build_rays(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+    if (nargs != 10 || !g_bound) {
+        PyErr_SetString(PyExc_TypeError, "build_rays(xs, rays, r_b, e_b, a_b, nr, ne, na, n_cols, "
+                                         "csr_address) after bind");
+        return nullptr;
+    }
+    int64_t nbins[3];
+    for (int k = 0; k < 3; ++k) {
+        nbins[k] = PyLong_AsLongLong(args[5 + k]);
+        if (nbins[k] == -1 && PyErr_Occurred()) return nullptr;
+    }
+    const int64_t n_cols = PyLong_AsLongLong(args[8]);
+    auto* c = static_cast<sphrt_csr*>(PyLong_AsVoidPtr(args[9]));
+    if (PyErr_Occurred()) return nullptr;
+    if (!THPVariable_Check(args[0]) || !THPVariable_Check(args[1])) Py_RETURN_NONE;
+    PlanGuard guard;
+    try {
+        const at::Tensor xs_in = THPVariable_Unpack(args[0]), ry_in = THPVariable_Unpack(args[1]);
+        if (!xs_in.device().is_cpu() || !ry_in.device().is_cpu() ||
+            xs_in.scalar_type() != at::kDouble || ry_in.scalar_type() != at::kDouble ||
+            xs_in.dim() < 1 || ry_in.dim() < 1 || xs_in.size(-1) != 3 || ry_in.size(-1) != 3)
+            Py_RETURN_NONE;
+        std::vector<int64_t> full;
+        try {
+            full = at::infer_size(xs_in.sizes(), ry_in.sizes());
+        } catch (const std::exception&) {
+            Py_RETURN_NONE;                          // (the Python path raises the error)
+        }
+        std::vector<int64_t> bshape(full.begin(), full.end() - 1);
+        int64_t n = 1;
+        for (int64_t v : bshape) n *= v;
+        if (bshape.empty() || (int64_t)bshape.size() > SPHRT_MAX_DIMS || n <= 0) Py_RETURN_NONE;
+        Prelude P;
+        P.xs = xs_in.contiguous();
+        if (!grid_prelude(args + 2, nbins, P)) {
+            if (PyErr_Occurred()) return nullptr;
+            Py_RETURN_NONE;
+        }
+        const at::Tensor ry_h = ry_in.contiguous();
+        const int dev = (int)c10::hip::current_device();
+        hipStream_t stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)dev).stream();
+        const at::TensorOptions on_dev = at::TensorOptions().device(at::kCUDA, dev);
+        const int64_t tbytes = (int64_t)g_lib.plan_table_bytes(&P.desc);
+        at::Tensor tables = at::empty({tbytes}, at::kByte);
+        check(g_lib.plan_pack_tables(&P.desc, tables.mutable_data_ptr()), "sphrt_plan_pack_tables");
+        Slots S;
+        const int s_tab = S.add(tables.const_data_ptr(), tbytes);
+        const int s_xs = S.add(P.xs.const_data_ptr(), nbytes(P.xs));
+        const int s_st = S.add(P.st.const_data_ptr(), nbytes(P.st));
+        const int s_ry = S.add(ry_h.const_data_ptr(), nbytes(ry_h));
+        at::Tensor host = at::empty({S.size}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+        S.write(host.mutable_data_ptr<uint8_t>());
+        const at::Tensor staged = host.to(on_dev.dtype(at::kByte), /*non_blocking=*/true);
+        auto dptr = [&](int slot) { return (uint8_t*)staged.data_ptr() + S.offs[slot]; };
+        check(g_lib.plan_create_external(&P.desc, dev, dptr(s_tab), &guard.p),
+              "sphrt_plan_create_external");
+        Batch B;
+        B.xs_keep = staged.narrow(0, S.offs[s_xs], nbytes(P.xs)).view(at::kDouble).view(P.xs.sizes());
+        const at::Tensor rays = staged.narrow(0, S.offs[s_ry], nbytes(ry_h)).view(at::kDouble)
+                                    .view(ry_h.sizes());
+        const std::vector<int64_t> xs_str = B.xs_keep.expand(full).strides().vec();
+        const std::vector<int64_t> ry_str = rays.expand(full).strides().vec();
+        B.rd.ndim = (int32_t)bshape.size();
+        for (size_t i = 0; i < bshape.size(); ++i) {
+            B.rd.shape[i] = bshape[i];
+            B.rd.xs_stride[i] = xs_str[i];
+            B.rd.rays_stride[i] = ry_str[i];
+        }
+        B.rd.xs = B.xs_keep.const_data_ptr<double>();
+        B.rd.rays = rays.const_data_ptr<double>();
+        B.rd.start = (const int32_t*)dptr(s_st);
+        B.n = n;
+        B.rshape = bshape;
+        return build_tail(guard, B, nbins, n_cols, c, stream, on_dev);
     } catch (const LibError& e) {
         PyErr_SetString(PyExc_RuntimeError, e.what.c_str());
     } catch (const std::exception& e) {

@@ -202,6 +202,7 @@ namespace sphrt_fast {   // csrc/construct.cpp
 PyObject* construct_bind(PyObject*, PyObject* const*, Py_ssize_t);
 PyObject* construct_cone_host(PyObject*, PyObject* const*, Py_ssize_t);
 PyObject* construct_build_cone(PyObject*, PyObject* const*, Py_ssize_t);
+PyObject* construct_build_rays(PyObject*, PyObject* const*, Py_ssize_t);
 }  // namespace sphrt_fast
 
 namespace {
@@ -217,6 +218,8 @@ PyMethodDef methods[] = {
      "cone_host(geom, r_b, e_b, a_b, nr, ne, na) -> host values of the trace | None"},
     {"build_cone", (PyCFunction)(void (*)(void))sphrt_fast::construct_build_cone, METH_FASTCALL,
      "build_cone(geom, r_b, e_b, a_b, nr, ne, na, perm, n_cols, csr_address) -> CSR | None"},
+    {"build_rays", (PyCFunction)(void (*)(void))sphrt_fast::construct_build_rays, METH_FASTCALL,
+     "build_rays(xs, rays, r_b, e_b, a_b, nr, ne, na, n_cols, csr_address) -> CSR | None"},
     {nullptr, nullptr, 0, nullptr},
 };
 

@@ -1132,8 +1132,15 @@ class Operator:
         if tiles is None and len(shape) in (2, 3) and shape[-1] > _WEDGE:   # _trace_order
             perm = _wedge_order(shape[-2], shape[-1])                       # (ConeCirc views)
         c = _lib.CSR()
-        res = fc.build_cone(self.geom, g.r_b, g.e_b, g.a_b, g.shape.r, g.shape.e, g.shape.a, perm,
-                            tiles, math.prod(g.shape[-3:]), ctypes.addressof(c))
+        if _ConeRays.of(self.geom) is not None:
+            res = fc.build_cone(self.geom, g.r_b, g.e_b, g.a_b, g.shape.r, g.shape.e, g.shape.a,
+                                perm, tiles, math.prod(g.shape[-3:]), ctypes.addressof(c))
+        else:   # ParallelGeom, ViewGeom, ...: geometry order, the host rays in the one copy
+            xs, rays = self.geom.ray_starts, self.geom.rays
+            if not (isinstance(xs, tr.Tensor) and isinstance(rays, tr.Tensor)):
+                return False
+            res = fc.build_rays(xs, rays, g.r_b, g.e_b, g.a_b, g.shape.r, g.shape.e, g.shape.a,
+                                math.prod(g.shape[-3:]), ctypes.addressof(c))
         if res is None:
             return False
         (row_ptr, vox, len32, row_ray, empty_ray, blocks, loc, tab, runs, ray_id, bound_ptr, slen,

@@ -1,5 +1,6 @@
-"""The native Operator construction (csrc/construct.cpp, _sphrt_fast.build_cone) against the
-Python construction sequence it replaces for cone-beam detectors (raytracer.Operator._trace_on).
+"""The native Operator construction (csrc/construct.cpp, _sphrt_fast.build_cone for cone-beam
+detectors, build_rays for any other geometry) against the Python construction sequence it
+replaces (raytracer.Operator._trace_on).
 
 CPU: the host values the trace reads — detector frames and pixel coordinates (_ConeRays.of), ray
 starts and their start voxels (_RayBatch.host_starts), the plan's trigonometric tables (_Plan) —
@@ -14,7 +15,7 @@ import pytest
 import torch
 
 from sph_raytracer_amd import (ConeCircGeom, ConeRectGeom, Operator, ParallelGeom, SphericalGrid,
-                               _lib)
+                               ViewGeom, _lib)
 from sph_raytracer_amd import raytracer as R
 
 
@@ -131,7 +132,32 @@ GPU_CASES = {
     # view tiles (9, 1): an odd view count and an odd detector width
     'odd_tiles': lambda: (SphericalGrid(shape=(24, 20, 28)), _orbit('rect', 9, (17, 41))),
     'few_views': lambda: (SphericalGrid(shape=(24, 20, 28)), _orbit('circ', 7, (20, 30))),
+    # build_rays: any other geometry from its host starts and directions (geometry order)
+    'parallel_orbit': lambda: (SphericalGrid(shape=(40, 30, 36)), _parallel_orbit(6, (32, 24))),
+    'parallel_single': lambda: (SphericalGrid(shape=(20, 18, 22)),
+                                ParallelGeom((40, 30), pos=(2, 1.5, 0.4), size=(1.5, 1.2))),
+    'viewgeom_rays': lambda: (SphericalGrid(shape=(30, 24, 40)), _random_viewgeom(3, (24, 33))),
+    'parallel_dynamic': lambda: (SphericalGrid(shape=(5, 16, 18, 20)), _parallel_orbit(5, (20, 16))),
 }
+
+
+def _parallel_orbit(n_views, det):
+    th = torch.linspace(0, 2 * torch.pi, n_views + 1)[:n_views]
+    return sum(ParallelGeom(det, pos=(3 * torch.cos(t), 3 * torch.sin(t), 0.3), size=(2, 1.6))
+               for t in th)
+
+
+def _random_viewgeom(n_views, det):
+    """Arbitrary ViewGeoms: per-pixel starts on a sphere of radius 2.5 and directions towards
+    jittered points of the unit ball."""
+    g = torch.Generator().manual_seed(11)
+    views = []
+    for _ in range(n_views):
+        d = torch.randn(det + (3,), generator=g, dtype=torch.float64)
+        xs = 2.5 * d / torch.linalg.norm(d, dim=-1, keepdim=True)
+        aim = 0.8 * torch.rand(det + (3,), generator=g, dtype=torch.float64) - 0.4
+        views.append(ViewGeom(xs, aim - xs))
+    return sum(views)
 
 
 @pytest.mark.gpu
@@ -193,7 +219,8 @@ def test_native_construction_matches_python(gpu, monkeypatch, name):
 
 @pytest.mark.gpu
 def test_native_construction_is_the_default(gpu, monkeypatch):
-    """Cone detectors at float64 construct natively unless a construction switch is set."""
+    """float64 traces construct natively unless a construction switch is set: cone detectors
+    (build_cone) and every other geometry (build_rays); the reference-mode trace does not."""
     monkeypatch.delenv('SPHRT_CONSTRUCT', raising=False)
     grid = SphericalGrid(shape=(10, 12, 14))
     geom = _orbit('rect', 3, (8, 9))
@@ -203,8 +230,10 @@ def test_native_construction_is_the_default(gpu, monkeypatch):
     monkeypatch.delenv('SPHRT_TRACE')
     assert not isinstance(Operator(grid, geom, device=gpu, ftype=torch.float32)._batch,
                           R._NativeBatch)
-    assert not isinstance(Operator(grid, ParallelGeom((4, 4), pos=(3, 0, 0)), device=gpu)._batch,
-                          R._NativeBatch)
+    assert isinstance(Operator(grid, ParallelGeom((4, 4), pos=(3, 0, 0)), device=gpu)._batch,
+                      R._NativeBatch)
+    xs = torch.tensor([[2.0, 0.1, 0.2], [0.0, -2.0, 0.3]], dtype=torch.float64)
+    assert isinstance(Operator(grid, ViewGeom(xs, -xs), device=gpu)._batch, R._NativeBatch)
 
 
 @pytest.mark.gpu
