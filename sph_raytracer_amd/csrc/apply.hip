@@ -1008,8 +1008,8 @@ template <typename T>
 constexpr int kGranLanes = (int)sizeof(T) / 4;        // 16-byte DMA lanes per granule
 // Early rounds cover kGranEarly chunks of 256 table entries whatever the workgroup size (THR
 // threads: a round moves THR / G granules).
-template <typename T, int THR = kThreads>
-constexpr int kEarlyRounds = kGranEarly * (256 / THR) * kGranLanes<T>;
+template <typename T, int THR = kThreads, int GE = kGranEarly>
+constexpr int kEarlyRounds = GE * (256 / THR) * kGranLanes<T>;
 
 template <typename T, int THR = kThreads>
 __device__ __forceinline__ int gran_entry0(int r, int w) {    // first entry of round r (uniform)
@@ -1070,13 +1070,13 @@ __device__ __forceinline__ void stage_granules_late(const T* __restrict__ rho,
 // (large tables) are fetched here.  When the volume's voxel count is not a multiple of 4 its
 // last granule is partial: only the table's last entry can be, it is skipped by the DMA (no read
 // past the volume) and copied lane by lane at the end.  Writes the zero granule.
-template <typename T, typename TabT, int THR = kThreads>
+template <typename T, typename TabT, int THR = kThreads, int GE = kGranEarly>
 __device__ __forceinline__ void stage_granules(const T* __restrict__ rho,
-                                               const int32_t (&ti)[kEarlyRounds<T, THR>],
+                                               const int32_t (&ti)[kEarlyRounds<T, THR, GE>],
                                                const TabT* __restrict__ tab_b, int n_tab,
                                                int32_t g_full, int64_t n_cols, T* dens) {
     constexpr int G = kGranLanes<T>;
-    constexpr int R = kEarlyRounds<T, THR>;
+    constexpr int R = kEarlyRounds<T, THR, GE>;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < 4) dens[threadIdx.x] = (T)0;
@@ -1100,12 +1100,12 @@ __device__ __forceinline__ void stage_granules(const T* __restrict__ rho,
 // follow the chunk's loads and waits for the chunk alone; the DMA round trip then overlaps the
 // chunk's arrival instead of following it.  Needs whole granules (columns % 4 == 0: no partial
 // tail granule) and an LDS image of at least kGranEarly * 256 granules.
-template <typename T, int THR = kThreads>
+template <typename T, int THR = kThreads, int GE = kGranEarly>
 __device__ __forceinline__ void stage_granules_early(const T* __restrict__ rho,
-                                                     const int32_t (&ti)[kEarlyRounds<T, THR>],
+                                                     const int32_t (&ti)[kEarlyRounds<T, THR, GE>],
                                                      int n_tab, T* dens) {
     constexpr int G = kGranLanes<T>;
-    constexpr int R = kEarlyRounds<T, THR>;
+    constexpr int R = kEarlyRounds<T, THR, GE>;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < 4) dens[threadIdx.x] = (T)0;
@@ -1288,7 +1288,8 @@ constexpr int kHalfTab = kGranEarly * kThreads;   // = the early DMA rounds' ent
 constexpr int kOutStage = 2048;                   // dense output range staged in LDS (elements)
 
 template <typename T, typename L, int MODE, typename TabT = int32_t, bool EDMA = false,
-          int P = kPer, bool RUNS = false, bool HALF = false, bool DENSE = false>
+          int P = kPer, bool RUNS = false, bool HALF = false, bool DENSE = false,
+          int GE = kGranEarly>
 __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_kernel(
     const int64_t* __restrict__ blocks, const int32_t* __restrict__ vox,
     const uint16_t* __restrict__ loc, const TabT* __restrict__ tab, const L* __restrict__ len,
@@ -1299,6 +1300,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     static_assert(!RUNS || MODE == kFwdTable, "run records serve the table mode");
     static_assert(!HALF || (MODE == kFwdTable && EDMA && P == kPer && kPass / P == kThreads),
                   "half tables: table mode, early DMA, 256-thread workgroups");
+    static_assert(!HALF || GE == kGranEarly, "half tables: kHalfTab is the early rounds' entries");
     __shared__ FwdShared sh;
     extern __shared__ __attribute__((aligned(16))) unsigned char fwd_dyn_lds[];
     T* dens = reinterpret_cast<T*>(fwd_dyn_lds);   // 4 * tab_stride entries (table mode)
@@ -1321,11 +1323,11 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     // table chunks beyond the stride read the next workgroup's entries (tab is padded by
     // kGranEarly*kThreads entries); they are never staged (j >= n_tab)
     const TabT* tab_b = tab + blk * tab_stride;
-    int32_t ti[kEarlyRounds<T, THR>];
+    int32_t ti[kEarlyRounds<T, THR, GE>];
     if (local) {
         const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
-        for (int r = 0; r < kEarlyRounds<T, THR>; ++r)
+        for (int r = 0; r < kEarlyRounds<T, THR, GE>; ++r)
             ti[r] = (int32_t)tab_b[gran_entry0<T, THR>(r, w) + (tid & 63) / kGranLanes<T>];
     }
     // the run record goes out with the table entries, before the chunk (the early-DMA wait below
@@ -1366,7 +1368,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     // output line is then written once (zeros and values together).  Larger ranges, and the
     // fallback launch, zero the range in global memory first.
     const bool ostaged = MODE == kFwdTable && dense && m[1] - m[0] <= kOutStage;
-    T* ost = dens + ((HALF ? kHalfTab : EDMA ? imax64(tab_stride, kGranEarly * kThreads)
+    T* ost = dens + ((HALF ? kHalfTab : EDMA ? imax64(tab_stride, GE * kThreads)
                                            : tab_stride) + 1) * 4;
     if (ostaged)
         for (int j = tid; j < (int)(m[1] - m[0]); j += THR) ost[j] = (T)0;
@@ -1426,9 +1428,9 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
         return;
     }
     const int32_t g_full = (int32_t)imin64(n_cols >> 2, INT32_MAX);   // whole granules
-    if (local && EDMA) stage_granules_early<T, THR>(density, ti, (int)n_tab, dens);
+    if (local && EDMA) stage_granules_early<T, THR, GE>(density, ti, (int)n_tab, dens);
     else if (local)
-        stage_granules<T, TabT, THR>(density, ti, tab_b, (int)n_tab, g_full, n_cols, dens);
+        stage_granules<T, TabT, THR, GE>(density, ti, tab_b, (int)n_tab, g_full, n_cols, dens);
     // pass-relative segment window [lo, hi) of this workgroup (32-bit lane arithmetic)
     auto window = [&](int64_t base, int& lo, int& hi) {
         lo = (int)imax64(s0 - base, -1);
@@ -1441,7 +1443,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
         // Loads complete in issue order: the chunk is in once at most the empty-list load and the
         // early DMAs issued after it are outstanding.  Said explicitly: the compiler's model
         // treats LDS-DMA as another event type and would wait for every DMA (vmcnt(0)).
-        constexpr int after = kEmptyLoads + kEarlyRounds<T, THR>;
+        constexpr int after = kEmptyLoads + kEarlyRounds<T, THR, GE>;
         static_assert(after < 16, "vmcnt field");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt((after & 15) | (7 << 4) | (15 << 8));
@@ -1453,7 +1455,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
         hmask = window_chunk<L, local, P>(raw, o, lo, hi, v, l);
     }
     if (local && EDMA && !HALF)   // rounds past the early ones (tables of more than 768 granules)
-        stage_granules_late<T, TabT, THR>(density, tab_b, kEarlyRounds<T, THR>, (int)n_tab, g_full,
+        stage_granules_late<T, TabT, THR>(density, tab_b, kEarlyRounds<T, THR, GE>, (int)n_tab, g_full,
                                           dens);
     if (dense && !ostaged) {      // (uniform) zeros before any close of this workgroup
         zero_range();
@@ -2134,27 +2136,37 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
         const bool half = sizeof(T) == 8 && P == kPer && edma &&
                           (size_t)(c->tab_stride + 1) * 32 > 40 * 1024 &&
                           c->tab_stride <= 2 * kHalfTab && half_tables_on();
+        // early DMA rounds: as many 256-entry chunks as the largest table needs (at most
+        // kGranEarly), so neither the LDS image nor the unconditional early DMAs exceed the
+        // tables (C4's time-paired adjoint: 448-entry tables, 3 -> 2 chunks)
+        const int ge = c->tab_stride <= kThreads ? 1 : c->tab_stride <= 2 * kThreads ? 2 : 3;
         size_t lds = (size_t)((half ? kHalfTab
-                               : edma ? imax64(c->tab_stride, kGranEarly * kThreads)
+                               : edma ? imax64(c->tab_stride, (int64_t)ge * kThreads)
                                       : c->tab_stride) + 1) * 4 * sizeof(T);   // + zero granule
         if (dense) lds += (size_t)kOutStage * sizeof(T);       // the staged output range
-#define FWD_TABLE(TabT, E, R, H, D)                                                         \
-        FWD_LAUNCH((forward_kernel<T, L, kFwdTable, TabT, E, P, R, H, D>), grid, block, lds, st, \
-                   FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
-#define FWD_TABLE_R(TabT, E, H)                                                             \
+#define FWD_TABLE(TabT, E, R, H, D, G)                                                      \
+        FWD_LAUNCH((forward_kernel<T, L, kFwdTable, TabT, E, P, R, H, D, G>), grid, block, lds, \
+                   st, FWD_ARGS(TabT, td, tcs, table_cols(c)), 0, c->runs)
+#define FWD_TABLE_R(TabT, E, H, G)                                                          \
         do {                                                                                      \
-            if (dense) FWD_TABLE(TabT, E, false, H, true);                                  \
-            else if (c->runs) FWD_TABLE(TabT, E, true, H, false);                           \
-            else FWD_TABLE(TabT, E, false, H, false);                                       \
+            if (dense) FWD_TABLE(TabT, E, false, H, true, G);                               \
+            else if (c->runs) FWD_TABLE(TabT, E, true, H, false, G);                        \
+            else FWD_TABLE(TabT, E, false, H, false, G);                                    \
         } while (0)
 #define FWD_TABLE_E(TabT)                                                                   \
         do {                                                                                      \
             if (half) {                                                                           \
-                if constexpr (sizeof(T) == 8 && P == kPer) { FWD_TABLE_R(TabT, true, true); } \
+                if constexpr (sizeof(T) == 8 && P == kPer) {                                      \
+                    FWD_TABLE_R(TabT, true, true, kGranEarly);                                    \
+                }                                                                                 \
+            } else if (edma && ge == 1) {                                                         \
+                FWD_TABLE_R(TabT, true, false, 1);                                                \
+            } else if (edma && ge == 2) {                                                         \
+                FWD_TABLE_R(TabT, true, false, 2);                                                \
             } else if (edma) {                                                                    \
-                FWD_TABLE_R(TabT, true, false);                                             \
+                FWD_TABLE_R(TabT, true, false, kGranEarly);                                       \
             } else {                                                                              \
-                FWD_TABLE_R(TabT, false, false);                                            \
+                FWD_TABLE_R(TabT, false, false, kGranEarly);                                      \
             }                                                                                     \
         } while (0)
         if (c->tab_bytes == 2) {

@@ -1458,9 +1458,11 @@ class Operator:
             # float64 half tables (apply.hip kHalfTab = 768 granules per phase)
             half = (es == 8 and edma == 'true' and (c.tab_stride + 1) * 32 > 40 * 1024
                     and c.tab_stride <= 1536 and os.environ.get('SPHRT_FWD_HALF', '1') != '0')
+            # early DMA rounds: 256-entry chunks of the largest table (apply.hip launch_forward)
+            ge = 3 if half or edma == 'false' else min(3, max(1, -(-c.tab_stride // 256)))
             return (f'forward_kernel<{t}, 0, {tabt}, {edma}, 8, {runs}, '
-                    f'{"true" if half else "false"}, {dense}>')
-        return f'forward_kernel<{t}, {2 if div else 1}, int, false, 8, false, false, {dense}>'
+                    f'{"true" if half else "false"}, {dense}, {ge}>')
+        return f'forward_kernel<{t}, {2 if div else 1}, int, false, 8, false, false, {dense}, 3>'
 
     def _apply_forward(self, density):
         with tr.cuda.device(self._cdev):      # launches and allocations on the operator's GPU

@@ -452,7 +452,7 @@ def test_half_tables_float64(gpu, monkeypatch):
     gen = tr.Generator().manual_seed(5)
     x = tr.rand((2,) + tuple(grid.shape), dtype=tr.float64, generator=gen)
     xg = x.to(gpu)
-    assert op._forward_kernel_name(xg[0]).endswith('true, true, false>')   # (half, not dense)
+    assert op._forward_kernel_name(xg[0]).endswith('true, true, false, 3>')   # (half, not dense)
     y = op(xg[0])
     rp, vx, ln = (t.cpu().numpy() for t in op.segments())
     nv = math.prod(grid.shape)
