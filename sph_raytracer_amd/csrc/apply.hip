@@ -1285,7 +1285,11 @@ using AccumOf = typename std::conditional<sizeof(T) == 4, float, double>::type;
 // Every segment reads its density in the phase that holds its granule (the other phase reads
 // the zero granule) and keeps that value: the sums are unchanged, bit for bit.
 constexpr int kHalfTab = kGranEarly * kThreads;   // = the early DMA rounds' entries (768)
-constexpr int kOutStage = 2048;                   // dense output range staged in LDS (elements)
+// dense output range staged in LDS (elements).  C4's time-paired adjoint (ranges of 1144 on
+// average, p99 2623) with 2-chunk early DMA: 1024 / 1536 / 2048 / 2560 / 4096 / 6144 outputs
+// measured 28.0 / 26.8 / 25.4 / 25.0 / 28.5 / 31.5 us (workgroups per CU against ranges staged;
+// profiles/r06_ostage_ab.jsonl, r06_adj_lds_ab.jsonl, r06_o2560_ab.jsonl)
+constexpr int kOutStage = 2560;
 
 template <typename T, typename L, int MODE, typename TabT = int32_t, bool EDMA = false,
           int P = kPer, bool RUNS = false, bool HALF = false, bool DENSE = false,

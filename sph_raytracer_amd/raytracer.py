@@ -1446,7 +1446,7 @@ class Operator:
         es = d.element_size()
         dense = 'true' if c.order & 4 else 'false'     # (dense output ranges, sphrt.h order)
         aligned = d.data_ptr() % (4 * es) == 0 and (n_chan == 1 or d[0].numel() % 4 == 0)
-        extra = 2048 * es if c.order & 4 else 0          # (apply.hip kOutStage)
+        extra = 2560 * es if c.order & 4 else 0          # (apply.hip kOutStage)
         table = (c.loc and div == 0 and 0 < c.tab_stride
                  and (max(c.tab_stride, 768) + 1) * 4 * es + extra <= 64 * 1024
                  and (c.stage_shape[0] > 0 or aligned))
