@@ -25,7 +25,7 @@ import weakref
 import torch as tr
 
 from . import _lib
-from .geometry import ConeRectGeom, ViewGeom, ViewGeomCollection
+from .geometry import ConeCircGeom, ConeRectGeom, ViewGeom, ViewGeomCollection
 
 DEVICE = 'cpu'
 PDEVICE = 'cpu'
@@ -1132,7 +1132,9 @@ class Operator:
         if tiles is None and len(shape) in (2, 3) and shape[-1] > _WEDGE:   # _trace_order
             perm = _wedge_order(shape[-2], shape[-1])                       # (ConeCirc views)
         c = _lib.CSR()
-        if _ConeRays.of(self.geom) is not None:
+        geoms = getattr(self.geom, 'geoms', [self.geom])
+        if all(type(v) in (ConeRectGeom, ConeCircGeom) for v in geoms):   # (type checks only:
+            # _ConeRays.of would build the cone spec in Python, the work build_cone does in C++)
             res = fc.build_cone(self.geom, g.r_b, g.e_b, g.a_b, g.shape.r, g.shape.e, g.shape.a,
                                 perm, tiles, math.prod(g.shape[-3:]), ctypes.addressof(c))
         else:   # ParallelGeom, ViewGeom, ...: geometry order, the host rays in the one copy
