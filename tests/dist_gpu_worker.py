@@ -73,6 +73,8 @@ def main():
     xc = tr.stack([x, 2 * x, x * x])
     res['fwd_mc'] = rel(sop.forward_full(xc), single(xc))
     res['T'] = rel(sop.T(y), single.T(y))
+    # the sharded results for the parent's oracle comparison (rank 0; every rank holds them)
+    sharded = {'x': x.cpu(), 'y': y.cpu(), 'fwd': sop.forward_full(x).cpu(), 'T': sop.T(y).cpu()}
 
     # dynamic grid: view i <-> time slice i; forward, autograd gradient, adjoint
     dgrid, dgeom = orbit(6, (16, 12), (6, 12, 10, 14), 'circ')
@@ -130,6 +132,7 @@ def main():
     if backend == 'nccl' and not (seen['all_gather_into_tensor'] and seen['all_reduce_cuda']):
         bad['rccl_path_not_taken'] = dict(seen)
     if rank == 0 and os.environ.get('SPHRT_DIST_OUT'):
+        tr.save(sharded, os.environ['SPHRT_DIST_OUT'] + '.pt')
         with open(os.environ['SPHRT_DIST_OUT'], 'w') as fh:
             json.dump(res, fh)
     dist.barrier()

@@ -8,6 +8,10 @@ adjoint (all_reduce) within 1e-12, the dynamic forward, autograd gradient and al
 adjoint within 1e-12, and the data-parallel retrieval (distributed.gd: the autograd-free loop
 with one all_reduce of the gradient per iteration) within 1e-12 of the single-GPU loop's
 coefficients and losses after 25 iterations.  The tolerances are checked inside every rank.
+The sharded static forward (all-gathered) and adjoint (all-reduced) are also checked here against
+the C oracle's trace of every ray (line integrals within 1e-10 relative, the adjoint within
+1e-10 of its largest magnitude): oracle parity of the multi-rank path, not only agreement with
+one GPU.
 """
 import json
 import os
@@ -52,6 +56,37 @@ def test_sharded_hip_operator_matches_single_gpu(world, backend, gpu, tmp_path):
     res = json.loads(out.read_text())
     print(json.dumps(res, indent=1))
     assert res['gd_drop'] < 0.05
+    _check_against_oracle(str(out) + '.pt')
     if backend == 'nccl':     # the RCCL branches ran (device all-gather and all-reduce)
         assert res['collectives']['all_gather_into_tensor'] > 0, res['collectives']
         assert res['collectives']['all_reduce_cuda'] > 0, res['collectives']
+
+
+def _check_against_oracle(path):
+    """The worker's static case (7-view ConeRect (32, 40) orbit over a (30, 28, 32) grid):
+    sharded forward and adjoint against the C oracle's segments of every ray."""
+    import numpy as np
+    import torch as tr
+    sys.path.insert(0, os.path.dirname(HERE))
+    from dist_gpu_worker import orbit
+    from oracle import oracle
+    from sph_raytracer_amd.raytracer import find_starts
+    got = tr.load(path, weights_only=True)
+    grid, geom = orbit(7, (32, 40), (30, 28, 32), 'rect')
+    oracle.use_mkl_sqrt(False)
+    oracle.load()
+    g = oracle.Grid.from_boundaries(grid.r_b.numpy(), grid.e_b.numpy(), grid.a_b.numpy())
+    rays = geom.rays.numpy().reshape(-1, 3)
+    xs = np.ascontiguousarray(np.broadcast_to(geom.ray_starts.numpy(), geom.rays.shape)
+                              .reshape(-1, 3))
+    st = find_starts(grid, tr.from_numpy(xs)).numpy()
+    ptr, vox, seg = oracle.trace_segments(g, xs, np.ascontiguousarray(rays), st)
+    x = got['x'].numpy().reshape(-1)
+    y = got['y'].numpy().reshape(-1)
+    want = np.array([float(np.sum(x[vox[a:b]] * seg[a:b])) for a, b in zip(ptr[:-1], ptr[1:])])
+    fwd = got['fwd'].numpy().reshape(-1)
+    assert np.max(np.abs(fwd - want)) <= 1e-10 * np.max(np.abs(want))
+    adj = np.zeros(x.size)
+    np.add.at(adj, vox, seg * np.repeat(y, np.diff(ptr)))
+    T = got['T'].numpy().reshape(-1)
+    assert np.max(np.abs(T - adj)) <= 1e-10 * np.max(np.abs(adj))
