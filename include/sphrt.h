@@ -207,7 +207,8 @@ int sphrt_rays_cone_tiled(int64_t n_views, int64_t h, int64_t w, int circ, const
  *   row_ray — ray id of every non-empty row, in order,
  *   empty_ray — the rays without segments, ascending (allocate n_rays + 1 entries),
  *   blocks  — n_blocks x 6 int64 {empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab}: block b
- *             owns the whole rows starting in segments [b*1792, (b+1)*1792) and zeroes the empty
+ *             owns the whole rows starting in segments [b*1792, (b+1)*1792) (b*1984 with dense
+ *             output ranges: sphrt_csr_index_dense) and zeroes the empty
  *             rays empty_ray[empty_lo .. empty_hi),
  *   tab     — (optional) per block b, its n_tab distinct 4-voxel granules (voxel >> 2) ascending
  *             at tab[b*tab_stride ..) (n_blocks * tab_stride entries),
@@ -288,6 +289,14 @@ size_t sphrt_csr_index_workspace_bytes(int64_t n_rays);
 int sphrt_csr_index(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_t *row_ray,
                     int32_t *empty_ray, int64_t *blocks, int64_t n_blocks, const int32_t *ray_ids,
                     void *workspace, void *stream);
+/* The same index for a CSR that will take dense output ranges (order bit 2: rows in output order,
+ * one output per row or empty row — the time-paired transposed adjoint): block b owns the rows
+ * starting in segments [b*1984, (b+1)*1984), n_blocks = sphrt_csr_blocks_dense(n_segments).  The
+ * forward reads a CSR with order bit 2 set by these blocks, so its index must come from here. */
+int64_t sphrt_csr_blocks_dense(int64_t n_segments);
+int sphrt_csr_index_dense(const int64_t *row_ptr, int64_t n_rays, int32_t *vox, int32_t *row_ray,
+                          int32_t *empty_ray, int64_t *blocks, int64_t n_blocks,
+                          const int32_t *ray_ids, void *workspace, void *stream);
 /* Granule tables in two passes.  _count sets n_tab in blocks (-1: no table) and writes two
  * device int64 to stats: {blocks without a table, largest n_tab}; the caller copies the first to
  * csr->n_fallback, picks tab_stride >= the second (csr->tab_stride; tab holds n_blocks *

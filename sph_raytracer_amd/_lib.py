@@ -89,6 +89,9 @@ _SIGNATURES = [
     ('sphrt_csr_blocks', c_i64, [c_i64]),
     ('sphrt_csr_index_workspace_bytes', ctypes.c_size_t, [c_i64]),
     ('sphrt_csr_index', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    ('sphrt_csr_blocks_dense', c_i64, [c_i64]),
+    ('sphrt_csr_index_dense', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+                                      c_vp]),
     ('sphrt_csr_index_staged', c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                                        c_vp]),
     ('sphrt_csr_runs', c_int, [ctypes.POINTER(CSR), c_vp, c_vp, c_vp]),

@@ -40,6 +40,14 @@ constexpr int kPer = 8;                         // segments per thread per pass
 constexpr int kPass = kThreads * kPer;          // 2048 segments per pass
 constexpr int64_t kSegPerBlock = 1792;          // row starts per workgroup (leaves room
                                                 // for the last row's overhang inside one pass)
+// CSRs with dense output ranges (sphrt_csr.order bit 2: the time-paired transposed adjoint, rows
+// of ~2 segments, one output per row or empty row) take blocks of 1984 row starts.  Blocks of
+// 1920 for every CSR measured C4 adjoint kernel 24.9 -> 23.6 us but the forwards slower (C2 5.86
+// -> 6.21 us, C5 34.1 -> 36.3; 1536 / 1664 slower everywhere; profiles/r06_spb_ab.jsonl); for the
+// dense CSR alone, C4 adjoint 24.8-24.9 (1792) / 23.8-24.0 (1920) / 23.6-23.7 (1984) / 24.0-24.2
+// us (2016), the rest unchanged (r06_dspb_ab.jsonl).  Indexed with sphrt_csr_index_dense /
+// sphrt_csr_blocks_dense.
+constexpr int64_t kDenseSegPerBlock = 1984;
 constexpr int kBlockFields = 6;                 // empty_lo, empty_hi, seg_lo, seg_hi, row_lo, n_tab
 constexpr int kLocalMax = 4096;                 // segments per workgroup with a granule table
 constexpr int kMaxGran = 2046;                  // granules per table (sphrt_csr_local): loc's
@@ -82,7 +90,8 @@ __global__ __launch_bounds__(256) void row_list_kernel(const int64_t* row_ptr,
 
 __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
                                                          const int64_t* row_pre, int64_t n,
-                                                         int64_t nblocks, int64_t* blocks) {
+                                                         int64_t nblocks, int64_t spb,
+                                                         int64_t* blocks) {
     const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (b >= nblocks) return;
     auto first_at_or_after = [&](int64_t target) {   // first ray r < n with row_ptr[r] >= target
@@ -94,8 +103,8 @@ __global__ __launch_bounds__(256) void block_meta_kernel(const int64_t* row_ptr,
         }
         return lo;
     };
-    const int64_t lo = first_at_or_after(b * kSegPerBlock);
-    const int64_t hi = (b + 1 == nblocks) ? n : first_at_or_after((b + 1) * kSegPerBlock);
+    const int64_t lo = first_at_or_after(b * spb);
+    const int64_t hi = (b + 1 == nblocks) ? n : first_at_or_after((b + 1) * spb);
     int64_t* m = blocks + kBlockFields * b;
     // this block's share of the empty-ray list (split evenly, independent of the segments)
     const int64_t n_empty = n - row_pre[n];
@@ -1320,7 +1329,7 @@ __global__ __launch_bounds__(kPass / P, (fwd_min_blocks<T, P>())) void forward_k
     // arrives: the first pass (rows of block b start in [b*kSegPerBlock, (b+1)*kSegPerBlock),
     // so its first pass is [b*kSegPerBlock, +kPass)) and the granule table (fixed stride).
     const int64_t blk = block_of(xcd_chunk);
-    const int64_t base0 = blk * kSegPerBlock;
+    const int64_t base0 = blk * (DENSE ? kDenseSegPerBlock : kSegPerBlock);
     const int64_t last_chunk = imax64((n_seg + P - 1) / P, 1) - 1;   // clamp for loads
     RawChunk<L, local, P> raw;
     if (!EDMA) raw_load<L, local, P>(vox, loc, len, imin64(base0 + o, last_chunk * P), raw);
@@ -1739,6 +1748,10 @@ extern "C" int64_t sphrt_csr_blocks(int64_t n_segments) {
     return n_segments < 0 ? -1 : n_segments / kSegPerBlock + 1;
 }
 
+extern "C" int64_t sphrt_csr_blocks_dense(int64_t n_segments) {
+    return n_segments < 0 ? -1 : n_segments / kDenseSegPerBlock + 1;
+}
+
 extern "C" size_t sphrt_csr_index_workspace_bytes(int64_t n_rays) {
     // nonempty flags (int32) | row prefix (int64, n+1) | scan workspace
     const size_t a = (((size_t)n_rays * 4 + 255) / 256) * 256;
@@ -1748,7 +1761,8 @@ extern "C" size_t sphrt_csr_index_workspace_bytes(int64_t n_rays) {
 
 static int csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* vox, int32_t* row_ray,
                      int32_t* empty_ray, int64_t* blocks, int64_t n_blocks,
-                     const int32_t* ray_ids, int32_t* nz_row, void* workspace, void* stream) {
+                     const int32_t* ray_ids, int32_t* nz_row, void* workspace, void* stream,
+                     int64_t spb = kSegPerBlock) {
     if (n_rays < 0 || n_blocks < 1) return fail("bad CSR index sizes");
     if (n_rays == 0) return 0;
     StreamGuard guard(stream);
@@ -1765,7 +1779,7 @@ static int csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* vox, int32
                        row_ray, empty_ray, nz_row);
     if (int e = check_launch("row_list")) return e;
     hipLaunchKernelGGL(block_meta_kernel, dim3((unsigned)((n_blocks + 255) / 256)), dim3(256), 0,
-                       st, row_ptr, pre, n_rays, n_blocks, blocks);
+                       st, row_ptr, pre, n_rays, n_blocks, spb, blocks);
     return check_launch("block_meta");
 }
 
@@ -1776,6 +1790,15 @@ extern "C" int sphrt_csr_index(const int64_t* row_ptr, int64_t n_rays, int32_t* 
     if (!vox && n_rays > 0) return fail("null vox");
     return csr_index(row_ptr, n_rays, vox, row_ray, empty_ray, blocks, n_blocks, ray_ids, nullptr,
                      workspace, stream);
+}
+
+extern "C" int sphrt_csr_index_dense(const int64_t* row_ptr, int64_t n_rays, int32_t* vox,
+                                     int32_t* row_ray, int32_t* empty_ray, int64_t* blocks,
+                                     int64_t n_blocks, const int32_t* ray_ids, void* workspace,
+                                     void* stream) {
+    if (!vox && n_rays > 0) return fail("null vox");
+    return csr_index(row_ptr, n_rays, vox, row_ray, empty_ray, blocks, n_blocks, ray_ids, nullptr,
+                     workspace, stream, kDenseSegPerBlock);
 }
 
 extern "C" int sphrt_csr_index_staged(const int64_t* row_ptr, int64_t n_rays, int32_t* row_ray,

@@ -1557,15 +1557,18 @@ class Operator:
         geom_cols = self._tcols_geom()
         if geom_cols:                    # columns: the rows' geometry rays instead of trace rows
             t_ray[:total] = csr['ray_id'].index_select(0, t_ray[:total])
-        nblocks = lib.sphrt_csr_blocks(total)
+        # (dense output ranges: the blocks of that layout, sphrt_csr_index_dense)
+        ranges = dense and rows is None
+        nblocks = (lib.sphrt_csr_blocks_dense if ranges else lib.sphrt_csr_blocks)(total)
         vox_list = tr.empty(n_vox, dtype=tr.int32, device=dev)
         empty_vox = tr.empty(n_vox + 1, dtype=tr.int32, device=dev)
         blocks = tr.empty(_lib.BLOCK_FIELDS * nblocks, dtype=tr.int64, device=dev)
         iws = tr.empty(lib.sphrt_csr_index_workspace_bytes(n_vox), dtype=tr.uint8, device=dev)
-        _lib.check(lib.sphrt_csr_index(_lib.ptr(col_ptr), n_vox, _lib.ptr(t_ray),
-                                       _lib.ptr(vox_list), _lib.ptr(empty_vox), _lib.ptr(blocks),
-                                       nblocks, _lib.ptr(rows.vperm) if rows is not None else None,
-                                       _lib.ptr(iws), stream),
+        index = lib.sphrt_csr_index_dense if ranges else lib.sphrt_csr_index
+        _lib.check(index(_lib.ptr(col_ptr), n_vox, _lib.ptr(t_ray), _lib.ptr(vox_list),
+                         _lib.ptr(empty_vox), _lib.ptr(blocks), nblocks,
+                         _lib.ptr(rows.vperm) if rows is not None else None, _lib.ptr(iws),
+                         stream),
                    'sphrt_csr_index(T)')
         t_len32 = tr.empty(t_len.shape, dtype=tr.float32, device=dev)   # (filled with the tables)
         c = _lib.CSR()
@@ -1582,7 +1585,7 @@ class Operator:
         _set_stage(c, shape3, _stage_brick(nblocks, 'SPHRT_BRICK_T', _BRICK_RAYS)
                    if shape3 else None)
         loc, tab, runs = _local_tables(lib, c, blocks, nblocks, total, dev, stream)
-        if dense and rows is None:
+        if ranges:
             _dense_ranges(c, blocks, vox_list, n_vox)
             runs = None
         return dict(desc=c, keep=(col_ptr, t_ray, t_len, t_len32, vox_list, empty_vox, blocks,
