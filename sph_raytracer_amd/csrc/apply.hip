@@ -2139,6 +2139,9 @@ static int launch_forward(const sphrt_csr* c, const L* len, const T* density, in
     if ((c->order & 4) && (n_chan != 1 || div > 0 || c->runs))
         return fail("dense output ranges need one channel, no time slices and no run records");
     const bool dense = (c->order & 4) != 0;        // (instantiations with DENSE)
+    // (dense output ranges read the blocks of sphrt_csr_index_dense: their count at least)
+    if (dense && c->n_blocks != c->n_segments / kDenseSegPerBlock + 1)
+        return fail("dense output ranges need the blocks of sphrt_csr_index_dense");
     const T* td = sm.on ? (const T*)c->stage : density;      // what the table kernel gathers
     const int64_t tcs = sm.on ? c->stage_cols : chan_stride;
     if (div > 0) {

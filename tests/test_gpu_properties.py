@@ -699,6 +699,39 @@ def test_dynamic_pairing_forward_and_adjoint(gpu):
     assert op._fastc is not None and tr.equal(op(x), fx)     # bound: the CPython fast path
 
 
+def test_dense_ranges_need_dense_blocks(gpu):
+    """The time-paired transposed CSR (dense output ranges, sphrt_csr.order bit 2) is indexed in
+    the blocks of sphrt_csr_index_dense (1984 row starts, apply.hip kDenseSegPerBlock); the
+    forward refuses a CSR that claims dense ranges with another block count instead of reading
+    the wrong first pass."""
+    from sph_raytracer_amd import ConeCircGeom, Operator, SphericalGrid, _lib
+    T = 6
+    grid = SphericalGrid(shape=(T, 20, 18, 24))
+    geom = sum(ConeCircGeom(shape=(30, 20), pos=(5 * tr.cos(th), 5 * tr.sin(th), 1), fov=(0, 45))
+               for th in tr.linspace(0, 2 * tr.pi, T))
+    op = Operator(grid, geom, dynamic=True, device=gpu)
+    x = tr.rand(grid.shape, dtype=tr.float64, device=gpu)
+    y = tr.rand(geom.shape, dtype=tr.float64, device=gpu)
+    g = op._apply_adjoint(y, tuple(x.shape), x.dtype, x.device)
+    n_chan, div, _ = op._layout(x.shape)
+    pt = op._paired(T, div)['transposed']['desc']
+    lib = _lib.load()
+    assert pt.order & 4 and pt.n_blocks == lib.sphrt_csr_blocks_dense(pt.n_segments)
+    bad = _lib.CSR.from_buffer_copy(pt)
+    bad.n_blocks = lib.sphrt_csr_blocks(pt.n_segments)
+    assert bad.n_blocks != pt.n_blocks
+    yt = y.reshape(-1).contiguous()
+    out = tr.empty(pt.n_rays, dtype=tr.float64, device=gpu)
+    rc = lib.sphrt_forward_f64(bad, _lib.ptr(yt), 1, yt.numel(), 0, _lib.ptr(out), pt.n_rays,
+                               _lib.stream_of(gpu))
+    with pytest.raises(RuntimeError, match='sphrt_csr_index_dense'):
+        _lib.check(rc, 'forward')
+    rc = lib.sphrt_forward_f64(pt, _lib.ptr(yt), 1, yt.numel(), 0, _lib.ptr(out), pt.n_rays,
+                               _lib.stream_of(gpu))
+    _lib.check(rc, 'forward')
+    assert tr.equal(out.reshape(g.shape), g)
+
+
 @pytest.mark.parametrize('grid_shape,n_views,det,order', [
     ((128, 128, 128), 6, (128, 128), 'runs'),     # density > 4 MB: runs of 64 blocks per XCD
     ((50, 50, 50), 80, (50, 100), 'dispatch'),    # > 1536 blocks, small density
