@@ -52,6 +52,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--config', default='c4')
     ap.add_argument('--reps', type=int, default=50)
+    ap.add_argument('--or-order', type=int, default=0,
+                    help='bits OR-ed into the adjoint CSR\'s order (block-order hints) before timing')
     args = ap.parse_args()
     import bench
     from sph_raytracer_amd import Operator, _lib
@@ -68,6 +70,7 @@ def main():
     n_chan, div, _ = op._layout(x.shape)
     tr_rec = op._paired(x.shape[0], div)['transposed'] if div else op._transposed()
     c = tr_rec['desc']
+    c.order |= args.or_order
     keep = tr_rec['keep']
     col_ptr, blocks = keep[0], keep[6]
     b = blocks.view(-1, 6)
